@@ -1,0 +1,242 @@
+// PyTorch bindings for the gfx950 kernels (module `generativeaiexamples_amd._C`).
+//
+// Thin shape/dtype checks, then a launch on the current HIP stream. No host
+// synchronisation and no allocation happens here, so every op can be captured
+// into a HIP graph by torch.cuda.graph().
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "gai_kernels.h"
+
+void gai_launch_error(const char* file, int line, const char* msg) {
+  throw std::runtime_error(std::string("gai kernel error at ") + file + ":" + std::to_string(line) + ": " + msg);
+}
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_i32(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kInt, name, " must be int32");
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+const void* opt_ptr(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+void rmsnorm(const Tensor& x, const Tensor& w, double eps, Tensor& out, const optional<Tensor>& residual_in,
+             const optional<Tensor>& residual_out) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(out, "out");
+  const int D = x.size(-1);
+  const int T = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && w.numel() == D, "rmsnorm: bad hidden size");
+  if (residual_in) check_bf16(*residual_in, "residual_in");
+  if (residual_out) check_bf16(*residual_out, "residual_out");
+  gai_rmsnorm(x.data_ptr(), opt_ptr(residual_in), residual_out ? residual_out->data_ptr() : nullptr, w.data_ptr(),
+              out.data_ptr(), T, D, (float)eps, cur_stream());
+}
+
+void layernorm(const Tensor& x, const Tensor& w, const optional<Tensor>& b, double eps, Tensor& out,
+               const optional<Tensor>& residual_in, const optional<Tensor>& residual_out) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(out, "out");
+  const int D = x.size(-1);
+  const int T = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && w.numel() == D, "layernorm: bad hidden size");
+  gai_layernorm(x.data_ptr(), opt_ptr(residual_in), residual_out ? residual_out->data_ptr() : nullptr, w.data_ptr(),
+                opt_ptr(b), out.data_ptr(), T, D, (float)eps, cur_stream());
+}
+
+void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, const Tensor& slots, Tensor& q_out,
+                   Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, bool rope) {
+  check_bf16(qkv, "qkv");
+  check_i32(pos, "positions");
+  check_f32(cos_sin, "cos_sin");
+  check_i32(slots, "slot_mapping");
+  check_bf16(q_out, "q_out");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_kv_write: qkv width mismatch");
+  TORCH_CHECK(k_cache.size(-2) == 16 && k_cache.size(-1) == D && v_cache.size(-1) == 16, "bad kv cache layout");
+  gai_rope_kv_write(qkv.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(),
+                    q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D, rope ? 1 : 0,
+                    cur_stream());
+}
+
+void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
+          int64_t epi, int64_t force) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_dev(C, "C");
+  const int K = A.size(-1);
+  const int M = A.numel() / K;
+  const int N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm: K mismatch");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm: C must be bf16 or fp32");
+  const int ldc = epi == 4 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm: C has wrong size");
+  if (bias) check_bf16(*bias, "bias");
+  if (R) {
+    check_bf16(*R, "residual");
+    TORCH_CHECK(R->numel() == (int64_t)M * N, "gemm: residual has wrong size");
+  }
+  gai_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr(bias), opt_ptr(R), M, N, K, ldc, (int)epi, f32 ? 1 : 0,
+           (int)force, cur_stream());
+}
+
+void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                  const Tensor& tiles, const Tensor& cu_q, const Tensor& ctx_lens, Tensor& out, int64_t Hq,
+                  int64_t Hkv, double scale, bool causal) {
+  check_bf16(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables");
+  check_i32(tiles, "tiles");
+  check_i32(cu_q, "cu_q");
+  check_i32(ctx_lens, "ctx_lens");
+  check_bf16(out, "out");
+  const int D = q.size(-1);
+  gai_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                   block_tables.size(1), tiles.data_ptr<int>(), tiles.numel() / 2, cu_q.data_ptr<int>(),
+                   ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, cur_stream());
+}
+
+void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                 const Tensor& ctx_lens, Tensor& out, Tensor& ws_o, Tensor& ws_ml, double scale, int64_t split_keys,
+                 int64_t max_splits) {
+  check_bf16(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables");
+  check_i32(ctx_lens, "ctx_lens");
+  check_bf16(out, "out");
+  check_f32(ws_o, "ws_o");
+  check_f32(ws_ml, "ws_ml");
+  const int B = q.size(0), Hq = q.size(1), D = q.size(2);
+  const int Hkv = k_cache.size(1);
+  TORCH_CHECK(ws_o.numel() >= (int64_t)max_splits * B * Hq * D, "attn_decode: ws_o too small");
+  TORCH_CHECK(ws_ml.numel() >= (int64_t)max_splits * B * Hq * 2, "attn_decode: ws_ml too small");
+  gai_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                  block_tables.size(1), ctx_lens.data_ptr<int>(), out.data_ptr(), ws_o.data_ptr<float>(),
+                  ws_ml.data_ptr<float>(), B, Hq, Hkv, D, (float)scale, split_keys, max_splits, cur_stream());
+}
+
+void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p, const Tensor& top_k,
+            const Tensor& seeds, int64_t step, Tensor& out) {
+  check_f32(logits, "logits");
+  check_f32(temperature, "temperature");
+  check_f32(top_p, "top_p");
+  check_i32(top_k, "top_k");
+  check_dev(seeds, "seeds");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
+  check_i32(out, "out");
+  const int B = logits.size(0), V = logits.size(1);
+  gai_sample(logits.data_ptr<float>(), B, V, logits.stride(0), temperature.data_ptr<float>(),
+             top_p.data_ptr<float>(), top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), step, out.data_ptr<int>(),
+             cur_stream());
+}
+
+void apply_penalties(Tensor& logits, const Tensor& tok_ids, const Tensor& tok_cnt, const Tensor& n,
+                     const Tensor& freq, const Tensor& pres, const Tensor& rep) {
+  check_f32(logits, "logits");
+  check_i32(tok_ids, "tok_ids");
+  check_i32(tok_cnt, "tok_cnt");
+  check_i32(n, "n");
+  gai_apply_penalties(logits.data_ptr<float>(), logits.size(0), logits.stride(0), tok_ids.data_ptr<int>(),
+                      tok_cnt.data_ptr<int>(), n.data_ptr<int>(), tok_ids.size(1), freq.data_ptr<float>(),
+                      pres.data_ptr<float>(), rep.data_ptr<float>(), cur_stream());
+}
+
+void sim_topk(const Tensor& Q, const Tensor& X, const Tensor& bias, int64_t n_rows, int64_t k, Tensor& ws_v,
+              Tensor& ws_i, int64_t nwg, int64_t rows_per_wg, Tensor& out_v, Tensor& out_i) {
+  check_bf16(Q, "Q");
+  check_bf16(X, "X");
+  check_f32(bias, "bias");
+  check_f32(ws_v, "ws_v");
+  check_i32(ws_i, "ws_i");
+  check_f32(out_v, "out_v");
+  check_dev(out_i, "out_i");
+  const int nq = Q.size(0), D = Q.size(1);
+  TORCH_CHECK(X.size(1) == D, "sim_topk: dim mismatch");
+  TORCH_CHECK(n_rows <= X.size(0) && n_rows <= bias.numel(), "sim_topk: n_rows exceeds storage");
+  TORCH_CHECK(rows_per_wg % 128 == 0, "sim_topk: rows_per_wg must be a multiple of 128");
+  const int cap = gai_topk_cap(k);
+  TORCH_CHECK(ws_v.numel() >= nwg * nq * cap && ws_i.numel() >= nwg * nq * cap, "sim_topk: workspace too small");
+  gai_sim_topk(Q.data_ptr(), X.data_ptr(), bias.data_ptr<float>(), nq, n_rows, D, k, ws_v.data_ptr<float>(),
+               ws_i.data_ptr<int>(), nwg, rows_per_wg, out_v.data_ptr<float>(), out_i.data_ptr<int64_t>(),
+               cur_stream());
+}
+
+void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart, int64_t vend) {
+  check_i32(ids, "ids");
+  check_bf16(table, "table");
+  check_bf16(out, "out");
+  const int D = table.size(1);
+  TORCH_CHECK(D % 8 == 0, "embedding: dim must be a multiple of 8");
+  gai_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), D, vstart, vend, cur_stream());
+}
+
+void pool(const Tensor& h, const Tensor& cu, Tensor& out, int64_t mode, bool normalize) {
+  check_bf16(h, "hidden");
+  check_i32(cu, "cu_seqlens");
+  check_f32(out, "out");
+  gai_pool(h.data_ptr(), cu.data_ptr<int>(), out.data_ptr<float>(), cu.numel() - 1, h.size(-1), mode,
+           normalize ? 1 : 0, cur_stream());
+}
+
+void silu_mul(const Tensor& x, Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  const int I = y.size(-1);
+  gai_silu_mul(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
+}
+
+void gelu(const Tensor& x, Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  const int I = y.size(-1);
+  gai_gelu(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels for generativeaiexamples_amd";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("layernorm", &layernorm);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("gemm", &gemm);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv) { return gai_attn_prefill_rows_per_tile(hq, hkv); });
+  m.def("attn_decode", &attn_decode);
+  m.def("sample", &sample);
+  m.def("apply_penalties", &apply_penalties);
+  m.def("sim_topk", &sim_topk);
+  m.def("topk_cap", [](int64_t k) { return gai_topk_cap(k); });
+  m.def("embedding", &embedding);
+  m.def("pool", &pool);
+  m.def("silu_mul", &silu_mul);
+  m.def("gelu", &gelu);
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,48 @@
+// Host-side launchers of the gfx950 kernels. Pointers are raw device pointers;
+// every launcher enqueues on `st` and never synchronises (graph-capture safe).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+void gai_launch_error(const char* file, int line, const char* msg);
+
+// norm.hip
+void gai_rmsnorm(const void* x, const void* residual_in, void* residual_out, const void* w, void* out, int T, int D,
+                 float eps, hipStream_t st);
+void gai_layernorm(const void* x, const void* residual_in, void* residual_out, const void* w, const void* b,
+                   void* out, int T, int D, float eps, hipStream_t st);
+
+// rope_kv.hip
+void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, const int* slots, void* q_out,
+                       void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, hipStream_t st);
+
+// gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu;
+//            force: 0 auto, 1 skinny, 2 tiled)
+void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+              int epi, int out_f32, int force, hipStream_t st);
+
+// attention.hip
+void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                      int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
+                      int Hq, int Hkv, int D, float scale, int causal, hipStream_t st);
+int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
+void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                     int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
+                     int Hkv, int D, float scale, int split_keys, int max_splits, hipStream_t st);
+
+// sampling.hip
+void gai_sample(const float* logits, int B, int V, long ld, const float* temperature, const float* top_p,
+                const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, hipStream_t st);
+void gai_apply_penalties(float* logits, int B, long ld, const int* tok_ids, const int* tok_cnt, const int* n,
+                         int max_n, const float* freq, const float* pres, const float* rep, hipStream_t st);
+
+// topk.hip
+int gai_topk_cap(int k);
+void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,
+                  int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st);
+
+// misc.hip
+void gai_embedding(const int* ids, const void* table, void* out, int T, int D, int vstart, int vend, hipStream_t st);
+void gai_pool(const void* h, const int* cu, float* out, int B, int D, int mode, int normalize, hipStream_t st);
+void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st);
+void gai_gelu(const void* x, void* y, int T, int I, hipStream_t st);

@@ -1,0 +1,439 @@
+// Paged flash attention for gfx950.
+//
+// KV cache layout (written by rope_kv.hip): K [num_blocks, Hkv, 16, D],
+// V^T [num_blocks, Hkv, D, 16] (16 tokens per page).
+//
+// attn_prefill: varlen, causal or bidirectional, GQA. Workgroup = 4 waves; each
+// wave owns 32 query rows of one q-head, the workgroup shares 64-key K / V^T tiles
+// in LDS (register-staged, issue-early / write-late, one barrier per tile, XOR
+// swizzled images). S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts a full query row
+// in one lane (swapped QK^T), so the online softmax is in-register; P^T is fed to
+// the P.V MFMA straight from the S accumulator (k-order permuted on the V side,
+// cdna_hip_programming §3 "accumulator tile as the next MFMA's operand"). exp2
+// domain, fp32 statistics. Used for LLM prefill (incl. chunked prefill over a
+// cached prefix) and for encoder self-attention (bidirectional, varlen).
+//
+// attn_decode: one query token per sequence, split-KV flash-decoding. Workgroup =
+// (split, kv head, sequence); the GQA group (<= 16 q heads) is the 16-wide MFMA
+// column, so K and V^T are read once per kv head with 16-B / 8-B loads straight to
+// VGPRs (memory-bound decode row of the glds-vs-register table); the 4 waves
+// combine through LDS, splits are merged by attn_decode_reduce.
+#include "gai_common.h"
+#include "gai_kernels.h"
+
+using namespace gai;
+
+namespace {
+
+constexpr int kBS = 16;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kNeg = -1e30f;
+
+// ----------------------------------------------------------------------------------------------
+// Prefill
+// ----------------------------------------------------------------------------------------------
+template <int D>
+struct PrefillCfg {
+  static constexpr int KT = 64;                  // keys per tile
+  static constexpr int KBYTES = KT * D * 2;      // K tile image
+  static constexpr int VBYTES = D * KT * 2;      // V^T tile image
+  static constexpr int BUF = KBYTES + VBYTES;
+  static constexpr int CH = D / 32;              // 16-B chunks per thread per operand
+  static constexpr int KU = D / 8;               // 16-B units per K row
+};
+
+// K image: row = key (D*2 bytes), unit u (16 B) stored at u ^ (key & (KU-1) & 15)
+template <int D>
+__device__ __forceinline__ int k_lds_off(int key, int u) {
+  constexpr int KU = D / 8;
+  constexpr int MASK = KU >= 16 ? 15 : KU - 1;
+  return key * D * 2 + ((u ^ (key & MASK)) << 4);
+}
+// V^T image: row = d (64 keys = 128 B), 8-B unit u (0..15) stored at u ^ ((d >> 1) & 15)
+__device__ __forceinline__ int v_lds_off(int d, int u) { return d * 128 + ((u ^ ((d >> 1) & 15)) << 3); }
+
+template <int D, int HPW>
+__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
+    const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
+    float scale, int causal) {
+  using Cfg = PrefillCfg<D>;
+  constexpr int RPW = 4 / HPW;  // row groups per workgroup
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int seq = tiles[2 * blockIdx.x], qs = tiles[2 * blockIdx.x + 1];
+  const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
+  const int ctx = ctx_lens[seq];
+  const int head = blockIdx.y * HPW + (wid % HPW);
+  const int g = (blockIdx.y * HPW) / (Hq / Hkv);
+  const int r0 = qs + 32 * (wid / HPW);  // first q row (within the sequence) of this wave
+  const int qrow = r0 + (lane & 31);
+  const int qpos = ctx - qlen + qrow;  // absolute position of this lane's query
+  const int* bt = block_tables + (size_t)seq * max_blocks;
+
+  // rows covered by the whole workgroup -> number of key tiles
+  const int last_row = min(qs + 32 * RPW, qlen) - 1;
+  const int kmax = causal ? (ctx - qlen + last_row + 1) : ctx;
+  const int ntiles = (kmax + Cfg::KT - 1) / Cfg::KT;
+
+  // Q fragments (B operand of S^T = K.Q^T): lane (q = lane&31, h) holds Q[q][16t + 8h .. +7]
+  bf16x8 qf[D / 16];
+  {
+    const bf16* qp = q + ((size_t)(qbeg + min(qrow, qlen - 1)) * Hq + head) * D + 8 * h;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) qf[t] = load8(qp + 16 * t);
+  }
+
+  // staging registers
+  bf16x8 kst[Cfg::CH], vst[Cfg::CH];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < Cfg::CH; ++c) {
+      const int id = c * 256 + tid;
+      const int page = id / (2 * D), w = id % (2 * D);
+      const int pidx = kt * 4 + page;
+      const int blk = (pidx * kBS < ctx) ? bt[pidx] : bt[0];
+      const size_t pbase = ((size_t)blk * Hkv + g) * kBS * D;
+      kst[c] = load8(kc + pbase + (size_t)w * 8);  // K page is [16][D] contiguous
+      vst[c] = load8(vc + pbase + (size_t)w * 8);  // V^T page is [D][16] contiguous
+    }
+  };
+  auto write_tile = [&](int buf) {
+    char* sk = smem + buf * Cfg::BUF;
+    char* sv = sk + Cfg::KBYTES;
+#pragma unroll
+    for (int c = 0; c < Cfg::CH; ++c) {
+      const int id = c * 256 + tid;
+      const int page = id / (2 * D), w = id % (2 * D);
+      const int key = page * 16 + w / Cfg::KU, u = w % Cfg::KU;
+      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kst[c];
+      const int d = w >> 1, half = w & 1;
+      const int u8 = 4 * page + 2 * half;
+      typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+      const bf16x4_t lo = {vst[c][0], vst[c][1], vst[c][2], vst[c][3]};
+      const bf16x4_t hi = {vst[c][4], vst[c][5], vst[c][6], vst[c][7]};
+      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8)) = lo;
+      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8 + 1)) = hi;
+    }
+  };
+
+  f32x16 acc_o[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) acc_o[i] = f32x16{};
+  float m_run = kNeg, l_run = 0.f;
+  const float sl2 = scale * kLog2e;
+
+  if (ntiles > 0) {
+    load_tile(0);
+    write_tile(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+    const char* sk = smem + cur * Cfg::BUF;
+    const char* sv = sk + Cfg::KBYTES;
+
+    // S^T[key][q] for two 32-key halves
+    f32x16 s[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      s[sub] = f32x16{};
+      const int key = 32 * sub + (lane & 31);
+#pragma unroll
+      for (int t = 0; t < D / 16; ++t) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
+        s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], s[sub], 0, 0, 0);
+      }
+    }
+    // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves
+    float mt = kNeg;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool ok = key < ctx && (!causal || key <= qpos);
+        const float x = ok ? s[sub][r] * sl2 : kNeg;
+        s[sub][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[sub][r] - m_new);
+        s[sub][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) acc_o[i] *= alpha;
+
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int sub = st >> 1, sp = st & 1;
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (bf16)s[sub][8 * sp + j];
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int d = 32 * dt + (lane & 31);
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(sv + v_lds_off(d, 4 * st + h));
+        const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(sv + v_lds_off(d, 4 * st + 2 + h));
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[dt], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < ntiles) write_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (qrow < qlen) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16* op = out + ((size_t)(qbeg + qrow) * Hq + head) * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc_o[dt][4 * c + r] * inv);
+        *reinterpret_cast<bf16x4_t*>(op + 32 * dt + 8 * c + 4 * h) = o;
+      }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Decode
+// ----------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_decode_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
+    float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int Hq, int Hkv, float scale, int split_keys,
+    int max_splits) {
+  __shared__ __attribute__((aligned(16))) float red_o[4][D][16];
+  __shared__ float red_m[4][16], red_l[4][16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, gq = lane >> 4;
+  const int split = blockIdx.x, g = blockIdx.y, seq = blockIdx.z;
+  const int ratio = Hq / Hkv;
+  const int ctx = ctx_lens[seq];
+  const int kstart = split * split_keys;
+  if (kstart >= ctx) return;
+  const int kend = min(ctx, kstart + split_keys);
+  const int nsplit = (ctx + split_keys - 1) / split_keys;
+  const int* bt = block_tables + (size_t)seq * max_blocks;
+  const int qi = lane & 15;  // GQA head index inside the group (MFMA column)
+
+  bf16x8 qf[D / 32];
+  {
+    const bool qv = qi < ratio;
+    const bf16* qp = q + ((size_t)seq * Hq + g * ratio + (qv ? qi : 0)) * D + 8 * gq;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) qf[t] = qv ? load8(qp + 32 * t) : bf16x8{};
+  }
+
+  f32x4 acc_o[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) acc_o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = kNeg, l_run = 0.f;
+  const float sl2 = scale * kLog2e;
+
+  for (int kb = kstart + 32 * wid; kb < kend; kb += 128) {
+    const int p0 = kb / kBS;
+    const int blk0 = bt[p0];
+    const int blk1 = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : blk0;
+    const size_t pb0 = ((size_t)blk0 * Hkv + g) * kBS * D, pb1 = ((size_t)blk1 * Hkv + g) * kBS * D;
+    // issue all loads of the chunk first
+    bf16x8 kf[2][D / 32];
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      kf[0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+      kf[1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+    }
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    bf16x4_t vlo[D / 16], vhi[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      const size_t off = (size_t)(16 * dt + (lane & 15)) * kBS + 4 * gq;
+      vlo[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
+      vhi[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
+    }
+    f32x4 s[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      s[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) s[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[i][t], qf[t], s[i], 0, 0, 0);
+    }
+    float mt = kNeg;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb + 16 * i + 4 * gq + r;
+        const float x = key < kend ? s[i][r] * sl2 : kNeg;
+        s[i][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    float rs = 0.f;
+    bf16x8 pf;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[i][r] - m_new);
+        rs += p;
+        pf[4 * i + r] = (bf16)p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      acc_o[dt] *= alpha;
+      const bf16x8 vf = {vlo[dt][0], vlo[dt][1], vlo[dt][2], vlo[dt][3], vhi[dt][0], vhi[dt][1], vhi[dt][2], vhi[dt][3]};
+      acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, acc_o[dt], 0, 0, 0);
+    }
+  }
+
+  // combine the 4 waves: acc_o lane layout O^T[d = 16dt + 4gq + r][q = lane&15]
+  if (lane < 16) {
+    red_m[wid][lane] = m_run;
+    red_l[wid][lane] = l_run;
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red_o[wid][16 * dt + 4 * gq + r][qi] = acc_o[dt][r];
+  __syncthreads();
+  for (int e = tid; e < ratio * D; e += 256) {
+    const int qq = e / D, d = e % D;
+    float M = kNeg;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][qq]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(red_m[w][qq] - M);
+      L += red_l[w][qq] * f;
+      O += red_o[w][d][qq] * f;
+    }
+    const int hq = g * ratio + qq;
+    if (nsplit == 1) {
+      out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+    } else {
+      ws_o[(((size_t)split * B + seq) * Hq + hq) * D + d] = O;
+      if (d == 0) {
+        ws_ml[(((size_t)split * B + seq) * Hq + hq) * 2] = M;
+        ws_ml[(((size_t)split * B + seq) * Hq + hq) * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void attn_decode_reduce_kernel(const float* __restrict__ ws_o, const float* __restrict__ ws_ml,
+                                          const int* __restrict__ ctx_lens, bf16* __restrict__ out, int B, int Hq,
+                                          int split_keys) {
+  const int seq = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const int ctx = ctx_lens[seq];
+  const int ns = (ctx + split_keys - 1) / split_keys;
+  if (ns <= 1) return;
+  float M = kNeg;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, ws_ml[(((size_t)s * B + seq) * Hq + hq) * 2]);
+  float L = 0.f, O = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    const size_t i = ((size_t)s * B + seq) * Hq + hq;
+    const float f = exp2f(ws_ml[i * 2] - M);
+    L += ws_ml[i * 2 + 1] * f;
+    O += ws_o[i * D + d] * f;
+  }
+  out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+}
+
+template <typename F>
+void set_max_lds(F* f, int bytes) {
+  static bool done = false;
+  if (!done) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    done = true;
+  }
+}
+
+}  // namespace
+
+void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                      int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
+                      int Hq, int Hkv, int D, float scale, int causal, hipStream_t st) {
+  if (ntiles == 0) return;
+  const int ratio = Hq / Hkv;
+  const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
+#define GAI_PF(DD, HP)                                                                                         \
+  if (D == DD && hpw == HP) {                                                                                  \
+    const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
+    auto kern = attn_prefill_kernel<DD, HP>;                                                                   \
+    set_max_lds(kern, lds);                                                                                    \
+    kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,  \
+                                                  block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq, \
+                                                  Hkv, scale, causal);                                         \
+    GAI_LAUNCH_CHECK();                                                                                        \
+    return;                                                                                                    \
+  }
+  GAI_PF(64, 1)
+  GAI_PF(64, 2)
+  GAI_PF(64, 4)
+  GAI_PF(128, 1)
+  GAI_PF(128, 2)
+  GAI_PF(128, 4)
+#undef GAI_PF
+  gai_launch_error(__FILE__, __LINE__, "attn_prefill: unsupported head_dim");
+}
+
+int gai_attn_prefill_rows_per_tile(int Hq, int Hkv) {
+  const int ratio = Hq / Hkv;
+  const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
+  return 32 * (4 / hpw);
+}
+
+void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                     int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
+                     int Hkv, int D, float scale, int split_keys, int max_splits, hipStream_t st) {
+  if (B == 0) return;
+  if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
+  if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
+  const dim3 grid(max_splits, Hkv, B);
+#define GAI_DEC(DD)                                                                                             \
+  if (D == DD) {                                                                                                \
+    attn_decode_kernel<DD><<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,    \
+                                                 block_tables, max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, \
+                                                 Hq, Hkv, scale, split_keys, max_splits);                       \
+    GAI_LAUNCH_CHECK();                                                                                         \
+    if (max_splits > 1) {                                                                                       \
+      attn_decode_reduce_kernel<DD><<<dim3(B, Hq), DD, 0, st>>>(ws_o, ws_ml, ctx_lens, (bf16*)out, B, Hq,       \
+                                                                 split_keys);                                   \
+      GAI_LAUNCH_CHECK();                                                                                       \
+    }                                                                                                           \
+    return;                                                                                                     \
+  }
+  GAI_DEC(64)
+  GAI_DEC(128)
+#undef GAI_DEC
+  gai_launch_error(__FILE__, __LINE__, "attn_decode: unsupported head_dim");
+}

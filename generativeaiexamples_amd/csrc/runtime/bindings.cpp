@@ -1,0 +1,87 @@
+// pybind11 module `generativeaiexamples_amd._rt`: the native host runtime.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "block_manager.h"
+#include "scheduler.h"
+
+namespace py = pybind11;
+using namespace gai;
+
+template <typename T>
+py::array_t<T> arr(const std::vector<T>& v) {
+  py::array_t<T> a(v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+template <typename T>
+py::array_t<T> arr2(const std::vector<T>& v, int cols) {
+  const size_t rows = cols ? v.size() / cols : 0;
+  py::array_t<T> a({rows, (size_t)cols});
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+PYBIND11_MODULE(_rt, m) {
+  m.doc() = "native host runtime: paged-KV block manager + continuous-batching scheduler";
+  m.attr("BLOCK_SIZE") = kBlockSize;
+
+  py::class_<BlockManager>(m, "BlockManager")
+      .def(py::init<int, bool>(), py::arg("num_blocks"), py::arg("prefix_cache") = true)
+      .def("alloc", &BlockManager::alloc)
+      .def("incref", &BlockManager::incref)
+      .def("decref", &BlockManager::decref)
+      .def("num_free", &BlockManager::num_free)
+      .def("num_blocks", &BlockManager::num_blocks)
+      .def("can_allocate", &BlockManager::can_allocate)
+      .def("match_prefix", &BlockManager::match_prefix)
+      .def("commit", &BlockManager::commit)
+      .def_static("chain_hash",
+                  [](uint64_t parent, const std::vector<int>& t) {
+                    return BlockManager::chain_hash(parent, t.data(), (int)t.size());
+                  });
+
+  py::class_<StepBatch>(m, "StepBatch")
+      .def_property_readonly("token_ids", [](const StepBatch& b) { return arr(b.token_ids); })
+      .def_property_readonly("positions", [](const StepBatch& b) { return arr(b.positions); })
+      .def_property_readonly("slots", [](const StepBatch& b) { return arr(b.slots); })
+      .def_property_readonly("prefill_seq_ids", [](const StepBatch& b) { return b.prefill_seq_ids; })
+      .def_property_readonly("cu_q", [](const StepBatch& b) { return arr(b.cu_q); })
+      .def_property_readonly("prefill_ctx", [](const StepBatch& b) { return arr(b.prefill_ctx); })
+      .def_property_readonly("prefill_qlen", [](const StepBatch& b) { return b.prefill_qlen; })
+      .def_property_readonly("prefill_block_tables",
+                             [](const StepBatch& b) { return arr2(b.prefill_block_tables, b.max_blocks); })
+      .def_property_readonly("prefill_samples",
+                             [](const StepBatch& b) { return std::vector<int>(b.prefill_samples.begin(), b.prefill_samples.end()); })
+      .def_property_readonly("decode_seq_ids", [](const StepBatch& b) { return b.decode_seq_ids; })
+      .def_property_readonly("decode_ctx", [](const StepBatch& b) { return arr(b.decode_ctx); })
+      .def_property_readonly("decode_block_tables",
+                             [](const StepBatch& b) { return arr2(b.decode_block_tables, b.max_blocks); })
+      .def_property_readonly("preempted", [](const StepBatch& b) { return b.preempted; })
+      .def_readonly("max_blocks", &StepBatch::max_blocks)
+      .def_readonly("num_prefill_tokens", &StepBatch::num_prefill_tokens)
+      .def_property_readonly("num_tokens", [](const StepBatch& b) { return (int)b.token_ids.size(); });
+
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<int, int, int, int, bool, int>(), py::arg("num_blocks"), py::arg("max_num_seqs"),
+           py::arg("max_batched_tokens"), py::arg("max_model_len"), py::arg("prefix_cache") = true,
+           py::arg("prefill_chunk") = 0)
+      .def("add", &Scheduler::add, py::arg("id"), py::arg("prompt"), py::arg("max_new_tokens"),
+           py::arg("priority") = 0)
+      .def("abort", &Scheduler::abort)
+      .def("finish", &Scheduler::finish)
+      .def("append_tokens", &Scheduler::append_tokens)
+      .def("schedule", &Scheduler::schedule, py::call_guard<py::gil_scoped_release>())
+      .def("num_waiting", &Scheduler::num_waiting)
+      .def("num_running", &Scheduler::num_running)
+      .def("num_free_blocks", &Scheduler::num_free_blocks)
+      .def("num_blocks", &Scheduler::num_blocks)
+      .def("prefix_hit_rate", &Scheduler::prefix_hit_rate)
+      .def("has_work", &Scheduler::has_work)
+      .def("num_tokens", &Scheduler::num_tokens)
+      .def("num_generated", &Scheduler::num_generated);
+}

@@ -1,0 +1,256 @@
+"""Plain-PyTorch fp32 reference implementations of every native op.
+
+These define the semantics the HIP kernels are tested against (tests compare the
+gfx950 kernels with these on random inputs) and they are the execution path for
+CPU tensors (BASELINE config 1, the CPU plumbing config, and the CPU test tier).
+Layouts are identical to the native ones:
+
+* paged K cache  ``[num_blocks, Hkv, 16, D]``
+* paged V^T cache ``[num_blocks, Hkv, D, 16]``
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+BLOCK = 16
+
+
+def rms_norm(x, w, eps, residual=None):
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(r)
+        x = r
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype)
+
+
+def layer_norm(x, w, b, eps, residual=None):
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(r)
+        x = r
+    y = F.layer_norm(x.float(), (x.shape[-1],), w.float(), None if b is None else b.float(), eps)
+    return y.to(x.dtype)
+
+
+def linear(x, w, bias=None, residual=None, act=None, out_dtype=None):
+    """y = act(x @ w^T + bias) + residual; act in {None, 'gelu', 'relu', 'swiglu'}.
+
+    'swiglu' expects w interleaved per 16 rows [gate16 | up16 | ...] (see
+    ``interleave_gate_up``) and returns width N/2.
+    """
+    y = x.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "relu":
+        y = F.relu(y)
+    elif act == "swiglu":
+        n = y.shape[-1]
+        y4 = y.reshape(*y.shape[:-1], n // 32, 2, 16)
+        y = (F.silu(y4[..., 0, :]) * y4[..., 1, :]).reshape(*y.shape[:-1], n // 2)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(out_dtype or x.dtype)
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """[I, K] gate and up -> [2I, K] with rows interleaved per 16 (the fused SwiGLU GEMM layout)."""
+    I, K = gate.shape
+    assert I % 16 == 0
+    return torch.stack([gate.reshape(I // 16, 16, K), up.reshape(I // 16, 16, K)], 1).reshape(2 * I, K)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float = 500000.0, scaling: dict | None = None,
+                 device=None) -> torch.Tensor:
+    """fp32 table [max_pos, D] = [cos(D/2) | sin(D/2)], neox rotate-half convention.
+
+    ``scaling`` implements the Llama-3.1 frequency-dependent rope scaling
+    ({"factor", "low_freq_factor", "high_freq_factor", "original_max_position_embeddings"}).
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:
+        factor = scaling.get("factor", 8.0)
+        lf, hf = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        low_wl, high_wl = old / lf, old / hf
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lf) / (hf - lf)
+        scaled = torch.where(wl > low_wl, inv / factor, inv)
+        mid = (wl <= low_wl) & (wl >= high_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], -1).float().to(device)
+
+
+def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope=True):
+    T = qkv.shape[0]
+    x = qkv.view(T, Hq + 2 * Hkv, D).float()
+    q, k, v = x[:, :Hq], x[:, Hq:Hq + Hkv], x[:, Hq + Hkv:]
+    if rope:
+        cs = cos_sin[positions.long()]
+        c, s = cs[:, None, : D // 2], cs[:, None, D // 2:]
+
+        def rot(t):
+            t = t.to(qkv.dtype).float()  # kernel rounds inputs to bf16 first (they already are)
+            a, b = t[..., : D // 2], t[..., D // 2:]
+            return torch.cat([a * c - b * s, b * c + a * s], -1)
+
+        q, k = rot(q), rot(k)
+    q_out.copy_(q.to(q_out.dtype).reshape(q_out.shape))
+    valid = slots >= 0
+    if valid.any():
+        sl = slots[valid].long()
+        blk, off = sl // BLOCK, sl % BLOCK
+        k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
+        v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+
+
+def gather_kv(k_cache, v_cache, block_table, n):
+    """-> K [n, Hkv, D], V [n, Hkv, D] for the first n tokens of a sequence."""
+    nb = (n + BLOCK - 1) // BLOCK
+    blocks = block_table[:nb].long()
+    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * BLOCK, k_cache.shape[1], k_cache.shape[3])[:n]
+    v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * BLOCK, v_cache.shape[1], v_cache.shape[2])[:n]
+    return k, v
+
+
+def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True):
+    """q [Tq, Hq, D]; per sequence b the queries are the last q_len positions of ctx_lens[b] keys."""
+    out = torch.empty_like(q)
+    Hq = q.shape[1]
+    Hkv = k_cache.shape[1]
+    cu = cu_q.tolist()
+    for b in range(len(cu) - 1):
+        s, e = cu[b], cu[b + 1]
+        if e == s:
+            continue
+        n = int(ctx_lens[b])
+        k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+        k = k.float().repeat_interleave(Hq // Hkv, dim=1)
+        v = v.float().repeat_interleave(Hq // Hkv, dim=1)
+        qq = q[s:e].float()
+        att = torch.einsum("qhd,khd->hqk", qq, k) * scale
+        if causal:
+            qpos = torch.arange(n - (e - s), n, device=q.device)
+            mask = torch.arange(n, device=q.device)[None, :] > qpos[:, None]
+            att = att.masked_fill(mask[None], float("-inf"))
+        p = att.softmax(-1)
+        out[s:e] = torch.einsum("hqk,khd->qhd", p, v).to(q.dtype)
+    return out
+
+
+def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale):
+    """q [B, Hq, D], one token per sequence attending to its ctx_lens[b] cached keys."""
+    B = q.shape[0]
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    return attention_prefill(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, causal=True)
+
+
+def attention_dense(q, k, v, cu_seqlens, scale, causal):
+    """Contiguous varlen attention (encoders): q/k/v [T, H, D] (k/v may have fewer heads)."""
+    out = torch.empty_like(q)
+    cu = cu_seqlens.tolist()
+    rep = q.shape[1] // k.shape[1]
+    for b in range(len(cu) - 1):
+        s, e = cu[b], cu[b + 1]
+        qq, kk, vv = q[s:e].float(), k[s:e].float(), v[s:e].float()
+        kk, vv = kk.repeat_interleave(rep, 1), vv.repeat_interleave(rep, 1)
+        att = torch.einsum("qhd,khd->hqk", qq, kk) * scale
+        if causal:
+            n = e - s
+            att = att.masked_fill(torch.ones(n, n, dtype=torch.bool, device=q.device).triu(1)[None], float("-inf"))
+        out[s:e] = torch.einsum("hqk,khd->qhd", att.softmax(-1), vv).to(q.dtype)
+    return out
+
+
+def sample(logits, temperature, top_p, top_k, seeds, step, generator=None):
+    """Reference sampler (distributionally equivalent to the kernel, not bit-identical)."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    for i in range(B):
+        x = logits[i].float()
+        T = float(temperature[i])
+        if T <= 0:
+            out[i] = int(torch.argmax(x))
+            continue
+        x = x / T
+        k = int(top_k[i])
+        if 0 < k < V:
+            kth = torch.topk(x, k).values[-1]
+            x = x.masked_fill(x < kth, float("-inf"))
+        p = float(top_p[i])
+        if p < 1.0:
+            probs = x.softmax(-1)
+            sp, si = probs.sort(descending=True)
+            cum = sp.cumsum(0)
+            keep = (cum - sp) < p
+            thr = sp[keep].min()
+            x = x.masked_fill(probs < thr, float("-inf"))
+        g = torch.Generator(device="cpu")
+        g.manual_seed((int(seeds[i]) * 1000003 + int(step)) & 0x7FFFFFFFFFFFFFFF)
+        probs = x.softmax(-1).cpu()
+        out[i] = int(torch.multinomial(probs, 1, generator=g))
+    return out
+
+
+def apply_penalties(logits, tok_ids, tok_cnt, n, freq, pres, rep):
+    for b in range(logits.shape[0]):
+        m = int(n[b])
+        ids, cnt = tok_ids[b, :m].long(), tok_cnt[b, :m].float()
+        v = logits[b, ids]
+        r = float(rep[b])
+        if r != 1.0:
+            v = torch.where(v > 0, v / r, v * r)
+        v = v - float(freq[b]) * cnt - (cnt > 0).float() * float(pres[b])
+        logits[b, ids] = v
+    return logits
+
+
+def sim_topk(Q, X, bias, n_rows, k):
+    s = Q.float() @ X[:n_rows].float().t() + bias[:n_rows].float()
+    k = min(k, n_rows)
+    v, i = torch.topk(s, k, dim=-1)
+    return v, i
+
+
+def embedding(ids, table, vstart=0, vend=None):
+    vend = table.shape[0] + vstart if vend is None else vend
+    ids = ids.long()
+    ok = (ids >= vstart) & (ids < vend)
+    out = table[(ids - vstart).clamp(0, table.shape[0] - 1)]
+    return out * ok[:, None].to(out.dtype)
+
+
+def pool(h, cu_seqlens, mode="mean", normalize=True):
+    cu = cu_seqlens.tolist()
+    outs = []
+    for b in range(len(cu) - 1):
+        s, e = cu[b], cu[b + 1]
+        x = h[s:e].float()
+        if mode == "mean":
+            v = x.mean(0)
+        elif mode == "cls":
+            v = x[0]
+        else:
+            v = x[-1]
+        outs.append(v)
+    o = torch.stack(outs) if outs else h.new_zeros(0, h.shape[-1], dtype=torch.float32)
+    if normalize:
+        o = F.normalize(o, dim=-1, eps=1e-12)
+    return o
+
+
+def silu_mul(x):
+    i = x.shape[-1] // 2
+    return (F.silu(x[..., :i].float()) * x[..., i:].float()).to(x.dtype)
+
+
+def gelu(x):
+    return F.gelu(x.float()).to(x.dtype)

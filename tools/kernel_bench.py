@@ -1,0 +1,140 @@
+"""Micro-benchmarks of the gfx950 kernels vs the PyTorch/hipBLASLt baseline on the same data.
+
+Interleaved rounds in one process (cdna_hip_programming §5.4 rule 24), random operands
+(rule 25). Prints one JSON line per case; use --out to also write them to a file.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import time
+
+import torch
+
+from generativeaiexamples_amd import ops
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def bench_gemm(rows, shapes):
+    for M, N, K, tag in shapes:
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+        t_ours = timeit(lambda: ops.linear(x, w))
+        t_blas = timeit(lambda: torch.matmul(x, w.t()))
+        fl = 2 * M * N * K
+        by = 2 * (M * K + N * K + M * N)
+        rows.append(dict(op="gemm", tag=tag, M=M, N=N, K=K, ours_ms=t_ours, hipblaslt_ms=t_blas,
+                         ours_tflops=fl / t_ours / 1e9, hipblaslt_tflops=fl / t_blas / 1e9,
+                         ours_gbs=by / t_ours / 1e6, speedup=t_blas / t_ours))
+
+
+def bench_prefill(rows, B, S, Hq, Hkv, D):
+    nb = B * ((S + 15) // 16)
+    kc = torch.randn(nb, Hkv, 16, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, D, 16, device="cuda", dtype=torch.bfloat16)
+    bt = torch.arange(nb, device="cuda", dtype=torch.int32).reshape(B, -1)
+    q = torch.randn(B * S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    cu = torch.arange(0, B * S + 1, S, device="cuda", dtype=torch.int32)
+    ctx = torch.full((B,), S, device="cuda", dtype=torch.int32)
+    tiles = ops.build_prefill_tiles([S] * B, Hq, Hkv, "cuda")
+    t = timeit(lambda: ops.attention_prefill(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), True, tiles=tiles))
+    qs = q.view(B, S, Hq, D).transpose(1, 2)
+    ks = torch.randn(B, Hkv, S, D, device="cuda", dtype=torch.bfloat16).repeat_interleave(Hq // Hkv, 1)
+    vs = torch.randn(B, Hkv, S, D, device="cuda", dtype=torch.bfloat16).repeat_interleave(Hq // Hkv, 1)
+    t_sdpa = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=True))
+    fl = 4 * B * Hq * S * S * D / 2
+    rows.append(dict(op="attn_prefill", B=B, S=S, Hq=Hq, Hkv=Hkv, D=D, ours_ms=t, sdpa_ms=t_sdpa,
+                     ours_tflops=fl / t / 1e9, sdpa_tflops=fl / t_sdpa / 1e9))
+
+
+def bench_decode(rows, B, ctx, Hq, Hkv, D):
+    nbps = (ctx + 15) // 16
+    nb = B * nbps
+    kc = torch.randn(nb, Hkv, 16, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, D, 16, device="cuda", dtype=torch.bfloat16)
+    bt = torch.randperm(nb, device="cuda").int().reshape(B, nbps)
+    q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    cl = torch.full((B,), ctx, device="cuda", dtype=torch.int32)
+    ws = ops.DecodeWorkspace(B, Hq, D, ctx, "cuda")
+    t = timeit(lambda: ops.attention_decode(q, kc, vc, bt, cl, 1 / math.sqrt(D), ws=ws))
+    by = 2 * B * ctx * Hkv * D * 2
+    rows.append(dict(op="attn_decode", B=B, ctx=ctx, Hq=Hq, Hkv=Hkv, D=D, split=ws.split_keys, ours_ms=t,
+                     ours_gbs=by / t / 1e6))
+
+
+def bench_misc(rows):
+    x = torch.randn(8192, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(4096, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    t = timeit(lambda: ops.rms_norm(x, w, 1e-5, r))
+    rows.append(dict(op="rmsnorm_residual", T=8192, D=4096, ours_ms=t, ours_gbs=4 * x.numel() * 2 / t / 1e6))
+    logits = torch.randn(64, 128256, device="cuda")
+    temp = torch.full((64,), 0.2, device="cuda")
+    tp = torch.full((64,), 0.7, device="cuda")
+    tk = torch.zeros(64, dtype=torch.int32, device="cuda")
+    sd = torch.arange(64, device="cuda", dtype=torch.int64)
+    t = timeit(lambda: ops.sample(logits, temp, tp, tk, sd, 0))
+    rows.append(dict(op="sample_top_p", B=64, V=128256, ours_ms=t))
+    X = torch.randn(1_000_000, 1024, device="cuda", dtype=torch.bfloat16)
+    bias = torch.zeros(1_000_000, device="cuda")
+    for nq in (1, 16, 64):
+        Q = torch.randn(nq, 1024, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: ops.sim_topk(Q, X, bias, 1_000_000, 4), iters=10)
+        t_ref = timeit(lambda: torch.topk(Q @ X.t(), 4, dim=-1), iters=10)
+        rows.append(dict(op="sim_topk", nq=nq, N=1_000_000, D=1024, k=4, ours_ms=t, torch_ms=t_ref,
+                         ours_gbs=X.numel() * 2 / t / 1e6))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="gemm,prefill,decode,misc")
+    a = ap.parse_args()
+    rows = []
+    only = set(a.only.split(","))
+    if "gemm" in only:
+        shapes = [
+            (4096, 6144, 4096, "llama8b qkv prefill"), (4096, 28672, 4096, "llama8b gate_up prefill"),
+            (4096, 4096, 14336, "llama8b down prefill"), (8192, 8192, 8192, "square 8k"),
+            (64, 6144, 4096, "qkv decode b64"), (64, 28672, 4096, "gate_up decode b64"),
+            (64, 4096, 14336, "down decode b64"), (64, 128256, 4096, "lm_head decode b64"),
+            (1, 6144, 4096, "qkv decode b1"), (128, 4096, 4096, "o decode b128"),
+            (16384, 1024, 1024, "e5 qkv-ish"), (16384, 4096, 1024, "e5 ffn up"),
+        ]
+        bench_gemm(rows, shapes)
+    if "prefill" in only:
+        bench_prefill(rows, 4, 2048, 32, 8, 128)
+        bench_prefill(rows, 64, 512, 16, 16, 64)
+    if "decode" in only:
+        bench_decode(rows, 64, 2304, 32, 8, 128)
+        bench_decode(rows, 1, 2304, 32, 8, 128)
+        bench_decode(rows, 128, 4096, 32, 8, 128)
+    if "misc" in only:
+        bench_misc(rows)
+    f = open(a.out, "w") if a.out else None
+    for r in rows:
+        line = json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()})
+        print(line, flush=True)
+        if f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
