@@ -1,0 +1,225 @@
+#!/usr/bin/env python
+"""Headline benchmark: end-to-end RAG queries/sec + p50 TTFT (BASELINE.json config 2 on every GPU).
+
+Per GPU: Llama-3-8B bf16 generator (TP=1, random-init weights of the real architecture),
+e5-large-v2 bf16 embedder (random-init), and a 1M x 1024 exact HBM vector index shard over a
+synthetic corpus of 506-token chunks. One timed *step* = one wave of ``--batch`` concurrent RAG
+queries per GPU through the whole query path of the reference's basic_rag chain
+(RAG/examples/basic_rag/langchain/chains.py rag_chain):
+
+  query -> e5 "query: " embedding (all-gathered across ranks: embedder DP)
+        -> exact top-4 search of every shard (candidates all-gathered + merged: index DP, RCCL)
+        -> prompt = rag_template + "Context: <4 chunks>\n\nQuestion: <q>" (Llama-3 chat format)
+        -> continuous-batching generation, temperature 0.2 / top_p 0.7, max_tokens 256 (the
+           reference evaluation tool's generation settings, llm_answer_generator.py:63).
+
+value = total queries/s over all ranks (weak scaling: --batch queries per GPU per step).
+TTFT = query arrival (step start) -> first generated token, per query; p50/p90 reported.
+vs_baseline = value / 0.2141 queries/s: the reference's own published single-stream L40S figures
+for Llama-3-8B (TTFT 0.062 s + 249 x 18.5 ms TPOT = 4.67 s per query).
+
+Notes: the KV prefix cache is off (every query prefills its full prompt); score_threshold is disabled (random-init embeddings give near-zero cosine to a random
+index; thresholding would drop every chunk); EOS is ignored so every query generates exactly
+max_tokens (fixed work per step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+METRIC = "end-to-end RAG queries/sec + p50 TTFT, Llama-3-8B gen + e5-large embed"
+BASELINE_QPS = 1.0 / (0.062 + 249 * 0.0185)  # BASELINE.md row 2 (L40S, single stream)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--top-k", type=int, default=4)
+    ap.add_argument("--chunk-tokens", type=int, default=506)
+    ap.add_argument("--index-size", type=int, default=1_000_000, help="vectors per GPU shard")
+    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "tiny"])
+    ap.add_argument("--embedder", default="e5-large-v2", choices=["e5-large-v2", "e5-base-v2", "tiny"])
+    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--prefix-cache", action="store_true",
+                    help="enable KV prefix caching (off by default: random-init embeddings retrieve the same "
+                         "chunks for every query, so caching would skip most of the prefill work)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.embedder import Embedder
+    from generativeaiexamples_amd.engine.tokenizer import (apply_chat_template, bert_byte_tokenizer,
+                                                           llama3_byte_tokenizer, small_byte_tokenizer)
+    from generativeaiexamples_amd.index.hbm_index import HBMIndex
+    from generativeaiexamples_amd.index.sharded import ShardedIndex
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.models.bert import BertConfig, BertModel
+    from generativeaiexamples_amd.parallel.dist import init_distributed
+    from generativeaiexamples_amd.rag import synthetic
+    from generativeaiexamples_amd.rag.prompts import RAG_TEMPLATE, rag_user_message
+
+    ctx = init_distributed(tp_size=1)
+    dev = ctx.device
+    rank, world = ctx.rank, ctx.world_size
+    torch.manual_seed(1234 + rank)
+    t_setup = time.perf_counter()
+
+    # ---------------- models
+    if args.model == "llama3-8b":
+        lcfg = LlamaConfig.llama3_8b()
+        ltok = llama3_byte_tokenizer(lcfg.vocab_size)
+    else:
+        lcfg = LlamaConfig.tiny(max_position=8192)
+        ltok = small_byte_tokenizer(lcfg.vocab_size)
+    llm = LlamaModel(lcfg, device=dev).random_init(seed=1)
+    if args.embedder == "e5-large-v2":
+        bcfg = BertConfig.e5_large_v2()
+    elif args.embedder == "e5-base-v2":
+        bcfg = BertConfig.e5_base_v2()
+    else:
+        bcfg = BertConfig.tiny()
+    enc = BertModel(bcfg, device=dev).random_init(seed=2)
+    embedder = Embedder(enc, bert_byte_tokenizer(bcfg.vocab_size))
+    log(f"models ready: {lcfg.name} {llm.num_params() / 1e9:.2f}B params, {bcfg.name}")
+
+    # ---------------- index shard (1M x dim per GPU, synthetic documents on demand)
+    index = HBMIndex(bcfg.hidden_size, "cosine", device=dev, capacity=args.index_size)
+    ct = args.chunk_tokens
+    index.add_random(args.index_size, seed=100 + rank, doc_fn=lambda r: synthetic.chunk_document(r, ct))
+    sharded = ShardedIndex(index)
+    log(f"index ready: {args.index_size} x {bcfg.hidden_size} per shard, {world} shard(s)")
+
+    # ---------------- engine
+    prompt_est = 60 + args.top_k * (args.chunk_tokens + 2) + 80
+    ecfg = EngineConfig(max_num_seqs=max(args.batch, 1), max_batched_tokens=args.max_batched_tokens,
+                        max_model_len=min(lcfg.max_position, prompt_est + args.max_tokens + 64),
+                        prefill_chunk=args.max_batched_tokens, use_graphs=not args.no_graphs,
+                        prefix_cache=args.prefix_cache,
+                        kv_memory_fraction=0.5)
+    engine = LLMEngine(llm, ltok, ecfg)
+    if not args.no_graphs:
+        engine.capture_graphs(max_bs=args.batch)
+    log(f"engine ready: {engine.kv.num_blocks} KV blocks ({engine.kv.nbytes / 2**30:.1f} GiB), "
+        f"graphs={sorted(engine.graphs)} setup {time.perf_counter() - t_setup:.1f}s")
+
+    params = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=args.max_tokens, ignore_eos=True)
+    doc_of = lambda g: index.document(ShardedIndex.split_row(g)[1]) if world > 1 else index.document(g)  # noqa
+
+    def run_step(step_idx: int):
+        qids = [(step_idx * world + rank) * args.batch + i for i in range(args.batch)]
+        questions = [synthetic.question(q) for q in qids]
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        emb = embedder.embed(questions, input_type="query")
+        rel, rows = sharded.search_raw(emb, args.top_k)
+        rows = rows.cpu().tolist()
+        uniq.update(g for r in rows for g in r)
+        reqs = []
+        for qi, q in enumerate(questions):
+            docs = [doc_of(g) for g in rows[qi] if g >= 0]
+            context = "\n\n".join(d.page_content for d in docs)
+            msgs = [{"role": "system", "content": RAG_TEMPLATE},
+                    {"role": "user", "content": rag_user_message(context, q)}]
+            reqs.append(engine.add_request(apply_chat_template(msgs, ltok), params))
+        t_retrieved = time.perf_counter()
+        while engine.has_work():
+            engine.step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        t1 = time.perf_counter()
+        ttft = [r.first_token_time - t0 for r in reqs]
+        ntok = sum(len(r.output_ids) for r in reqs)
+        plen = statistics.mean(len(r.prompt_ids) for r in reqs)
+        return t1 - t0, ttft, ntok, plen, t_retrieved - t0
+
+    uniq = set()
+    for w in range(args.warmup):
+        dt, *_ = run_step(10_000 + w)
+        log(f"warmup {w}: {dt:.2f}s")
+    times, ttfts, toks, plens, rtimes = [], [], 0, [], []
+    for s in range(args.steps):
+        dt, ttft, ntok, plen, rt = run_step(s)
+        times.append(dt)
+        ttfts += ttft
+        toks += ntok
+        plens.append(plen)
+        rtimes.append(rt)
+        log(f"step {s}: {dt:.3f}s  p50 TTFT {statistics.median(ttft):.3f}s  retrieval {rt * 1000:.1f} ms")
+
+    total = sum(times)
+    # max over ranks
+    if world > 1:
+        tt = torch.tensor([total], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        total = float(tt)
+        allt = ctx.all_gather_obj(ttfts)
+        ttfts = [x for part in allt for x in part]
+        toks = int(sum(ctx.all_gather_obj(toks)))
+    nq = args.batch * args.steps * world
+    qps = nq / total
+    ttfts.sort()
+    p50 = ttfts[len(ttfts) // 2]
+    p90 = ttfts[min(len(ttfts) - 1, int(0.9 * len(ttfts)))]
+    out = {
+        "metric": METRIC,
+        "value": round(qps, 4),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * total / args.steps, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(qps / BASELINE_QPS, 3),
+        "dtype": "bf16",
+        "data": "synthetic (random-init weights of the named architectures; synthetic 506-token chunk corpus "
+                "and questions; score_threshold off, EOS ignored)",
+        "config": {
+            "model": f"{lcfg.name} + {bcfg.name} + {args.index_size}-vector exact HBM index per GPU",
+            "global_batch": args.batch * world,
+            "seq_len": int(statistics.mean(plens)) + args.max_tokens,
+            "parallelism": f"dp{world}",
+            "prompt_tokens": int(statistics.mean(plens)),
+            "max_tokens": args.max_tokens,
+            "top_k": args.top_k,
+        },
+        "p50_ttft_s": round(p50, 4),
+        "p90_ttft_s": round(p90, 4),
+        "output_tokens_per_s": round(toks / total, 1),
+        "retrieval_ms": round(1000 * statistics.mean(rtimes), 2),
+        "unique_chunks_retrieved": len(uniq),
+        "prefix_cache": bool(args.prefix_cache),
+        "baseline_qps": round(BASELINE_QPS, 4),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(out, f)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,191 @@
+"""Embedding and reranking engines (replace the embedding NIM and the reranking NIM).
+
+* :class:`Embedder` - E5-style asymmetric encoding (``"query: "`` / ``"passage: "`` prefixes selected
+  by the NIM ``input_type`` field), ``truncate`` = END | START | NONE like ``NVIDIAEmbeddings``,
+  length-sorted packing into varlen micro-batches under a token budget (no padding FLOPs).
+* :class:`Reranker` - cross-encoder scoring of (query, passage) pairs (``/v1/ranking``; the
+  multi-turn example reranks 40 candidates down to 4, multi_turn_rag/chains.py:147,177-191).
+* :class:`DynamicBatcher` - coalesces concurrent requests (<= max_batch, <= max_delay) onto one
+  engine call, the Triton ``dynamic_batching`` behaviour of the reference's MiniLM service
+  (all-MiniLM-L6-v2_config.pbtxt: preferred sizes up to 256, max_queue_delay 50 ms).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from concurrent.futures import Future
+from typing import List, Sequence, Tuple
+
+import torch
+
+from ..models.bert import BertModel
+from .tokenizer import Tokenizer
+
+
+class TruncationError(ValueError):
+    pass
+
+
+def _truncate(ids: List[int], max_len: int, mode: str) -> List[int]:
+    if len(ids) <= max_len:
+        return ids
+    mode = (mode or "END").upper()
+    if mode == "NONE":
+        raise TruncationError(f"input has {len(ids)} tokens > max {max_len} and truncate=NONE")
+    return ids[:max_len] if mode == "END" else ids[-max_len:]
+
+
+class Embedder:
+    def __init__(self, model: BertModel, tokenizer: Tokenizer, max_len: int | None = None,
+                 max_batch_tokens: int = 65536, query_prefix: str = "query: ", passage_prefix: str = "passage: ",
+                 model_name: str | None = None):
+        self.model, self.tok = model, tokenizer
+        self.max_len = min(max_len or model.cfg.max_position, model.cfg.max_position)
+        self.max_batch_tokens = max_batch_tokens
+        self.prefix = {"query": query_prefix, "passage": passage_prefix}
+        self.dim = model.cfg.hidden_size
+        self.name = model_name or model.cfg.name
+        self.cls_id = tokenizer.token_id("[CLS]") if tokenizer.token_id("[CLS]") is not None else tokenizer.bos_id
+        self.sep_id = tokenizer.token_id("[SEP]") if tokenizer.token_id("[SEP]") is not None else (
+            tokenizer.eos_ids[0] if tokenizer.eos_ids else None)
+        self.lock = threading.Lock()
+
+    def tokenize(self, text: str, input_type: str = "passage", truncate: str = "END") -> List[int]:
+        body = self.tok.encode(self.prefix.get(input_type, "") + text)
+        n_special = (self.cls_id is not None) + (self.sep_id is not None)
+        body = _truncate(body, self.max_len - n_special, truncate)
+        ids = ([self.cls_id] if self.cls_id is not None else []) + body + ([self.sep_id] if self.sep_id is not None else [])
+        return ids
+
+    def count_tokens(self, texts: Sequence[str]) -> int:
+        return sum(len(self.tok.encode(t)) for t in texts)
+
+    @torch.inference_mode()
+    def embed_ids(self, seqs: List[List[int]]) -> torch.Tensor:
+        """Token id lists -> fp32 [B, D] on the model device (input order preserved)."""
+        dev = self.model.device
+        order = sorted(range(len(seqs)), key=lambda i: len(seqs[i]))
+        out = torch.empty(len(seqs), self.dim, dtype=torch.float32, device=dev)
+        i = 0
+        with self.lock:
+            while i < len(order):
+                j, tot = i, 0
+                while j < len(order) and (tot + len(seqs[order[j]]) <= self.max_batch_tokens or j == i):
+                    tot += len(seqs[order[j]])
+                    j += 1
+                idx = order[i:j]
+                lens = [len(seqs[k]) for k in idx]
+                flat = torch.tensor([t for k in idx for t in seqs[k]], dtype=torch.int32)
+                cu = torch.zeros(len(idx) + 1, dtype=torch.int32)
+                cu[1:] = torch.tensor(lens).cumsum(0)
+                if dev.type == "cuda":
+                    flat, cu = flat.pin_memory().to(dev, non_blocking=True), cu.pin_memory().to(dev, non_blocking=True)
+                e = self.model.embed(flat, cu, lens)
+                out[torch.tensor(idx, device=dev)] = e
+                i = j
+        return out
+
+    def embed(self, texts: Sequence[str], input_type: str = "passage", truncate: str = "END") -> torch.Tensor:
+        return self.embed_ids([self.tokenize(t, input_type, truncate) for t in texts])
+
+
+class Reranker:
+    def __init__(self, model: BertModel, tokenizer: Tokenizer, max_len: int | None = None,
+                 max_batch_tokens: int = 65536, model_name: str | None = None):
+        assert model.cfg.num_labels > 0, "reranker needs a cross-encoder head (num_labels > 0)"
+        self.model, self.tok = model, tokenizer
+        self.max_len = min(max_len or model.cfg.max_position, model.cfg.max_position)
+        self.max_batch_tokens = max_batch_tokens
+        self.name = model_name or model.cfg.name
+        self.cls_id = tokenizer.token_id("[CLS]") if tokenizer.token_id("[CLS]") is not None else tokenizer.bos_id
+        self.sep_id = tokenizer.token_id("[SEP]") if tokenizer.token_id("[SEP]") is not None else (
+            tokenizer.eos_ids[0] if tokenizer.eos_ids else 0)
+        self.lock = threading.Lock()
+
+    def pair_ids(self, query: str, passage: str, truncate: str = "END") -> Tuple[List[int], List[int]]:
+        q = self.tok.encode(query)[: self.max_len // 2]
+        p = self.tok.encode(passage)
+        budget = self.max_len - len(q) - 3
+        p = _truncate(p, max(budget, 1), truncate)
+        ids = [self.cls_id] + q + [self.sep_id] + p + [self.sep_id]
+        types = [0] * (len(q) + 2) + [1] * (len(p) + 1)
+        return ids, types
+
+    @torch.inference_mode()
+    def score(self, query: str, passages: Sequence[str], truncate: str = "END") -> List[float]:
+        if not passages:
+            return []
+        pairs = [self.pair_ids(query, p, truncate) for p in passages]
+        dev = self.model.device
+        scores = [0.0] * len(pairs)
+        order = sorted(range(len(pairs)), key=lambda i: len(pairs[i][0]))
+        i = 0
+        with self.lock:
+            while i < len(order):
+                j, tot = i, 0
+                while j < len(order) and (tot + len(pairs[order[j]][0]) <= self.max_batch_tokens or j == i):
+                    tot += len(pairs[order[j]][0])
+                    j += 1
+                idx = order[i:j]
+                lens = [len(pairs[k][0]) for k in idx]
+                flat = torch.tensor([t for k in idx for t in pairs[k][0]], dtype=torch.int32, device=dev)
+                typ = torch.tensor([t for k in idx for t in pairs[k][1]], dtype=torch.int32, device=dev)
+                cu = torch.zeros(len(idx) + 1, dtype=torch.int32)
+                cu[1:] = torch.tensor(lens).cumsum(0)
+                s = self.model.score(flat, cu.to(dev), lens, typ).float().cpu().tolist()
+                for k, v in zip(idx, s):
+                    scores[k] = v
+                i = j
+        return scores
+
+    def rank(self, query: str, passages: Sequence[str], top_n: int | None = None, truncate: str = "END"):
+        """-> [(index, logit)] sorted by relevance (the NIM ``rankings`` list)."""
+        s = self.score(query, passages, truncate)
+        r = sorted(enumerate(s), key=lambda x: -x[1])
+        return r[:top_n] if top_n else r
+
+
+class DynamicBatcher:
+    """Thread-safe request coalescer in front of a batch function ``fn(list[item]) -> list[result]``."""
+
+    def __init__(self, fn, max_batch: int = 256, max_delay_ms: float = 5.0):
+        self.fn, self.max_batch, self.max_delay = fn, max_batch, max_delay_ms / 1000.0
+        self.q: List[Tuple[object, Future]] = []
+        self.cv = threading.Condition()
+        self.stop = False
+        self.t = threading.Thread(target=self._loop, daemon=True, name="dynamic-batcher")
+        self.t.start()
+
+    def submit(self, item) -> Future:
+        f: Future = Future()
+        with self.cv:
+            self.q.append((item, f))
+            self.cv.notify()
+        return f
+
+    def _loop(self):
+        while not self.stop:
+            with self.cv:
+                while not self.q and not self.stop:
+                    self.cv.wait()
+                deadline = time.perf_counter() + self.max_delay
+                while len(self.q) < self.max_batch and not self.stop:
+                    rem = deadline - time.perf_counter()
+                    if rem <= 0:
+                        break
+                    self.cv.wait(rem)
+                batch, self.q = self.q[: self.max_batch], self.q[self.max_batch:]
+            if not batch:
+                continue
+            try:
+                res = self.fn([b[0] for b in batch])
+                for (_, f), r in zip(batch, res):
+                    f.set_result(r)
+            except Exception as e:  # propagate to every waiter
+                for _, f in batch:
+                    f.set_exception(e)
+
+    def close(self):
+        with self.cv:
+            self.stop = True
+            self.cv.notify_all()

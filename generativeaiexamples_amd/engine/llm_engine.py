@@ -1,0 +1,364 @@
+"""Generator engine: continuous batching over the native scheduler, paged KV, HIP-graph decode.
+
+Replaces the LLM NIM (TRT-LLM / vLLM inside ``nvcr.io/nim/meta/llama3-8b-instruct``, SURVEY S1,
+call stack §3.3 steps 3.1.2: tokenize -> prefill -> decode loop -> detokenize -> SSE delta).
+
+One :meth:`LLMEngine.step`:
+  1. ``_rt.Scheduler.schedule()`` (C++) picks decodes + prefill chunks under the token budget and
+     flattens them into int32 arrays (token ids, positions, KV slots, varlen metadata);
+  2. the arrays go to the GPU in ONE pinned host->device copy;
+  3. the model runs (decode-only steps replay a captured HIP graph for the padded batch size);
+  4. the gfx950 sampler draws one token per finished-prompt / decode row;
+  5. tokens come back to the host, stop conditions (EOS, stop ids, stop strings, max_tokens) are
+     applied and text deltas are produced by the incremental detokenizer.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.common import ForwardBatch
+from .kv_cache import KVCache
+from .sampling import SamplingBatch, SamplingParams
+from .tokenizer import IncrementalDetokenizer, Tokenizer
+
+
+def _rt():
+    from .. import _rt as m  # native runtime (C++), built by generativeaiexamples_amd._build
+
+    return m
+
+
+@dataclass
+class EngineConfig:
+    max_num_seqs: int = 256
+    max_batched_tokens: int = 16384
+    max_model_len: int = 8192
+    prefill_chunk: int = 16384
+    num_blocks: Optional[int] = None
+    kv_memory_fraction: float = 0.80      # of the HBM left after weights
+    kv_memory_bytes: Optional[int] = None
+    prefix_cache: bool = True
+    use_graphs: bool = True
+    graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+
+
+@dataclass
+class Request:
+    request_id: str
+    prompt_ids: List[int]
+    params: SamplingParams
+    seq_id: int
+    detok: IncrementalDetokenizer
+    arrival: float = field(default_factory=time.perf_counter)
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    output_ids: List[int] = field(default_factory=list)
+    finished: bool = False
+    finish_reason: Optional[str] = None
+    seed: int = 0
+    token_counts: Dict[int, int] = field(default_factory=dict)
+
+    @property
+    def text(self) -> str:
+        return self.detok.text
+
+    @property
+    def ttft(self) -> Optional[float]:
+        return None if self.first_token_time is None else self.first_token_time - self.arrival
+
+
+@dataclass
+class RequestOutput:
+    request_id: str
+    token_id: int
+    delta: str
+    finished: bool
+    finish_reason: Optional[str] = None
+
+
+class LLMEngine:
+    def __init__(self, model, tokenizer: Tokenizer, cfg: EngineConfig | None = None):
+        self.model, self.tok = model, tokenizer
+        self.cfg = cfg = cfg or EngineConfig()
+        self.device = model.device
+        mc = model.cfg
+        cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
+        self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
+        nb = cfg.num_blocks or self._blocks_from_memory()
+        # one extra block, never handed out, is the scratch page of padded graph rows
+        self.kv = KVCache(mc.num_layers, nb + 1, model.hkv, mc.head_dim, self.device, model.dtype)
+        self.pad_block = nb
+        self.sched = _rt().Scheduler(nb, cfg.max_num_seqs, cfg.max_batched_tokens, cfg.max_model_len,
+                                     cfg.prefix_cache, cfg.prefill_chunk)
+        self.decode_ws = None
+        if self.device.type == "cuda":
+            self.decode_ws = ops.DecodeWorkspace(max(cfg.max_num_seqs, max(cfg.graph_batch_sizes)), model.hq,
+                                                 mc.head_dim, cfg.max_model_len, self.device)
+        self.requests: Dict[int, Request] = {}
+        self.by_rid: Dict[str, Request] = {}
+        self._ids = itertools.count(1)
+        self.step_count = 0
+        self.graphs: Dict[int, tuple] = {}
+        self.lock = threading.RLock()
+        self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0)
+        self.eos = set(mc.eos_token_ids) | set(getattr(tokenizer, "eos_ids", ()) or ())
+
+    # ------------------------------------------------------------------ memory
+    def _blocks_from_memory(self) -> int:
+        mc = self.model.cfg
+        if self.cfg.kv_memory_bytes:
+            nbytes = self.cfg.kv_memory_bytes
+        elif self.device.type == "cuda":
+            free, _total = torch.cuda.mem_get_info(self.device)
+            nbytes = int(free * self.cfg.kv_memory_fraction)
+        else:
+            nbytes = 256 << 20
+        nb = KVCache.blocks_for_memory(nbytes, mc.num_layers, self.model.hkv, mc.head_dim, self.model.dtype)
+        return max(nb, 2 * self.max_blocks_per_seq)
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, prompt_ids: List[int], params: SamplingParams | None = None,
+                    request_id: Optional[str] = None) -> Request:
+        params = params or SamplingParams()
+        with self.lock:
+            sid = next(self._ids)
+            rid = request_id or f"req-{sid}"
+            max_new = max(0, min(params.max_tokens, self.cfg.max_model_len - len(prompt_ids)))
+            if len(prompt_ids) >= self.cfg.max_model_len:
+                # keep the tail (reference truncates retrieved context the same way: truncate="END")
+                prompt_ids = prompt_ids[-(self.cfg.max_model_len - 1):]
+                max_new = 1
+            req = Request(rid, list(prompt_ids), params, sid, IncrementalDetokenizer(self.tok, params.stop),
+                          seed=params.seed if params.seed is not None else (sid * 7919) & 0x7FFFFFFF)
+            self.requests[sid] = req
+            self.by_rid[rid] = req
+            if max_new == 0:
+                req.finished, req.finish_reason = True, "length"
+                return req
+            self.sched.add(sid, req.prompt_ids, max_new)
+            return req
+
+    def abort(self, request_id: str) -> bool:
+        with self.lock:
+            req = self.by_rid.pop(request_id, None)
+            if req is None:
+                return False
+            self.sched.abort(req.seq_id)
+            self.requests.pop(req.seq_id, None)
+            req.finished, req.finish_reason = True, "abort"
+            return True
+
+    def has_work(self) -> bool:
+        return self.sched.has_work()
+
+    # ------------------------------------------------------------------ batch construction
+    def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
+        sizes = [a.size for a in arrays]
+        flat = np.concatenate([a.reshape(-1).astype(np.int32, copy=False) for a in arrays]) if arrays else np.zeros(0, np.int32)
+        t = torch.from_numpy(flat)
+        if self.device.type == "cuda":
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        out, o = [], 0
+        for a, n in zip(arrays, sizes):
+            out.append(t[o:o + n].view(*a.shape) if a.ndim > 1 else t[o:o + n])
+            o += n
+        return out
+
+    def _make_batch(self, b) -> tuple:
+        P = b.num_prefill_tokens
+        samples = b.prefill_samples
+        cu = b.cu_q
+        rows, seq_order = [], []
+        for i, sid in enumerate(b.prefill_seq_ids):
+            if samples[i]:
+                rows.append(int(cu[i + 1]) - 1)
+                seq_order.append(sid)
+        for j, sid in enumerate(b.decode_seq_ids):
+            rows.append(P + j)
+            seq_order.append(sid)
+        arrs = [b.token_ids, b.positions, b.slots, cu, b.prefill_ctx, b.prefill_block_tables, b.decode_ctx,
+                b.decode_block_tables, np.asarray(rows, dtype=np.int32)]
+        if P > 0:
+            q_lens = b.prefill_qlen
+            rpt = ops.prefill_rows_per_tile(self.model.hq, self.model.hkv)
+            tiles = np.asarray([(i, s) for i, n in enumerate(q_lens) for s in range(0, n, rpt)], dtype=np.int32)
+            arrs.append(tiles)
+        dev = self._to_device(arrs)
+        fb = ForwardBatch(token_ids=dev[0], positions=dev[1], slots=dev[2], num_prefill_tokens=P)
+        if P > 0:
+            fb.cu_q, fb.prefill_ctx, fb.prefill_block_tables = dev[3], dev[4], dev[5]
+            fb.prefill_qlen = list(b.prefill_qlen)
+            fb.prefill_tiles = dev[9].reshape(-1)
+        if len(b.decode_seq_ids):
+            fb.decode_ctx, fb.decode_block_tables = dev[6], dev[7]
+            fb.max_decode_ctx = int(b.decode_ctx.max())
+        fb.sample_rows = dev[8].long()
+        return fb, seq_order
+
+    # ------------------------------------------------------------------ HIP graphs (decode)
+    def _graph_bucket(self, n: int) -> Optional[int]:
+        for s in self.cfg.graph_batch_sizes:
+            if s >= n:
+                return s
+        return None
+
+    def _capture(self, bs: int):
+        mc = self.model.cfg
+        d = self.device
+        ids = torch.zeros(bs, dtype=torch.int32, device=d)
+        pos = torch.zeros(bs, dtype=torch.int32, device=d)
+        slots = torch.full((bs,), self.pad_block * ops.BLOCK, dtype=torch.int32, device=d)
+        ctx = torch.ones(bs, dtype=torch.int32, device=d)
+        bt = torch.full((bs, self.max_blocks_per_seq), self.pad_block, dtype=torch.int32, device=d)
+        fb = ForwardBatch(token_ids=ids, positions=pos, slots=slots, num_prefill_tokens=0, decode_ctx=ctx,
+                          decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
+        s = torch.cuda.Stream(device=d)
+        s.wait_stream(torch.cuda.current_stream(d))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.model.forward(fb, self.kv, self.decode_ws)
+        torch.cuda.current_stream(d).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            logits = self.model.forward(fb, self.kv, self.decode_ws)
+        self.graphs[bs] = (g, fb, logits)
+        del mc
+
+    def capture_graphs(self, max_bs: Optional[int] = None):
+        if self.device.type != "cuda" or not self.cfg.use_graphs:
+            return
+        for bs in self.cfg.graph_batch_sizes:
+            if bs <= (max_bs or self.cfg.max_num_seqs):
+                self._capture(bs)
+
+    def _run_graph(self, b, n: int):
+        bs = self._graph_bucket(n)
+        if bs not in self.graphs:
+            self._capture(bs)
+        g, fb, logits = self.graphs[bs]
+        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx])
+        fb.token_ids[:n].copy_(src[0])
+        fb.positions[:n].copy_(src[1])
+        fb.slots[:n].copy_(src[2])
+        fb.decode_ctx[:n].copy_(src[3])
+        mb = b.max_blocks
+        bt = self._to_device([b.decode_block_tables])[0]
+        fb.decode_block_tables[:n, :mb].copy_(bt)
+        if n < bs:  # padded rows: scratch page, ctx 1
+            fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
+            fb.decode_ctx[n:].fill_(1)
+            fb.decode_block_tables[n:, 0].fill_(self.pad_block)
+        g.replay()
+        self.stats["graph_steps"] += 1
+        return logits[:n]
+
+    # ------------------------------------------------------------------ step
+    @torch.inference_mode()
+    def step(self) -> List[RequestOutput]:
+        with self.lock:
+            b = self.sched.schedule()
+            n_tok = b.num_tokens
+            if n_tok == 0:
+                return []
+            self.step_count += 1
+            self.stats["steps"] += 1
+            P = b.num_prefill_tokens
+            self.stats["prefill_tokens"] += P
+            self.stats["decode_tokens"] += n_tok - P
+            nd = len(b.decode_seq_ids)
+            if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
+                    and self._graph_bucket(nd) is not None):
+                seq_order = list(b.decode_seq_ids)
+                logits = self._run_graph(b, nd)
+            else:
+                fb, seq_order = self._make_batch(b)
+                if not seq_order:
+                    self.model.forward(fb, self.kv, self.decode_ws)
+                    return []
+                logits = self.model.forward(fb, self.kv, self.decode_ws)
+            reqs = [self.requests.get(s) for s in seq_order]
+            params = [r.params if r else SamplingParams() for r in reqs]
+            self._penalize(logits, reqs)
+            sb = SamplingBatch(params, [r.seed if r else 0 for r in reqs], self.device)
+            toks = ops.sample(logits, sb.temperature, sb.top_p, sb.top_k, sb.seeds, self.step_count)
+            toks = toks.cpu().tolist()
+            return self._process(seq_order, reqs, toks)
+
+    def _penalize(self, logits, reqs):
+        rows = [i for i, r in enumerate(reqs) if r is not None and r.params.has_penalty and r.token_counts]
+        if not rows:
+            return
+        m = max(len(reqs[i].token_counts) for i in rows)
+        ids = np.zeros((len(reqs), m), np.int32)
+        cnt = np.zeros((len(reqs), m), np.int32)
+        n = np.zeros(len(reqs), np.int32)
+        f = np.zeros(len(reqs), np.float32)
+        p = np.zeros(len(reqs), np.float32)
+        rp = np.ones(len(reqs), np.float32)
+        for i in rows:
+            r = reqs[i]
+            k = list(r.token_counts.items())
+            ids[i, : len(k)] = [a for a, _ in k]
+            cnt[i, : len(k)] = [c for _, c in k]
+            n[i] = len(k)
+            f[i], p[i], rp[i] = r.params.frequency_penalty, r.params.presence_penalty, r.params.repetition_penalty
+        d = self.device
+        ops.apply_penalties(logits, *(torch.from_numpy(a).to(d) for a in (ids, cnt, n)),
+                            *(torch.from_numpy(a).to(d) for a in (f, p, rp)))
+
+    def _process(self, seq_order, reqs, toks) -> List[RequestOutput]:
+        outs: List[RequestOutput] = []
+        cont_ids, cont_toks = [], []
+        now = time.perf_counter()
+        for sid, req, t in zip(seq_order, reqs, toks):
+            if req is None or req.finished:
+                continue
+            if req.first_token_time is None:
+                req.first_token_time = now
+            req.output_ids.append(t)
+            if req.params.has_penalty:
+                req.token_counts[t] = req.token_counts.get(t, 0) + 1
+            ntok = len(req.output_ids)
+            reason = None
+            is_eos = (t in self.eos and not req.params.ignore_eos) or t in req.params.stop_token_ids
+            if is_eos and ntok > req.params.min_tokens:
+                reason = "stop"
+                delta = req.detok.flush()
+            else:
+                delta = req.detok.add(t)
+                if req.detok.stopped:
+                    reason = "stop"
+                elif ntok >= req.params.max_tokens or len(req.prompt_ids) + ntok >= self.cfg.max_model_len:
+                    reason = "length"
+                if reason:
+                    delta += req.detok.flush()
+            if reason:
+                req.finished, req.finish_reason, req.finish_time = True, reason, now
+                self.sched.finish(sid)
+                self.requests.pop(sid, None)
+                self.by_rid.pop(req.request_id, None)
+            else:
+                cont_ids.append(sid)
+                cont_toks.append(t)
+            outs.append(RequestOutput(req.request_id, t, delta, reason is not None, reason))
+        if cont_ids:
+            self.sched.append_tokens(cont_ids, cont_toks)
+        return outs
+
+    # ------------------------------------------------------------------ offline API
+    def generate(self, prompts: List[List[int]], params: SamplingParams | List[SamplingParams] | None = None
+                 ) -> List[Request]:
+        ps = params if isinstance(params, list) else [params or SamplingParams()] * len(prompts)
+        reqs = [self.add_request(p, sp) for p, sp in zip(prompts, ps)]
+        while self.has_work():
+            self.step()
+        return reqs

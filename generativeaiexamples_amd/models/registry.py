@@ -1,0 +1,102 @@
+"""Model presets -> (model, tokenizer). Weights come from a local HF directory (safetensors +
+tokenizer.json) when given, else random init of the real architecture (benchmarks / offline)."""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from ..engine.tokenizer import Tokenizer, bert_byte_tokenizer, load_tokenizer, llama3_byte_tokenizer, small_byte_tokenizer
+from .bert import BertConfig, BertModel
+from .llama import LlamaConfig, LlamaModel
+from .opt import OPTConfig, OPTModel
+
+LLM_PRESETS = {
+    "llama3-8b": ("meta/llama3-8b-instruct", lambda: LlamaConfig.llama3_8b()),
+    "llama3-70b": ("meta/llama3-70b-instruct", lambda: LlamaConfig.llama3_70b()),
+    "llama3.1-8b": ("meta/llama-3.1-8b-instruct", lambda: LlamaConfig.llama31_8b()),
+    "mistral-7b": ("mistralai/mistral-7b-instruct-v0.3", lambda: LlamaConfig.mistral_7b()),
+    "tiny-llama": ("tiny-llama", lambda: LlamaConfig.tiny(max_position=4096)),
+    "opt-125m": ("facebook/opt-125m", lambda: OPTConfig.opt_125m()),
+}
+
+ENCODER_PRESETS = {
+    "e5-large-v2": ("nvidia/nv-embedqa-e5-v5", lambda: BertConfig.e5_large_v2()),
+    "e5-base-v2": ("intfloat/e5-base-v2", lambda: BertConfig.e5_base_v2()),
+    "tiny-e5": ("tiny-e5", lambda: BertConfig.tiny()),
+}
+
+RERANKER_PRESETS = {
+    "bge-reranker-large": ("nv-rerank-qa-mistral-4b:1", lambda: BertConfig.bge_reranker_large()),
+    "tiny-reranker": ("tiny-reranker", lambda: BertConfig.tiny(num_labels=1, pooling="cls", normalize=False)),
+}
+
+
+def _is_hf_dir(p: Optional[str]) -> bool:
+    return bool(p) and os.path.isfile(os.path.join(p, "config.json"))
+
+
+def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=None, seed: int = 0):
+    """-> (model, tokenizer, served_name)."""
+    if _is_hf_dir(weights):
+        import json
+
+        arch = json.load(open(os.path.join(weights, "config.json"))).get("model_type", "llama")
+        if arch == "opt":
+            m = OPTModel(OPTConfig.from_hf(weights), device=device)
+        else:
+            m = LlamaModel(LlamaConfig.from_hf(weights), device=device)
+        m.load_safetensors_dir(weights) if hasattr(m, "load_safetensors_dir") else _load_st(m, weights)
+        tok = load_tokenizer(weights, "llama3", m.cfg.vocab_size)
+        return m, tok, os.path.basename(weights.rstrip("/"))
+    name, mk = LLM_PRESETS[preset]
+    cfg = mk()
+    if isinstance(cfg, OPTConfig):
+        m = OPTModel(cfg, device=device).random_init(seed)
+        tok: Tokenizer = small_byte_tokenizer(512) if cfg.vocab_size < 1000 else _opt_tok(cfg.vocab_size)
+    else:
+        m = LlamaModel(cfg, device=device).random_init(seed)
+        tok = llama3_byte_tokenizer(cfg.vocab_size) if cfg.vocab_size >= 128256 else small_byte_tokenizer(cfg.vocab_size) \
+            if cfg.vocab_size <= 4096 else _generic_tok(cfg)
+    return m, tok, name
+
+
+def _opt_tok(vocab):
+    from ..engine.tokenizer import ByteTokenizer
+
+    return ByteTokenizer(vocab, 4, {"<s>": 2, "</s>": 2, "<pad>": 1}, bos="<s>", eos=("</s>",), pad="<pad>")
+
+
+def _generic_tok(cfg):
+    from ..engine.tokenizer import ByteTokenizer
+
+    return ByteTokenizer(cfg.vocab_size, 3, {"<s>": 1, "</s>": 2}, bos="<s>", eos=("</s>",))
+
+
+def _load_st(m, path):
+    from safetensors.torch import load_file
+
+    sd = {}
+    for f in sorted(os.listdir(path)):
+        if f.endswith(".safetensors"):
+            sd.update(load_file(os.path.join(path, f)))
+    m.load_hf_state(sd)
+
+
+def build_encoder(preset: str = "e5-large-v2", weights: Optional[str] = None, device=None, seed: int = 0,
+                  reranker: bool = False) -> Tuple[BertModel, Tokenizer, str]:
+    if _is_hf_dir(weights):
+        cfg = BertConfig.from_hf(weights)
+        m = BertModel(cfg, device=device)
+        _load_st(m, weights)
+        return m, load_tokenizer(weights, "bert", cfg.vocab_size), os.path.basename(weights.rstrip("/"))
+    table = RERANKER_PRESETS if reranker else ENCODER_PRESETS
+    name, mk = table[preset]
+    cfg = mk()
+    m = BertModel(cfg, device=device).random_init(seed)
+    return m, bert_byte_tokenizer(cfg.vocab_size), name
+
+
+def default_device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")

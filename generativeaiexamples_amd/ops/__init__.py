@@ -20,6 +20,14 @@ _C = None
 _C_ERR: Exception | None = None
 
 
+def _into(out, y):
+    """CPU path: honour a caller-provided output buffer."""
+    if out is None:
+        return y
+    out.copy_(y.reshape(out.shape))
+    return out
+
+
 def native():
     """Return the loaded native module (raises if unavailable)."""
     global _C, _C_ERR
@@ -59,7 +67,7 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[to
              out: Optional[torch.Tensor] = None):
     """y = rmsnorm(x [+ residual]) * w. With ``residual``, it is updated in place to x + residual."""
     if not x.is_cuda:
-        return ref.rms_norm(x, w, eps, residual)
+        return _into(out, ref.rms_norm(x, w, eps, residual))
     out = torch.empty_like(x) if out is None else out
     native().rmsnorm(x, w, eps, out, residual, residual)
     return out
@@ -67,7 +75,7 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[to
 
 def layer_norm(x, w, b, eps, residual=None, out=None):
     if not x.is_cuda:
-        return ref.layer_norm(x, w, b, eps, residual)
+        return _into(out, ref.layer_norm(x, w, b, eps, residual))
     out = torch.empty_like(x) if out is None else out
     native().layernorm(x, w, b, eps, out, residual, residual)
     return out
@@ -84,7 +92,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     act: None | 'gelu' | 'relu' | 'swiglu' (w interleaved per 16 rows, see interleave_gate_up).
     """
     if not x.is_cuda:
-        return ref.linear(x, w, bias, residual, act, out_dtype)
+        return _into(out, ref.linear(x, w, bias, residual, act, out_dtype))
     K = x.shape[-1]
     N = w.shape[0]
     lead = x.shape[:-1]
@@ -142,7 +150,7 @@ def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device) -> tor
 def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, tiles=None,
                       q_lens: Sequence[int] | None = None, out=None):
     if not q.is_cuda:
-        return ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal)
+        return _into(out, ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal))
     Hq, Hkv = q.shape[1], k_cache.shape[1]
     if tiles is None:
         if q_lens is None:
@@ -173,7 +181,7 @@ class DecodeWorkspace:
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
                      max_ctx: int | None = None, out=None):
     if not q.is_cuda:
-        return ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+        return _into(out, ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale))
     B, Hq, D = q.shape
     if ws is None:
         mc = max_ctx if max_ctx is not None else int(ctx_lens.max())
@@ -234,7 +242,7 @@ def sim_topk(Q: torch.Tensor, X: torch.Tensor, bias: torch.Tensor, n_rows: int, 
 # ---------------------------------------------------------------------------------------------
 def embedding(ids, table, vstart: int = 0, vend: int | None = None, out=None):
     if not ids.is_cuda:
-        return ref.embedding(ids, table, vstart, vend)
+        return _into(out, ref.embedding(ids, table, vstart, vend))
     vend = table.shape[0] + vstart if vend is None else vend
     out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=ids.device) if out is None else out
     native().embedding(ids.int().contiguous() if ids.dtype != torch.int32 else ids, table, out, vstart, vend)

@@ -1,0 +1,133 @@
+"""Process groups and collectives.
+
+MI355X topology: 8 GPUs, fully connected by xGMI, 7 point-to-point links of
+~153 GB/s per GPU. One process per GPU; ``torch.distributed`` with backend ``nccl`` is RCCL on
+ROCm. Sub-groups: ``tp`` (generator tensor parallel), ``dp`` (embedder / index shards) and ``ep``
+(MoE experts). Collectives are issued on the current stream; the engine places them on a
+separate high-priority stream when it overlaps communication with compute.
+
+On the CPU test tier the same code runs over ``gloo`` (world_size 2, 127.0.0.1 rendezvous).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    tp_size: int = 1
+    dp_size: int = 1
+    backend: str = "none"
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    tp_group: Optional[object] = None
+    dp_group: Optional[object] = None
+    world_group: Optional[object] = None
+
+    @property
+    def tp_rank(self) -> int:
+        return self.rank % self.tp_size
+
+    @property
+    def dp_rank(self) -> int:
+        return self.rank // self.tp_size
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    # ---------------- collectives (no-ops when the group has one member) ----------------
+    def tp_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            dist.all_reduce(t, group=self.tp_group)
+        return t
+
+    def tp_all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate the per-rank shards along the last dim (vocab-parallel logits)."""
+        if self.tp_size == 1:
+            return t
+        parts = [torch.empty_like(t) for _ in range(self.tp_size)]
+        dist.all_gather(parts, t.contiguous(), group=self.tp_group)
+        return torch.cat(parts, dim=-1)
+
+    def all_gather_obj(self, obj, group=None):
+        if not self.is_distributed:
+            return [obj]
+        out = [None] * (dist.get_world_size(group) if group is not None else self.world_size)
+        dist.all_gather_object(out, obj, group=group)
+        return out
+
+    def barrier(self):
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+
+_CTX: DistContext | None = None
+
+
+def get_context() -> DistContext:
+    global _CTX
+    if _CTX is None:
+        _CTX = DistContext()
+        if torch.cuda.is_available():
+            _CTX.device = torch.device("cuda", 0)
+    return _CTX
+
+
+def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int = 600) -> DistContext:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+
+    Falls back to a single-process context when WORLD_SIZE is unset or 1.
+    """
+    global _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend if world > 1 else "none")
+    if use_gpu:
+        torch.cuda.set_device(local)
+        ctx.device = torch.device("cuda", local)
+    if world > 1:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = ctx.device
+            dist.init_process_group(**kw)
+        assert world % tp_size == 0, "world size must be a multiple of tp_size"
+        ctx.tp_size, ctx.dp_size = tp_size, world // tp_size
+        ctx.world_group = dist.group.WORLD
+        # every rank must create every group in the same order
+        for d in range(ctx.dp_size):
+            ranks = list(range(d * tp_size, (d + 1) * tp_size))
+            g = dist.new_group(ranks) if tp_size > 1 else None
+            if rank in ranks:
+                ctx.tp_group = g
+        for t in range(tp_size):
+            ranks = list(range(t, world, tp_size))
+            g = dist.new_group(ranks) if ctx.dp_size > 1 else None
+            if rank in ranks:
+                ctx.dp_group = g
+    _CTX = ctx
+    return ctx
+
+
+def shutdown():
+    global _CTX
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None

@@ -1,0 +1,42 @@
+"""Deterministic synthetic corpus and query set (no datasets offline).
+
+Chunk ``i`` is a reproducible pseudo-random word sequence of ~``chunk_tokens`` tokens (the
+reference splits documents into 510-token chunks, compose uses 506; configuration.py:86-90,
+basic_rag/langchain/docker-compose.yaml:40-41). Text is generated on demand from the row id, so
+a 10M-row index needs no host storage for its documents.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..index.hbm_index import Document
+
+_WORDS = (
+    "accelerator bandwidth cache kernel wavefront matrix tensor memory latency throughput cluster "
+    "pipeline retrieval embedding vector index query document passage context answer model layer "
+    "attention softmax gradient batch token sequence prefix decode prefill schedule router replica "
+    "shard collective reduce gather scatter stream graph launch compiler register buffer queue "
+    "policy service request response latency budget quality recall precision benchmark report "
+    "network storage compute energy thermal clock frequency voltage power board rack node fabric"
+).split()
+
+
+def chunk_text(row: int, chunk_tokens: int = 506, bytes_per_token: float = 1.0) -> str:
+    rng = np.random.default_rng(row * 2654435761 % (1 << 32))
+    target = int(chunk_tokens * bytes_per_token)
+    parts, n = [], 0
+    while n < target:
+        w = _WORDS[int(rng.integers(len(_WORDS)))]
+        parts.append(w)
+        n += len(w) + 1
+    return " ".join(parts)[:target]
+
+
+def chunk_document(row: int, chunk_tokens: int = 506) -> Document:
+    return Document(chunk_text(row, chunk_tokens), {"filename": f"synthetic_{row // 64:07d}.txt", "row": row})
+
+
+def question(i: int) -> str:
+    rng = np.random.default_rng(i + 12345)
+    a, b = (_WORDS[int(x)] for x in rng.integers(len(_WORDS), size=2))
+    return f"What does the report say about the {a} of the {b} in section {i % 97}?"

@@ -1,0 +1,49 @@
+"""``python -m generativeaiexamples_amd.serving`` - the NIM-compatible model server (port 8000).
+
+Equivalent of the reference's ``nemollm-inference`` + ``nemollm-embedding`` + ``ranking-ms``
+containers in one MI355X process. Example:
+
+    python -m generativeaiexamples_amd.serving --llm llama3-8b --embedder e5-large-v2 \\
+        --reranker bge-reranker-large --port 8000
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--llm", default=os.environ.get("APP_ENGINE_LLM", "llama3-8b"))
+    ap.add_argument("--llm-weights", default=os.environ.get("APP_ENGINE_LLMWEIGHTS"))
+    ap.add_argument("--embedder", default=os.environ.get("APP_ENGINE_EMBEDDER", "e5-large-v2"))
+    ap.add_argument("--embedder-weights", default=os.environ.get("APP_ENGINE_EMBEDDERWEIGHTS"))
+    ap.add_argument("--reranker", default=os.environ.get("APP_ENGINE_RERANKER"))
+    ap.add_argument("--reranker-weights", default=os.environ.get("APP_ENGINE_RERANKERWEIGHTS"))
+    ap.add_argument("--served-model-name", default=None)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--lora", action="append", default=[], help="adapter name served as an alias of the base model")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--device", default=None)
+    a = ap.parse_args()
+    logging.basicConfig(level=os.environ.get("LOGLEVEL", "INFO").upper())
+
+    import uvicorn
+
+    from .hub import HubSpec, ServiceHub
+    from .openai_api import create_openai_app
+
+    spec = HubSpec(llm=a.llm or None, llm_weights=a.llm_weights, embedder=a.embedder or None,
+                   embedder_weights=a.embedder_weights, reranker=a.reranker, reranker_weights=a.reranker_weights,
+                   served_llm_name=a.served_model_name, max_num_seqs=a.max_num_seqs, max_model_len=a.max_model_len,
+                   use_graphs=not a.no_graphs, lora_adapters={n: "" for n in a.lora}, device=a.device)
+    hub = ServiceHub.build(spec)
+    uvicorn.run(create_openai_app(hub), host=a.host, port=a.port, log_level="info")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+"""Asynchronous front of the generator engine for HTTP serving.
+
+A single background thread owns the GPU and runs ``LLMEngine.step()`` whenever there is work;
+HTTP handlers only enqueue requests and await per-request ``asyncio.Queue`` s that the engine
+thread feeds through ``loop.call_soon_threadsafe``. The event loop therefore never blocks on
+GPU work (fixes the reference's event-loop blocking), and a client
+disconnect aborts its request (frees its KV blocks) immediately.
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+from typing import AsyncIterator, Dict, List, Optional
+
+from ..engine.llm_engine import LLMEngine, RequestOutput
+from ..engine.sampling import SamplingParams
+from ..utils.metrics import METRICS
+
+
+@dataclass
+class StreamItem:
+    delta: str
+    token_id: int
+    finished: bool
+    finish_reason: Optional[str]
+
+
+class AsyncLLMEngine:
+    def __init__(self, engine: LLMEngine):
+        self.engine = engine
+        self.queues: Dict[str, tuple] = {}
+        self.cv = threading.Condition()
+        self.running = True
+        self.healthy = True
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
+        self.thread.start()
+
+    @property
+    def tokenizer(self):
+        return self.engine.tok
+
+    def _loop(self):
+        eng = self.engine
+        while self.running:
+            with self.cv:
+                while self.running and not eng.has_work():
+                    self.cv.wait(0.05)
+            if not self.running:
+                break
+            try:
+                t0 = time.perf_counter()
+                outs = eng.step()
+                METRICS.observe_step(time.perf_counter() - t0, len(outs))
+            except BaseException as e:  # engine failure: fail every pending request, keep serving health
+                self.error, self.healthy = e, False
+                for rid, (loop, q) in list(self.queues.items()):
+                    loop.call_soon_threadsafe(q.put_nowait, e)
+                self.queues.clear()
+                continue
+            for o in outs:
+                ent = self.queues.get(o.request_id)
+                if ent is None:
+                    continue
+                loop, q = ent
+                loop.call_soon_threadsafe(q.put_nowait, o)
+                if o.finished:
+                    self.queues.pop(o.request_id, None)
+
+    async def generate(self, prompt_ids: List[int], params: SamplingParams,
+                       request_id: Optional[str] = None) -> AsyncIterator[StreamItem]:
+        rid = request_id or f"cmpl-{uuid.uuid4().hex}"
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        self.queues[rid] = (loop, q)
+        t0 = time.perf_counter()
+        first = True
+        with self.cv:
+            req = self.engine.add_request(prompt_ids, params, rid)
+            self.cv.notify()
+        METRICS.requests_total.inc()
+        METRICS.prompt_tokens.inc(len(prompt_ids))
+        if req.finished:  # zero-budget request
+            self.queues.pop(rid, None)
+            yield StreamItem("", -1, True, req.finish_reason)
+            return
+        try:
+            while True:
+                o = await q.get()
+                if isinstance(o, BaseException):
+                    raise RuntimeError(f"engine failure: {o!r}")
+                assert isinstance(o, RequestOutput)
+                if first:
+                    METRICS.ttft.observe(time.perf_counter() - t0)
+                    first = False
+                METRICS.generation_tokens.inc()
+                yield StreamItem(o.delta, o.token_id, o.finished, o.finish_reason)
+                if o.finished:
+                    METRICS.e2e.observe(time.perf_counter() - t0)
+                    return
+        finally:
+            if rid in self.queues:  # client went away or error: free the sequence now
+                self.queues.pop(rid, None)
+                with self.cv:
+                    self.engine.abort(rid)
+
+    async def complete(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None):
+        text, ids, reason = [], [], None
+        async for it in self.generate(prompt_ids, params, request_id):
+            text.append(it.delta)
+            if it.token_id >= 0:
+                ids.append(it.token_id)
+            reason = it.finish_reason
+        return "".join(text), ids, reason
+
+    def shutdown(self):
+        self.running = False
+        with self.cv:
+            self.cv.notify_all()
+        self.thread.join(timeout=5)
