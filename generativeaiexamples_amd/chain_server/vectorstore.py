@@ -1,0 +1,102 @@
+"""Vector-store facade over the HBM index (the LangChain VectorStore / LlamaIndex VectorStoreIndex
+roles of the reference: ``add_documents``, ``similarity_search_with_relevance_scores``,
+``as_retriever(search_type="similarity_score_threshold")``, delete and list by filename).
+Collections are named (``COLLECTION_NAME`` env, ``conv_store`` for multi-turn memory) and each is
+one :class:`HBMIndex`, optionally persisted (snapshot + WAL) under ``APP_VECTORSTORE_PERSISTDIR``."""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from typing import Dict, List, Optional, Tuple
+
+from ..index.hbm_index import Document, HBMIndex
+from ..utils.metrics import METRICS
+from .connectors import Embeddings
+
+log = logging.getLogger(__name__)
+
+
+class Retriever:
+    def __init__(self, store: "VectorStore", k: int = 4, score_threshold: Optional[float] = None):
+        self.store, self.k, self.threshold = store, k, score_threshold
+
+    def get_relevant_documents(self, query: str) -> List[Document]:
+        return [d for d, _ in self.store.similarity_search_with_relevance_scores(query, self.k, self.threshold)]
+
+    invoke = get_relevant_documents
+
+
+class VectorStore:
+    def __init__(self, name: str, embeddings: Embeddings, metric: str = "cosine", device=None,
+                 persist_dir: Optional[str] = None, batch: int = 256):
+        self.name, self.emb, self.batch = name, embeddings, batch
+        self.persist = os.path.join(persist_dir, name) if persist_dir else None
+        self.lock = threading.Lock()
+        if self.persist and os.path.exists(os.path.join(self.persist, "index.json")):
+            self.index = HBMIndex.load(self.persist, device=device)
+            log.info("loaded collection %s (%d vectors) from %s", name, len(self.index), self.persist)
+        else:
+            self.index = HBMIndex(embeddings.dim or 1024, metric, device=device, name=name)
+        if self.persist:
+            self.index.attach_wal(self.persist)
+
+    def add_documents(self, docs: List[Document]) -> List[int]:
+        rows: List[int] = []
+        for i in range(0, len(docs), self.batch):
+            part = docs[i:i + self.batch]
+            vecs = self.emb.embed_tensor([d.page_content for d in part], "passage")
+            if self.index.dim != vecs.shape[1] and len(self.index) == 0:
+                self.index = HBMIndex(vecs.shape[1], self.index.metric, device=self.index.device, name=self.name)
+            rows += self.index.add(vecs, part)
+        if self.persist:
+            self.index.save(self.persist)
+        return rows
+
+    add_texts = lambda self, texts, metadatas=None: self.add_documents(  # noqa: E731
+        [Document(t, (metadatas or [{}] * len(texts))[i]) for i, t in enumerate(texts)])
+
+    def similarity_search_with_relevance_scores(self, query: str, k: int = 4,
+                                                score_threshold: Optional[float] = None) -> List[Tuple[Document, float]]:
+        import time
+
+        t0 = time.perf_counter()
+        q = self.emb.embed_tensor([query], "query")
+        hits = self.index.search(q, k, score_threshold)[0]
+        METRICS.search.observe(time.perf_counter() - t0)
+        return [(h.document, h.score) for h in hits]
+
+    def similarity_search(self, query: str, k: int = 4) -> List[Document]:
+        return [d for d, _ in self.similarity_search_with_relevance_scores(query, k)]
+
+    def as_retriever(self, search_type: str = "similarity", k: int = 4, score_threshold: Optional[float] = None):
+        return Retriever(self, k, score_threshold if search_type == "similarity_score_threshold" else None)
+
+    def delete_filename(self, filename: str) -> bool:
+        n = self.index.delete_filename(filename)
+        if self.persist and n:
+            self.index.save(self.persist)
+        return n > 0
+
+    def filenames(self) -> List[str]:
+        return self.index.filenames()
+
+    def __len__(self):
+        return len(self.index)
+
+
+_STORES: Dict[str, VectorStore] = {}
+_LOCK = threading.Lock()
+
+
+def get_store(name: str, embeddings: Embeddings, metric: str = "cosine", persist_dir: Optional[str] = None,
+              device=None) -> VectorStore:
+    with _LOCK:
+        if name not in _STORES:
+            _STORES[name] = VectorStore(name, embeddings, metric, device, persist_dir)
+        return _STORES[name]
+
+
+def reset_stores():
+    with _LOCK:
+        _STORES.clear()

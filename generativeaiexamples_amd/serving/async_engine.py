@@ -13,7 +13,7 @@ import threading
 import time
 import uuid
 from dataclasses import dataclass
-from typing import AsyncIterator, Dict, List, Optional
+from typing import AsyncIterator, Dict, Iterator, List, Optional
 
 from ..engine.llm_engine import LLMEngine, RequestOutput
 from ..engine.sampling import SamplingParams
@@ -103,6 +103,47 @@ class AsyncLLMEngine:
                     return
         finally:
             if rid in self.queues:  # client went away or error: free the sequence now
+                self.queues.pop(rid, None)
+                with self.cv:
+                    self.engine.abort(rid)
+
+    def generate_sync(self, prompt_ids: List[int], params: SamplingParams,
+                      request_id: Optional[str] = None) -> Iterator[StreamItem]:
+        """Blocking streaming API for worker threads (chain-server example pipelines)."""
+        import queue as _q
+
+        rid = request_id or f"cmpl-{uuid.uuid4().hex}"
+        q: _q.Queue = _q.Queue()
+
+        class _Shim:  # duck-types the (loop, queue) pair used by the engine thread
+            @staticmethod
+            def call_soon_threadsafe(fn, item):
+                q.put(item)
+
+        self.queues[rid] = (_Shim, q)
+        t0 = time.perf_counter()
+        with self.cv:
+            req = self.engine.add_request(prompt_ids, params, rid)
+            self.cv.notify()
+        METRICS.requests_total.inc()
+        if req.finished:
+            self.queues.pop(rid, None)
+            yield StreamItem("", -1, True, req.finish_reason)
+            return
+        first = True
+        try:
+            while True:
+                o = q.get()
+                if isinstance(o, BaseException):
+                    raise RuntimeError(f"engine failure: {o!r}")
+                if first:
+                    METRICS.ttft.observe(time.perf_counter() - t0)
+                    first = False
+                yield StreamItem(o.delta, o.token_id, o.finished, o.finish_reason)
+                if o.finished:
+                    return
+        finally:
+            if rid in self.queues:
                 self.queues.pop(rid, None)
                 with self.cv:
                     self.engine.abort(rid)

@@ -1,0 +1,99 @@
+"""NIM/OpenAI-compatible /v1 API contract on tiny CPU models: chat (stream / non-stream / usage),
+completions, embeddings (input_type, truncate, base64), ranking, models, health, tool-call parsing."""
+import base64
+import json
+import struct
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def client():
+    from fastapi.testclient import TestClient
+
+    from generativeaiexamples_amd.serving.hub import HubSpec, ServiceHub
+    from generativeaiexamples_amd.serving.openai_api import create_openai_app
+
+    hub = ServiceHub.build(HubSpec(llm="tiny-llama", embedder="tiny-e5", reranker="tiny-reranker", device="cpu",
+                                   served_llm_name="meta/llama3-8b-instruct", served_embedder_name="NV-Embed-QA",
+                                   max_num_seqs=8, max_model_len=1024, lora_adapters={"my-lora": ""}))
+    with TestClient(create_openai_app(hub)) as c:
+        yield c
+    hub.shutdown()
+
+
+def test_models_and_health(client):
+    r = client.get("/v1/models").json()
+    ids = {m["id"] for m in r["data"]}
+    assert {"meta/llama3-8b-instruct", "NV-Embed-QA", "my-lora"} <= ids
+    assert client.get("/v1/health/ready").status_code == 200
+    assert client.get("/v1/health/live").json()["message"] == "Service is live."
+    assert b"gai_requests_total" in client.get("/metrics").content
+
+
+def test_chat_non_stream(client):
+    r = client.post("/v1/chat/completions", json={"model": "meta/llama3-8b-instruct", "max_tokens": 5,
+                                                   "temperature": 0, "messages": [{"role": "user", "content": "hi"}]})
+    assert r.status_code == 200, r.text
+    j = r.json()
+    assert j["object"] == "chat.completion" and j["choices"][0]["message"]["role"] == "assistant"
+    assert j["choices"][0]["finish_reason"] in ("length", "stop")
+    assert j["usage"]["completion_tokens"] <= 5 and j["usage"]["total_tokens"] > j["usage"]["prompt_tokens"]
+
+
+def test_chat_stream(client):
+    r = client.post("/v1/chat/completions", json={"model": "my-lora", "max_tokens": 6, "stream": True,
+                                                   "stream_options": {"include_usage": True},
+                                                   "messages": [{"role": "system", "content": "be brief"},
+                                                                {"role": "user", "content": "hello"}]})
+    assert r.status_code == 200
+    lines = [ln for ln in r.text.split("\n\n") if ln]
+    assert all(ln.startswith("data: ") for ln in lines)
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(ln[6:]) for ln in lines[:-1]]
+    assert chunks[0]["choices"][0]["delta"]["role"] == "assistant"
+    assert any(c["choices"] and c["choices"][0]["finish_reason"] for c in chunks)
+    assert "usage" in chunks[-1]
+
+
+def test_completions(client):
+    r = client.post("/v1/completions", json={"prompt": "Once upon", "max_tokens": 4, "temperature": 0})
+    j = r.json()
+    assert j["object"] == "text_completion" and len(j["choices"]) == 1
+    assert j["usage"]["completion_tokens"] <= 4
+
+
+def test_embeddings(client):
+    r = client.post("/v1/embeddings", json={"input": ["a", "bb"], "model": "NV-Embed-QA", "input_type": "passage"})
+    j = r.json()
+    assert len(j["data"]) == 2 and j["data"][1]["index"] == 1
+    v = j["data"][0]["embedding"]
+    assert abs(sum(x * x for x in v) - 1.0) < 1e-2
+    r = client.post("/v1/embeddings", json={"input": "q", "encoding_format": "base64", "input_type": "query"})
+    raw = base64.b64decode(r.json()["data"][0]["embedding"])
+    assert len(raw) == 4 * len(v)
+    assert client.post("/v1/embeddings", json={"input": "q", "input_type": "bogus"}).status_code == 400
+    long = "x" * 5000
+    assert client.post("/v1/embeddings", json={"input": long, "truncate": "NONE"}).status_code == 400
+    assert client.post("/v1/embeddings", json={"input": long, "truncate": "END"}).status_code == 200
+
+
+def test_ranking(client):
+    r = client.post("/v1/ranking", json={"model": "x", "query": {"text": "q"},
+                                         "passages": [{"text": "a"}, {"text": "b b"}, {"text": "c c c"}]})
+    rk = r.json()["rankings"]
+    assert sorted(x["index"] for x in rk) == [0, 1, 2]
+    assert rk[0]["logit"] >= rk[-1]["logit"]
+    r2 = client.post("/v1/retrieval/nvidia/reranking", json={"query": {"text": "q"}, "passages": [{"text": "a"}]})
+    assert r2.status_code == 200
+
+
+def test_tool_call_parsing():
+    from generativeaiexamples_amd.serving.openai_api import parse_tool_calls
+
+    tools = [{"type": "function", "function": {"name": "get_weather", "parameters": {}}}]
+    calls = parse_tool_calls('{"name": "get_weather", "parameters": {"city": "Austin"}}', tools)
+    assert calls[0]["function"]["name"] == "get_weather"
+    assert json.loads(calls[0]["function"]["arguments"]) == {"city": "Austin"}
+    assert parse_tool_calls("no tools here", tools) is None
+    assert parse_tool_calls('{"name": "other", "parameters": {}}', tools) is None
