@@ -188,6 +188,36 @@ void sim_topk(const Tensor& Q, const Tensor& X, const Tensor& bias, int64_t n_ro
                cur_stream());
 }
 
+void moe_route(const Tensor& logits, int64_t k, bool renorm, Tensor& ids, Tensor& w) {
+  check_f32(logits, "router logits");
+  check_i32(ids, "topk ids");
+  check_f32(w, "topk weights");
+  gai_moe_route(logits.data_ptr<float>(), logits.size(0), logits.size(1), k, renorm ? 1 : 0, ids.data_ptr<int>(),
+                w.data_ptr<float>(), cur_stream());
+}
+
+void moe_gemm(const Tensor& A, const optional<Tensor>& a_rows, const Tensor& W, Tensor& C, const Tensor& offs,
+              int64_t rows_total, bool swiglu) {
+  check_bf16(A, "A");
+  check_bf16(W, "W");
+  check_bf16(C, "C");
+  check_i32(offs, "expert offsets");
+  if (a_rows) check_i32(*a_rows, "a_rows");
+  TORCH_CHECK(W.dim() == 3 && W.size(2) == A.size(-1), "moe_gemm: W must be [E, N, K]");
+  gai_moe_gemm(A.data_ptr(), a_rows ? a_rows->data_ptr<int>() : nullptr, W.data_ptr(), C.data_ptr(),
+               offs.data_ptr<int>(), W.size(0), rows_total, W.size(1), W.size(2), swiglu ? 1 : 0, cur_stream());
+}
+
+void moe_combine(const Tensor& Y, const Tensor& pos, const Tensor& w, const optional<Tensor>& residual, Tensor& out) {
+  check_bf16(Y, "Y");
+  check_i32(pos, "pos");
+  check_f32(w, "w");
+  check_bf16(out, "out");
+  const int T = pos.size(0), k = pos.size(1), D = out.size(-1);
+  gai_moe_combine(Y.data_ptr(), pos.data_ptr<int>(), w.data_ptr<float>(), opt_ptr(residual), out.data_ptr(), T, k, D,
+                  cur_stream());
+}
+
 void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart, int64_t vend) {
   check_i32(ids, "ids");
   check_bf16(table, "table");
@@ -212,6 +242,14 @@ void silu_mul(const Tensor& x, Tensor& y) {
   gai_silu_mul(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
 }
 
+void silu_mul_interleaved(const Tensor& x, Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  const int I = y.size(-1);
+  TORCH_CHECK(I % 16 == 0 && x.size(-1) == 2 * I, "silu_mul_interleaved: bad widths");
+  gai_silu_mul_interleaved(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
+}
+
 void gelu(const Tensor& x, Tensor& y) {
   check_bf16(x, "x");
   check_bf16(y, "y");
@@ -234,9 +272,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("apply_penalties", &apply_penalties);
   m.def("sim_topk", &sim_topk);
   m.def("topk_cap", [](int64_t k) { return gai_topk_cap(k); });
+  m.def("moe_route", &moe_route);
+  m.def("moe_gemm", &moe_gemm);
+  m.def("moe_combine", &moe_combine);
   m.def("embedding", &embedding);
   m.def("pool", &pool);
   m.def("silu_mul", &silu_mul);
   m.def("gelu", &gelu);
+  m.def("silu_mul_interleaved", &silu_mul_interleaved);
   m.attr("ARCH") = "gfx950";
 }

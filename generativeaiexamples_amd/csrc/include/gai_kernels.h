@@ -17,7 +17,7 @@ void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, co
                        void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, hipStream_t st);
 
 // gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu;
-//            force: 0 auto, 1 skinny, 2 tiled)
+//            force: 0 auto, 1 skinny, 2 tiled 128x128, 3 large 256x256)
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
               int epi, int out_f32, int force, hipStream_t st);
 
@@ -41,8 +41,16 @@ int gai_topk_cap(int k);
 void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,
                   int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st);
 
+// moe.hip
+void gai_moe_route(const float* logits, int T, int E, int k, int renorm, int* ids, float* w, hipStream_t st);
+void gai_moe_gemm(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E, int rows_total,
+                  int N, int K, int swiglu, hipStream_t st);
+void gai_moe_combine(const void* Y, const int* pos, const float* w, const void* residual, void* out, int T, int k,
+                     int D, hipStream_t st);
+
 // misc.hip
 void gai_embedding(const int* ids, const void* table, void* out, int T, int D, int vstart, int vend, hipStream_t st);
 void gai_pool(const void* h, const int* cu, float* out, int B, int D, int mode, int normalize, hipStream_t st);
 void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_gelu(const void* x, void* y, int T, int I, hipStream_t st);
+void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t st);

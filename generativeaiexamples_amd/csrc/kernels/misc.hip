@@ -71,7 +71,13 @@ __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf
   if (e >= (long)T * units) return;
   const int t = (int)(e / units), u = (int)(e % units);
   bf16x8 o;
-  if (MODE == 0) {
+  if (MODE == 2) {  // gate/up interleaved per 16 columns (the fused-SwiGLU weight layout)
+    const int c = u * 8, p = c >> 4, c0 = c & 15;
+    const bf16x8 g = load8(x + (size_t)t * 2 * I + 32 * p + c0);
+    const bf16x8 up = load8(x + (size_t)t * 2 * I + 32 * p + 16 + c0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(silu((float)g[j]) * (float)up[j]);
+  } else if (MODE == 0) {
     const bf16x8 g = load8(x + (size_t)t * 2 * I + u * 8);
     const bf16x8 up = load8(x + (size_t)t * 2 * I + I + u * 8);
 #pragma unroll
@@ -104,6 +110,13 @@ void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st) {
   if (T == 0) return;
   const long n = (long)T * (I / 8);
   act_kernel<0><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)x, (bf16*)y, T, I);
+  GAI_LAUNCH_CHECK();
+}
+
+void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t st) {
+  if (T == 0) return;
+  const long n = (long)T * (I / 8);
+  act_kernel<2><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)x, (bf16*)y, T, I);
   GAI_LAUNCH_CHECK();
 }
 

@@ -168,11 +168,7 @@ class LlamaModel:
             put(p + "qkv", torch.cat([q, k, v]))
             o = sd[h + "self_attn.o_proj.weight"]
             put(p + "o", o.reshape(o.shape[0], tp, -1)[:, r] if tp > 1 else o)
-            g = shard_rows(sd[h + "mlp.gate_proj.weight"], c.intermediate_size)
-            u = shard_rows(sd[h + "mlp.up_proj.weight"], c.intermediate_size)
-            put(p + "gate_up", ops.interleave_gate_up(g, u))
-            dn = sd[h + "mlp.down_proj.weight"]
-            put(p + "down", dn.reshape(dn.shape[0], tp, -1)[:, r] if tp > 1 else dn)
+            self._load_mlp(sd, i)
         put("norm", sd["model.norm.weight"])
         if not c.tie_embeddings:
             lm = sd["lm_head.weight"]
@@ -180,6 +176,42 @@ class LlamaModel:
                 lm = torch.cat([lm, lm.new_zeros(pad, lm.shape[1])])
             put("lm_head", shard_rows(lm, lm.shape[0]))
         return self
+
+    def _load_mlp(self, sd: Dict[str, torch.Tensor], i: int):
+        c, tp, r = self.cfg, self.ctx.tp_size, self.ctx.tp_rank
+        p, h = f"l{i}.", f"model.layers.{i}."
+
+        def shard_rows(t, n):
+            return t.reshape(tp, n // tp, *t.shape[1:])[r] if tp > 1 else t
+
+        g = shard_rows(sd[h + "mlp.gate_proj.weight"], c.intermediate_size)
+        u = shard_rows(sd[h + "mlp.up_proj.weight"], c.intermediate_size)
+        self.w[p + "gate_up"].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
+        dn = sd[h + "mlp.down_proj.weight"]
+        self.w[p + "down"].copy_((dn.reshape(dn.shape[0], tp, -1)[:, r] if tp > 1 else dn).to(self.dtype))
+
+    def export_hf_state(self) -> Dict[str, torch.Tensor]:
+        """Inverse of load_hf_state for a TP=1 model (checkpoint export, TP-reshard tests)."""
+        assert self.ctx.tp_size == 1
+        c, hd, w = self.cfg, self.cfg.head_dim, self.w
+        sd = {"model.embed_tokens.weight": w["embed"].clone(), "model.norm.weight": w["norm"].clone()}
+        if not c.tie_embeddings:
+            sd["lm_head.weight"] = w["lm_head"].clone()
+        nq, nk = c.num_heads * hd, c.num_kv_heads * hd
+        for i in range(c.num_layers):
+            p, h = f"l{i}.", f"model.layers.{i}."
+            qkv = w[p + "qkv"]
+            sd[h + "self_attn.q_proj.weight"] = qkv[:nq].clone()
+            sd[h + "self_attn.k_proj.weight"] = qkv[nq:nq + nk].clone()
+            sd[h + "self_attn.v_proj.weight"] = qkv[nq + nk:].clone()
+            sd[h + "self_attn.o_proj.weight"] = w[p + "o"].clone()
+            gu = w[p + "gate_up"].reshape(-1, 2, 16, c.hidden_size)
+            sd[h + "mlp.gate_proj.weight"] = gu[:, 0].reshape(-1, c.hidden_size).clone()
+            sd[h + "mlp.up_proj.weight"] = gu[:, 1].reshape(-1, c.hidden_size).clone()
+            sd[h + "mlp.down_proj.weight"] = w[p + "down"].clone()
+            sd[h + "input_layernorm.weight"] = w[p + "attn_norm"].clone()
+            sd[h + "post_attention_layernorm.weight"] = w[p + "mlp_norm"].clone()
+        return sd
 
     def load_safetensors_dir(self, path: str):
         from safetensors.torch import load_file
@@ -207,14 +239,17 @@ class LlamaModel:
         c, w, ctx = self.cfg, self.w, self.ctx
         T, P = fb.num_tokens, fb.num_prefill_tokens
         hd = c.head_dim
-        tp0 = ctx.tp_rank == 0
-        h = ops.embedding(fb.token_ids, w["embed"], self.vstart, self.vstart + self.vocab_local)
-        ctx.tp_all_reduce(h)
-        q = torch.empty(T, self.hq, hd, device=h.device, dtype=self.dtype)
+        # residual stream `res` is updated in place by the fused add+RMSNorm kernel, so the O and down
+        # projections are plain GEMMs (row-parallel partial sums all-reduced before the add)
+        res = ops.embedding(fb.token_ids, w["embed"], self.vstart, self.vstart + self.vocab_local)
+        ctx.tp_all_reduce(res)
+        q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
         attn = torch.empty_like(q)
+        h = None
         for i in range(c.num_layers):
             p = f"l{i}."
-            x = ops.rms_norm(h, w[p + "attn_norm"], c.rms_eps)
+            x = ops.rms_norm(res, w[p + "attn_norm"], c.rms_eps) if h is None else \
+                ops.rms_norm(h, w[p + "attn_norm"], c.rms_eps, residual=res)
             qkv = ops.linear(x, w[p + "qkv"])
             kc, vc = kv.layer(i)
             ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True)
@@ -224,15 +259,16 @@ class LlamaModel:
             if T > P:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
                                      max_ctx=fb.max_decode_ctx, out=attn[P:])
-            h = ops.linear(attn.view(T, -1), w[p + "o"], residual=h if tp0 else None)
+            h = ops.linear(attn.view(T, -1), w[p + "o"])
             ctx.tp_all_reduce(h)
-            x = ops.rms_norm(h, w[p + "mlp_norm"], c.rms_eps)
+            x = ops.rms_norm(h, w[p + "mlp_norm"], c.rms_eps, residual=res)
             g = ops.linear(x, w[p + "gate_up"], act="swiglu")
-            h = ops.linear(g, w[p + "down"], residual=h if tp0 else None)
+            h = ops.linear(g, w[p + "down"])
             ctx.tp_all_reduce(h)
         if fb.sample_rows is not None:
             h = h.index_select(0, fb.sample_rows)
-        x = ops.rms_norm(h, w["norm"], c.rms_eps)
+            res = res.index_select(0, fb.sample_rows)
+        x = ops.rms_norm(h, w["norm"], c.rms_eps, residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
         logits = ctx.tp_all_gather_last(logits)
         return logits[:, : c.vocab_size]

@@ -1,0 +1,188 @@
+"""Mixtral-8x7B family (sparse MoE decoder; BASELINE config 5).
+
+Attention is the Llama block. The MLP is a top-2-of-8 mixture: router GEMM (fp32 logits) ->
+``moe_route`` (softmax, top-k, renormalise) -> device-side dispatch plan (expert-sorted rows, no
+host sync) -> grouped GEMM w1|w3 with the SwiGLU epilogue gathering token rows -> grouped GEMM w2
+-> weighted combine (+ residual). 47B parameters = 94 GB bf16: fits ONE 288 GB MI355X.
+
+Expert parallelism: experts are sharded over the TP group (rank r owns experts
+[r*E/tp, (r+1)*E/tp)); hidden states are replicated by the attention all-reduce, so each rank
+computes only the (token, expert) pairs it owns and the row-parallel all-reduce sums the expert
+outputs - no extra collective. :mod:`..parallel.ep` provides the all-to-all dispatch/combine for
+data-parallel attention + EP.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict
+
+import torch
+
+from .. import ops
+from .common import ForwardBatch, randn_like_
+from .llama import LlamaConfig, LlamaModel
+
+
+@dataclass
+class MixtralConfig(LlamaConfig):
+    num_experts: int = 8
+    top_k: int = 2
+
+    @staticmethod
+    def mixtral_8x7b(**kw):
+        return MixtralConfig(name="mistralai/mixtral-8x7b-instruct-v0.1", vocab_size=32000, rope_theta=1e6,
+                             max_position=32768, bos_token_id=1, eos_token_ids=(2,), **kw)
+
+    @staticmethod
+    def tiny_moe(**kw):
+        base = dict(vocab_size=512, hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4, num_kv_heads=2,
+                    head_dim=64, max_position=2048, bos_token_id=1, eos_token_ids=(2,), name="tiny-moe",
+                    num_experts=4, top_k=2)
+        base.update(kw)
+        return MixtralConfig(**base)
+
+
+class MixtralModel(LlamaModel):
+    def _alloc(self):
+        c = self.cfg
+        tp, r = self.ctx.tp_size, self.ctx.tp_rank
+        assert c.num_experts % tp == 0, "experts must divide the TP/EP group"
+        self.e_local = c.num_experts // tp
+        self.e_start = r * self.e_local
+        # the dense MLP of LlamaModel is replaced by experts: allocate attention etc. via the parent,
+        # then drop its MLP weights
+        inter = self.inter
+        self.inter = 16  # tiny placeholder for the parent allocation
+        super()._alloc()
+        self.inter = inter
+        d, dt, D, I = self.device, self.dtype, c.hidden_size, c.intermediate_size
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            del self.w[p + "gate_up"], self.w[p + "down"]
+            self.w[p + "router"] = torch.empty(c.num_experts, D, device=d, dtype=dt)
+            self.w[p + "w13"] = torch.empty(self.e_local, 2 * I, D, device=d, dtype=dt)  # interleaved per 16
+            self.w[p + "w2"] = torch.empty(self.e_local, D, I, device=d, dtype=dt)
+
+    def random_init(self, seed: int = 0):
+        s = seed * 1000 + self.ctx.tp_rank
+        for k, t in self.w.items():
+            if k.endswith("norm"):
+                t.fill_(1.0)
+            elif k in ("embed",):
+                randn_like_(t, s, 0.02)
+            else:
+                randn_like_(t, s, 1.0 / math.sqrt(t.shape[-1]))
+            s += 1
+        return self
+
+    def _load_mlp(self, sd: Dict[str, torch.Tensor], i: int):
+        p, h = f"l{i}.", f"model.layers.{i}.block_sparse_moe."
+        self.w[p + "router"].copy_(sd[h + "gate.weight"].to(self.dtype))
+        for j in range(self.e_local):
+            e = self.e_start + j
+            g, u = sd[h + f"experts.{e}.w1.weight"], sd[h + f"experts.{e}.w3.weight"]
+            self.w[p + "w13"][j].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
+            self.w[p + "w2"][j].copy_(sd[h + f"experts.{e}.w2.weight"].to(self.dtype))
+
+    def moe_mlp(self, x: torch.Tensor, layer: int, residual: torch.Tensor | None) -> torch.Tensor:
+        c, w, p = self.cfg, self.w, f"l{layer}."
+        T = x.shape[0]
+        logits = ops.linear(x, w[p + "router"], out_dtype=torch.float32)
+        ids, wts = ops.moe_route(logits, c.top_k, True)
+        k = c.top_k
+        if self.e_local != c.num_experts:  # EP: keep only local experts; others -> sentinel bin, weight 0
+            loc = ids - self.e_start
+            mine = (loc >= 0) & (loc < self.e_local)
+            ids = torch.where(mine, loc, torch.full_like(loc, self.e_local)).to(torch.int32)
+            wts = torch.where(mine, wts, torch.zeros_like(wts))
+            a_rows, offs, pos = ops.moe_dispatch(ids, self.e_local + 1)
+        else:
+            a_rows, offs, pos = ops.moe_dispatch(ids, c.num_experts)
+        h1 = ops.moe_gemm(x, a_rows, w[p + "w13"], offs, T * k, swiglu=True)
+        y = ops.moe_gemm(h1, None, w[p + "w2"], offs, T * k, swiglu=False) if self.e_local == c.num_experts else \
+            self._moe_down_ep(h1, w[p + "w2"], offs, T * k)
+        return ops.moe_combine(y, pos, wts, residual)
+
+    def _moe_down_ep(self, h1, w2, offs, rows):
+        y = ops.moe_gemm(h1, None, w2, offs, rows, swiglu=False)
+        # rows of non-local pairs were never written: zero them (their combine weight is 0)
+        valid = torch.arange(rows, device=y.device) < offs[self.e_local].to(torch.int64)
+        return torch.where(valid[:, None], y, torch.zeros((), dtype=y.dtype, device=y.device))
+
+    def forward(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
+        c, w, ctx = self.cfg, self.w, self.ctx
+        T, P = fb.num_tokens, fb.num_prefill_tokens
+        hd = c.head_dim
+        res = ops.embedding(fb.token_ids, w["embed"], self.vstart, self.vstart + self.vocab_local)
+        ctx.tp_all_reduce(res)
+        q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
+        attn = torch.empty_like(q)
+        h = None
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            x = ops.rms_norm(res, w[p + "attn_norm"], c.rms_eps) if h is None else \
+                ops.rms_norm(h, w[p + "attn_norm"], c.rms_eps, residual=res)
+            qkv = ops.linear(x, w[p + "qkv"])
+            kc, vc = kv.layer(i)
+            ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True)
+            if P > 0:
+                ops.attention_prefill(q[:P], kc, vc, fb.prefill_block_tables, fb.cu_q, fb.prefill_ctx, self.scale,
+                                      True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P])
+            if T > P:
+                ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
+                                     max_ctx=fb.max_decode_ctx, out=attn[P:])
+            h = ops.linear(attn.view(T, -1), w[p + "o"])
+            ctx.tp_all_reduce(h)
+            x = ops.rms_norm(h, w[p + "mlp_norm"], c.rms_eps, residual=res)
+            h = self.moe_mlp(x, i, None)
+            ctx.tp_all_reduce(h)
+        if fb.sample_rows is not None:
+            h = h.index_select(0, fb.sample_rows)
+            res = res.index_select(0, fb.sample_rows)
+        x = ops.rms_norm(h, w["norm"], c.rms_eps, residual=res)
+        logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
+        logits = ctx.tp_all_gather_last(logits)
+        return logits[:, : c.vocab_size]
+
+    @torch.no_grad()
+    def reference_forward(self, token_ids: torch.Tensor) -> torch.Tensor:
+        """Dense fp32 oracle (TP=1)."""
+        c = self.cfg
+        wf = {k: v.float().cpu() for k, v in self.w.items()}
+        T, hd = token_ids.numel(), c.head_dim
+        h = wf["embed"][token_ids.long().cpu()]
+        cs = self.cos_sin.cpu()[:T]
+        cos, sin = cs[:, None, : hd // 2], cs[:, None, hd // 2:]
+
+        def rope(t):
+            a, b = t[..., : hd // 2], t[..., hd // 2:]
+            return torch.cat([a * cos - b * sin, b * cos + a * sin], -1)
+
+        def rms(x, g):
+            return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_eps) * g
+
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            x = rms(h, wf[p + "attn_norm"])
+            qkv = (x @ wf[p + "qkv"].t()).view(T, self.hq + 2 * self.hkv, hd)
+            q, k_, v = qkv[:, : self.hq], qkv[:, self.hq: self.hq + self.hkv], qkv[:, self.hq + self.hkv:]
+            q, k_ = rope(q), rope(k_)
+            rep = self.hq // self.hkv
+            k_, v = k_.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1)
+            att = torch.einsum("qhd,khd->hqk", q, k_) * self.scale
+            att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1)[None], float("-inf"))
+            h = h + torch.einsum("hqk,khd->qhd", att.softmax(-1), v).reshape(T, -1) @ wf[p + "o"].t()
+            x = rms(h, wf[p + "mlp_norm"])
+            pr = (x @ wf[p + "router"].t()).softmax(-1)
+            tw, ti = torch.topk(pr, c.top_k, -1)
+            tw = tw / tw.sum(-1, keepdim=True)
+            out = torch.zeros_like(x)
+            for t in range(T):
+                for j in range(c.top_k):
+                    e = int(ti[t, j])
+                    gu = (x[t] @ wf[p + "w13"][e].t()).reshape(-1, 2, 16)
+                    g = (torch.nn.functional.silu(gu[:, 0]) * gu[:, 1]).reshape(-1)
+                    out[t] += tw[t, j] * (g @ wf[p + "w2"][e].t())
+            h = h + out
+        return rms(h, wf["norm"]) @ wf["lm_head"].t()

@@ -55,9 +55,7 @@ def native_available() -> bool:
 
 
 EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6}
-_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
-# Plain (epilogue-free) GEMMs may use hipBLASLt when GAI_PLAIN_GEMM=hipblaslt; fused ones are always native.
-_PLAIN_GEMM = os.environ.get("GAI_PLAIN_GEMM", "native")
+_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "large": 3}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -112,17 +110,101 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         epi, ncol = (EPI["bias_residual"] if bias is not None else EPI["residual"]), N
     else:
         epi, ncol = (EPI["bias"] if bias is not None else 0), N
-    if epi == 0 and _PLAIN_GEMM == "hipblaslt" and out is None and out_dtype == x.dtype:
-        return torch.matmul(x, w.t())
-    if out is None:
-        out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
     if M == 0:
-        return out
+        return torch.empty(*lead, ncol, dtype=out_dtype, device=x.device) if out is None else out
     x2 = x.reshape(M, K)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
+    if residual is None and out is None and TUNER.pick(M, N, K, act, bias is not None, out_dtype, x2, w) == "blas":
+        return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
+    if out is None:
+        out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
     native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE)
     return out
+
+
+def _blas_linear(x2, w, bias, act, out_dtype):
+    """hipBLASLt GEMM (plain library GEMM) + the framework's own elementwise epilogue kernel."""
+    y = torch.addmm(bias, x2, w.t()) if bias is not None else torch.mm(x2, w.t())
+    if act == "swiglu":
+        z = torch.empty(y.shape[0], y.shape[1] // 2, dtype=y.dtype, device=y.device)
+        native().silu_mul_interleaved(y, z)
+        y = z
+    elif act == "gelu":
+        z = torch.empty_like(y)
+        native().gelu(y, z)
+        y = z
+    elif act == "relu":
+        y = torch.relu_(y)
+    return y if out_dtype == y.dtype else y.to(out_dtype)
+
+
+class GemmTuner:
+    """Per-shape choice between the hand-written MFMA GEMM (fused epilogue) and hipBLASLt + an
+    elementwise epilogue kernel, decided by timing both on the first call of each (M-bucket, N, K,
+    epilogue) outside graph capture (engines warm their shapes up before capturing). Policy via
+    GAI_GEMM_POLICY = tune (default) | native | hipblaslt."""
+
+    def __init__(self):
+        self.mode = os.environ.get("GAI_GEMM_POLICY", "tune")
+        self.cache: dict = {}
+        self.log: list = []
+
+    @staticmethod
+    def bucket(M: int) -> int:
+        b = 1
+        while b < M:
+            b *= 2
+        return min(b, 1 << 16)
+
+    def heuristic(self, M, N, K, act, out_dtype) -> str:
+        if out_dtype == torch.float32:
+            return "native"
+        return "native" if M <= 8 else "blas"
+
+    def pick(self, M, N, K, act, has_bias, out_dtype, x2, w) -> str:
+        if self.mode == "native":
+            return "native"
+        if self.mode == "hipblaslt":
+            return "blas"
+        key = (self.bucket(M), N, K, act, has_bias, out_dtype)
+        got = self.cache.get(key)
+        if got is not None:
+            return got
+        if torch.cuda.is_current_stream_capturing():
+            return self.heuristic(M, N, K, act, out_dtype)
+        got = self._measure(x2, w, act, has_bias, out_dtype, M, N)
+        self.cache[key] = got
+        return got
+
+    def _measure(self, x2, w, act, has_bias, out_dtype, M, N) -> str:
+        bias = torch.zeros(N, dtype=x2.dtype, device=x2.device) if has_bias else None
+        ncol = N // 2 if act == "swiglu" else N
+        out = torch.empty(M, ncol, dtype=out_dtype, device=x2.device)
+        epi = EPI[act] if act else (EPI["bias"] if has_bias else 0)
+
+        def run_native():
+            native().gemm(x2, w, out, bias, None, epi, _GEMM_FORCE)
+
+        def run_blas():
+            _blas_linear(x2, w, bias, act, out_dtype)
+
+        ts = {}
+        for name, fn in (("native", run_native), ("blas", run_blas)):
+            fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                fn()
+            e.record()
+            e.synchronize()
+            ts[name] = s.elapsed_time(e) / 3
+        best = min(ts, key=ts.get)
+        self.log.append({"M": M, "N": N, "K": x2.shape[1], "act": act, "bias": has_bias, **ts, "pick": best})
+        return best
+
+
+TUNER = GemmTuner()
 
 
 # ---------------------------------------------------------------------------------------------
@@ -246,6 +328,49 @@ def embedding(ids, table, vstart: int = 0, vend: int | None = None, out=None):
     vend = table.shape[0] + vstart if vend is None else vend
     out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=ids.device) if out is None else out
     native().embedding(ids.int().contiguous() if ids.dtype != torch.int32 else ids, table, out, vstart, vend)
+    return out
+
+
+def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):
+    """Router softmax + top-k -> (expert ids int32 [T,k], weights fp32 [T,k])."""
+    if not logits.is_cuda:
+        return ref.moe_route(logits, k, renorm)
+    T = logits.shape[0]
+    ids = torch.empty(T, k, dtype=torch.int32, device=logits.device)
+    w = torch.empty(T, k, dtype=torch.float32, device=logits.device)
+    native().moe_route(logits.float().contiguous(), k, renorm, ids, w)
+    return ids, w
+
+
+def moe_dispatch(ids: torch.Tensor, num_experts: int):
+    """Expert-sorted dispatch plan without host sync: (a_rows [T*k], offsets [E+1], pos [T,k])."""
+    T, k = ids.shape
+    flat = ids.reshape(-1).long()
+    order = torch.argsort(flat, stable=True)
+    a_rows = (order // k).to(torch.int32)
+    counts = torch.zeros(num_experts, dtype=torch.int64, device=ids.device).scatter_add_(0, flat, torch.ones_like(flat))
+    offs = torch.zeros(num_experts + 1, dtype=torch.int32, device=ids.device)
+    offs[1:] = counts.cumsum(0).to(torch.int32)
+    pos = torch.empty(T * k, dtype=torch.int32, device=ids.device)
+    pos[order] = torch.arange(T * k, dtype=torch.int32, device=ids.device)
+    return a_rows, offs, pos.view(T, k)
+
+
+def moe_gemm(A, a_rows, W, offs, rows_total: int, swiglu: bool):
+    """Grouped expert GEMM over expert-sorted rows (A rows gathered through a_rows when given)."""
+    if not A.is_cuda:
+        return ref.moe_gemm(A, a_rows, W, offs, rows_total, swiglu)
+    N = W.shape[1]
+    C = torch.empty(rows_total, N // 2 if swiglu else N, dtype=A.dtype, device=A.device)
+    native().moe_gemm(A.contiguous(), a_rows, W, C, offs, rows_total, swiglu)
+    return C
+
+
+def moe_combine(Y, pos, w, residual=None):
+    if not Y.is_cuda:
+        return ref.moe_combine(Y, pos, w, residual)
+    out = torch.empty(pos.shape[0], Y.shape[1], dtype=Y.dtype, device=Y.device)
+    native().moe_combine(Y, pos, w, residual, out)
     return out
 
 

@@ -220,6 +220,35 @@ def sim_topk(Q, X, bias, n_rows, k):
     return v, i
 
 
+def moe_route(logits, k, renorm=True):
+    p = logits.float().softmax(-1)
+    w, ids = torch.topk(p, k, dim=-1)
+    if renorm:
+        w = w / w.sum(-1, keepdim=True)
+    return ids.int(), w
+
+
+def moe_gemm(A, a_rows, W, offs, rows_total, swiglu):
+    E, N, K = W.shape
+    outw = N // 2 if swiglu else N
+    C = torch.empty(rows_total, outw, dtype=A.dtype)
+    o = offs.tolist()
+    for e in range(E):
+        s, t = o[e], o[e + 1]
+        if t == s:
+            continue
+        rows = a_rows[s:t].long() if a_rows is not None else torch.arange(s, t)
+        C[s:t] = linear(A[rows], W[e], act="swiglu" if swiglu else None)
+    return C
+
+
+def moe_combine(Y, pos, w, residual=None):
+    y = (Y[pos.long()].float() * w.float()[..., None]).sum(1)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(Y.dtype)
+
+
 def embedding(ids, table, vstart=0, vend=None):
     vend = table.shape[0] + vstart if vend is None else vend
     ids = ids.long()

@@ -47,7 +47,12 @@ class DistContext:
     # ---------------- collectives (no-ops when the group has one member) ----------------
     def tp_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
-            dist.all_reduce(t, group=self.tp_group)
+            if t.is_cuda or t.dtype in (torch.float32, torch.float64):
+                dist.all_reduce(t, group=self.tp_group)
+            else:  # gloo (CPU test tier): reduce reduced-precision tensors in fp32
+                f = t.float()
+                dist.all_reduce(f, group=self.tp_group)
+                t.copy_(f)
         return t
 
     def tp_all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
