@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--prefix-cache", action="store_true",
                     help="enable KV prefix caching (off by default: random-init embeddings retrieve the same "
                          "chunks for every query, so caching would skip most of the prefill work)")
+    ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache size per rank (default: 50%% of free HBM)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -114,7 +115,8 @@ def main():
                         max_model_len=min(lcfg.max_position, prompt_est + args.max_tokens + 64),
                         prefill_chunk=args.max_batched_tokens, use_graphs=not args.no_graphs,
                         prefix_cache=args.prefix_cache,
-                        kv_memory_fraction=0.5)
+                        kv_memory_fraction=0.5,
+                        kv_memory_bytes=int(args.kv_gb * (1 << 30)) if args.kv_gb else None)
     engine = LLMEngine(llm, ltok, ecfg)
     if not args.no_graphs:
         engine.capture_graphs(max_bs=args.batch)
@@ -169,9 +171,7 @@ def main():
     total = sum(times)
     # max over ranks
     if world > 1:
-        tt = torch.tensor([total], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        total = float(tt)
+        total = max(ctx.all_gather_obj(total))  # slowest rank defines the step time
         allt = ctx.all_gather_obj(ttfts)
         ttfts = [x for part in allt for x in part]
         toks = int(sum(ctx.all_gather_obj(toks)))

@@ -33,16 +33,26 @@ class ShardedIndex:
     def split_row(g: int) -> Tuple[int, int]:
         return g >> 40, g & ((1 << 40) - 1)
 
+    def _comm_dev(self, t: torch.Tensor) -> torch.device:
+        # gloo (CPU test tier / single-GPU rehearsal) only moves host tensors
+        return t.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+
+    def _all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
+        dev = self._comm_dev(t)
+        src = t.to(dev)
+        if src.dtype == torch.bfloat16 and dev.type == "cpu":
+            src = src.float()
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src.contiguous(), group=self.group)
+        return [p.to(t.device, t.dtype) for p in parts]
+
     def _gather_var(self, t: torch.Tensor) -> Tuple[torch.Tensor, List[int]]:
         n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.int64)
-        ns = [torch.zeros_like(n) for _ in range(self.world)]
-        dist.all_gather(ns, n, group=self.group)
-        counts = [int(x) for x in ns]
+        counts = [int(x) for x in self._all_gather(n)]
         mx = max(counts)
         pad = torch.zeros(mx, *t.shape[1:], dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
-        parts = [torch.empty_like(pad) for _ in range(self.world)]
-        dist.all_gather(parts, pad.contiguous(), group=self.group)
+        parts = self._all_gather(pad)
         return torch.cat([p[:c] for p, c in zip(parts, counts)]), counts
 
     def search_raw(self, queries: torch.Tensor, k: int):
@@ -58,12 +68,8 @@ class ShardedIndex:
             rel = torch.cat([rel, rel.new_full((rel.shape[0], padn), float("-inf"))], 1)
             rows = torch.cat([rows, rows.new_full((rows.shape[0], padn), -1)], 1)
         rows = torch.where(rows >= 0, self.global_row(rows, self.rank), rows)
-        parts_r = [torch.empty_like(rel) for _ in range(self.world)]
-        parts_i = [torch.empty_like(rows) for _ in range(self.world)]
-        dist.all_gather(parts_r, rel.contiguous(), group=self.group)
-        dist.all_gather(parts_i, rows.contiguous(), group=self.group)
-        R = torch.cat(parts_r, 1)  # [Q, world*k]
-        I = torch.cat(parts_i, 1)
+        R = torch.cat(self._all_gather(rel.float()), 1)  # [Q, world*k]
+        I = torch.cat(self._all_gather(rows), 1)
         top, pos = torch.topk(R, k, dim=1)
         gi = torch.gather(I, 1, pos)
         start = sum(counts[: self.rank])

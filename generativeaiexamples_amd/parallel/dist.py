@@ -101,16 +101,18 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("GAI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend if world > 1 else "none")
     if use_gpu:
-        torch.cuda.set_device(local)
-        ctx.device = torch.device("cuda", local)
+        # GAI_SINGLE_DEVICE=1: every rank on cuda:0 (gloo rehearsal of a multi-rank run on one GPU)
+        dev_idx = 0 if os.environ.get("GAI_SINGLE_DEVICE") == "1" else local
+        torch.cuda.set_device(dev_idx)
+        ctx.device = torch.device("cuda", dev_idx)
     if world > 1:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-            if backend == "nccl":
+            if backend == "nccl" and os.environ.get("GAI_SINGLE_DEVICE") != "1":
                 kw["device_id"] = ctx.device
             dist.init_process_group(**kw)
         assert world % tp_size == 0, "world size must be a multiple of tp_size"
