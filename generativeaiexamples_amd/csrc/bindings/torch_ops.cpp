@@ -196,6 +196,72 @@ void moe_route(const Tensor& logits, int64_t k, bool renorm, Tensor& ids, Tensor
                 w.data_ptr<float>(), cur_stream());
 }
 
+void patchify(const Tensor& img, int64_t P, const Tensor& mean, const Tensor& inv_std, Tensor& out) {
+  check_dev(img, "img");
+  TORCH_CHECK(img.scalar_type() == at::kFloat && img.dim() == 4 && img.is_contiguous(),
+              "patchify: img must be contiguous fp32 [B, C, H, W]");
+  check_bf16(out, "out");
+  const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
+  TORCH_CHECK(H % P == 0 && W % P == 0, "patchify: image size must be a multiple of the patch size");
+  TORCH_CHECK(mean.numel() >= C && inv_std.numel() >= C && mean.scalar_type() == at::kFloat &&
+                  inv_std.scalar_type() == at::kFloat, "patchify: mean/inv_std must be fp32 [C]");
+  const int Kp = out.size(-1);
+  TORCH_CHECK(Kp >= C * P * P && out.numel() == (int64_t)B * (H / P) * (W / P) * Kp, "patchify: out shape");
+  gai_patchify(img.data_ptr<float>(), B, C, H, W, (int)P, Kp, mean.data_ptr<float>(), inv_std.data_ptr<float>(),
+               out.data_ptr(), cur_stream());
+}
+
+void vit_embed(const Tensor& patches, const Tensor& cls, const Tensor& pos, Tensor& out, int64_t B) {
+  check_bf16(patches, "patches");
+  check_bf16(cls, "cls");
+  check_bf16(pos, "pos");
+  check_bf16(out, "out");
+  const int D = cls.numel();
+  TORCH_CHECK(D % 8 == 0, "vit_embed: dim must be a multiple of 8");
+  const int NP = patches.numel() / ((int64_t)B * D);
+  TORCH_CHECK(pos.numel() >= (int64_t)(NP + 1) * D && out.numel() == (int64_t)B * (NP + 1) * D, "vit_embed: shapes");
+  gai_vit_embed(patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), out.data_ptr(), B, NP, D, cur_stream());
+}
+
+void quant_rows_fp8(const Tensor& x, Tensor& q, Tensor& scale) {
+  check_bf16(x, "x");
+  check_dev(q, "q");
+  TORCH_CHECK(q.element_size() == 1, "quant_rows_fp8: q must be a 1-byte (fp8) tensor");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat, "quant_rows_fp8: scale must be fp32");
+  const int K = x.size(-1);
+  const int M = x.numel() / K;
+  TORCH_CHECK(x.stride(-1) == 1 && (x.dim() == 1 || x.stride(-2) >= K), "quant_rows_fp8: rows must be contiguous");
+  TORCH_CHECK(q.numel() == (int64_t)M * K && scale.numel() == M, "quant_rows_fp8: output sizes");
+  const long ldx = x.dim() > 1 ? x.stride(-2) : K;
+  gai_quant_rows_fp8(x.data_ptr(), M, K, ldx, q.data_ptr(), scale.data_ptr<float>(), cur_stream());
+}
+
+void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& sa, const Tensor& sb, Tensor& C,
+              const optional<Tensor>& bias, const optional<Tensor>& R, int64_t epi, int64_t force) {
+  check_dev(A, "A");
+  check_dev(B, "B");
+  check_dev(C, "C");
+  TORCH_CHECK(A.element_size() == 1 && B.element_size() == 1, "gemm_fp8: A and B must be fp8");
+  TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm_fp8: A and B must be contiguous");
+  const int K = A.size(-1);
+  const int M = A.numel() / K;
+  const int N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm_fp8: K mismatch");
+  TORCH_CHECK(sa.scalar_type() == at::kFloat && sa.numel() == M, "gemm_fp8: sa must be fp32 [M]");
+  TORCH_CHECK(sb.scalar_type() == at::kFloat && sb.numel() == N, "gemm_fp8: sb must be fp32 [N]");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm_fp8: C must be bf16 or fp32");
+  const int ldc = epi == 4 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm_fp8: C has wrong size");
+  if (bias) check_bf16(*bias, "bias");
+  if (R) {
+    check_bf16(*R, "residual");
+    TORCH_CHECK(R->numel() == (int64_t)M * N, "gemm_fp8: residual has wrong size");
+  }
+  gai_gemm_fp8(A.data_ptr(), B.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(), C.data_ptr(), opt_ptr(bias),
+               opt_ptr(R), M, N, K, ldc, (int)epi, f32 ? 1 : 0, (int)force, cur_stream());
+}
+
 void moe_gemm(const Tensor& A, const optional<Tensor>& a_rows, const Tensor& W, Tensor& C, const Tensor& offs,
               int64_t rows_total, bool swiglu) {
   check_bf16(A, "A");
@@ -265,6 +331,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("gemm", &gemm);
+  m.def("gemm_fp8", &gemm_fp8);
+  m.def("patchify", &patchify);
+  m.def("vit_embed", &vit_embed);
+  m.def("quant_rows_fp8", &quant_rows_fp8);
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv) { return gai_attn_prefill_rows_per_tile(hq, hkv); });
   m.def("attn_decode", &attn_decode);

@@ -16,10 +16,15 @@ void gai_layernorm(const void* x, const void* residual_in, void* residual_out, c
 void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, const int* slots, void* q_out,
                        void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, hipStream_t st);
 
-// gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu;
+// gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu, 7 bias+quick-gelu;
 //            force: 0 auto, 1 skinny, 2 tiled 128x128, 3 large 256x256)
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
               int epi, int out_f32, int force, hipStream_t st);
+
+// gemm_fp8.hip (force: 0 auto, 2 tiled 128x128, 3 large 256x256; OCP e4m3fn operands, per-row sa[M] x per-channel sb[N] scales; epi as gai_gemm + 7 bias+quick-gelu)
+void gai_gemm_fp8(const void* A, const void* B, const float* sa, const float* sb, void* C, const void* bias,
+                  const void* R, int M, int N, int K, int ldc, int epi, int out_f32, int force, hipStream_t st);
+void gai_quant_rows_fp8(const void* x, int M, int K, long ldx, void* q, float* scale, hipStream_t st);
 
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -54,3 +59,9 @@ void gai_pool(const void* h, const int* cu, float* out, int B, int D, int mode, 
 void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_gelu(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t st);
+
+// vision.hip
+void gai_patchify(const float* img, int B, int C, int H, int W, int P, int Kp, const float* mean,
+                  const float* inv_std, void* out, hipStream_t st);
+void gai_vit_embed(const void* patches, const void* cls, const void* pos, void* out, int B, int NP, int D,
+                   hipStream_t st);

@@ -19,25 +19,11 @@
 // fp32 output (fp32 for LM-head logits).
 #include "gai_common.h"
 #include "gai_kernels.h"
+#include "gai_epilogue.h"
 
 using namespace gai;
 
 namespace {
-
-enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_RESIDUAL = 3, EPI_SWIGLU = 4, EPI_BIAS_RESIDUAL = 5, EPI_BIAS_RELU = 6 };
-
-template <int EPI, bool OUTF32>
-__device__ __forceinline__ void store_out(void* C, const bf16* bias, const bf16* R, int ldc, int m, int n, float v) {
-  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESIDUAL || EPI == EPI_BIAS_RELU)
-    v += (float)bias[n];
-  if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
-  if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-  if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) v += (float)R[(size_t)m * ldc + n];
-  if (OUTF32)
-    reinterpret_cast<float*>(C)[(size_t)m * ldc + n] = v;
-  else
-    reinterpret_cast<bf16*>(C)[(size_t)m * ldc + n] = (bf16)v;
-}
 
 // ----------------------------------------------------------------------------------------------
 // Tiled kernel
@@ -520,6 +506,7 @@ void gai_gemm(const void* A, const void* B, void* C, const void* bias, const voi
     GAI_GEMM_EPI(EPI_SWIGLU)
     GAI_GEMM_EPI(EPI_BIAS_RESIDUAL)
     GAI_GEMM_EPI(EPI_BIAS_RELU)
+    GAI_GEMM_EPI(EPI_BIAS_QUICKGELU)
     default:
       gai_launch_error(__FILE__, __LINE__, "gemm: unknown epilogue");
   }

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import torch
 
@@ -56,3 +56,77 @@ def randn_like_(w: torch.Tensor, seed: int, std: float) -> torch.Tensor:
     if w.is_floating_point():
         w.normal_(0.0, std, generator=g)
     return w
+
+
+def quantize_linear_weights_fp8(w: dict, keys) -> int:
+    """Replace the 2-D linear weights ``w[k]`` (k in keys) by per-output-channel e4m3fn
+    :class:`~generativeaiexamples_amd.ops.Fp8Weight` in place; ops.linear then runs them on the fp8
+    MFMA GEMM (BASELINE config 4). Returns the bytes saved."""
+    from ..ops import Fp8Weight
+    saved = 0
+    for k in keys:
+        t = w[k]
+        if isinstance(t, Fp8Weight) or t.dim() != 2 or t.shape[1] % 128:
+            continue
+        w[k] = Fp8Weight.quantize(t)
+        saved += t.numel() * (t.element_size() - 1)
+        del t
+    return saved
+
+
+class PackedAttention:
+    """Self- (or cross-) attention over a packed varlen batch for encoders (BERT/E5, CLIP, ViT).
+
+    The paged flash-attention kernels read K/V from a paged cache, so an encoder forward allocates
+    one *transient* cache for the whole batch (sequence b owns blocks [off_b, off_b + ceil(n_b/16)));
+    every layer scatters its K/V into it with the RoPE/KV kernel (rotation off) and runs the
+    bidirectional (or causal) prefill kernel. All index tensors are built once per forward.
+    ``kv_lens`` (cross-attention) gives the key length per sequence when it differs from the query.
+    """
+
+    def __init__(self, q_lens: Sequence[int], num_heads: int, head_dim: int, device, dtype=torch.bfloat16,
+                 causal: bool = False, num_kv_heads: Optional[int] = None, kv_lens: Optional[Sequence[int]] = None):
+        from .. import ops
+        self.H, self.Hkv, self.hd = num_heads, num_kv_heads or num_heads, head_dim
+        self.causal, self.dtype, self.device = causal, dtype, torch.device(device)
+        q_lens = [int(n) for n in q_lens]
+        kv_lens = [int(n) for n in (kv_lens if kv_lens is not None else q_lens)]
+        self.q_lens, self.kv_lens = q_lens, kv_lens
+        self.T = sum(q_lens)
+        B, BS = len(q_lens), ops.BLOCK
+        nbs = [(n + BS - 1) // BS for n in kv_lens]
+        offs = [0]
+        for n in nbs:
+            offs.append(offs[-1] + n)
+        bt = torch.zeros(B, max(nbs + [1]), dtype=torch.int32)
+        kv_slots = torch.empty(sum(kv_lens), dtype=torch.int32)
+        t0 = 0
+        for b, n in enumerate(kv_lens):
+            bt[b, : nbs[b]] = torch.arange(offs[b], offs[b] + nbs[b], dtype=torch.int32)
+            kv_slots[t0:t0 + n] = offs[b] * BS + torch.arange(n, dtype=torch.int32)
+            t0 += n
+        cu = [0]
+        for n in q_lens:
+            cu.append(cu[-1] + n)
+        dev = self.device
+        self.positions = torch.cat([torch.arange(n, dtype=torch.int32) for n in q_lens] or
+                                   [torch.zeros(0, dtype=torch.int32)]).to(dev, non_blocking=True)
+        self.block_tables = bt.to(dev, non_blocking=True)
+        self.slots = kv_slots.to(dev, non_blocking=True)
+        self.cu_q = torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True)
+        self.ctx = torch.tensor(kv_lens, dtype=torch.int32).to(dev, non_blocking=True)
+        self.tiles = ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev) if dev.type == "cuda" else None
+        self.k_cache = torch.zeros(offs[-1] + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
+        self.v_cache = torch.zeros(offs[-1] + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)
+        self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)
+        self.cs = torch.zeros(1, head_dim, dtype=torch.float32, device=dev)  # never read (rope off)
+
+    def __call__(self, qkv: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """qkv [T, (H + 2 Hkv) * hd] -> attention output [T, H * hd]."""
+        from .. import ops
+        ops.rope_kv_write(qkv, self.positions, self.cs, self.slots, self.q, self.k_cache, self.v_cache, self.H,
+                          self.Hkv, self.hd, rope=False)
+        o = torch.empty_like(self.q) if out is None else out.view(self.T, self.H, self.hd)
+        ops.attention_prefill(self.q, self.k_cache, self.v_cache, self.block_tables, self.cu_q, self.ctx, scale,
+                              causal=self.causal, tiles=self.tiles, q_lens=self.q_lens, out=o)
+        return o.view(self.T, self.H * self.hd)

@@ -54,7 +54,7 @@ def native_available() -> bool:
         return False
 
 
-EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6}
+EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6, "quick_gelu": 7}
 _GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "large": 3}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
 
 
@@ -87,8 +87,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(x @ w^T + bias) + residual on the MFMA GEMM with a fused epilogue.
 
-    act: None | 'gelu' | 'relu' | 'swiglu' (w interleaved per 16 rows, see interleave_gate_up).
+    act: None | 'gelu' | 'relu' | 'quick_gelu' | 'swiglu' (w interleaved per 16 rows, see interleave_gate_up).
+    An :class:`Fp8Weight` ``w`` routes to the fp8 MFMA GEMM (``linear_fp8``).
     """
+    if isinstance(w, Fp8Weight):
+        return linear_fp8(x, w, bias, residual, act, out_dtype, out)
     if not x.is_cuda:
         return _into(out, ref.linear(x, w, bias, residual, act, out_dtype))
     K = x.shape[-1]
@@ -103,9 +106,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     elif act == "gelu":
         assert bias is not None and residual is None
         epi, ncol = EPI["gelu"], N
-    elif act == "relu":
+    elif act in ("relu", "quick_gelu"):
         assert bias is not None and residual is None
-        epi, ncol = EPI["relu"], N
+        epi, ncol = EPI[act], N
     elif residual is not None:
         epi, ncol = (EPI["bias_residual"] if bias is not None else EPI["residual"]), N
     else:
@@ -136,7 +139,84 @@ def _blas_linear(x2, w, bias, act, out_dtype):
         y = z
     elif act == "relu":
         y = torch.relu_(y)
+    elif act == "quick_gelu":
+        y = y * torch.sigmoid(1.702 * y)
     return y if out_dtype == y.dtype else y.to(out_dtype)
+
+
+_FP8_FORCE = int(os.environ.get("GAI_FP8_FORCE", "0"))  # 0 auto, 2 tiled, 3 large
+
+
+class Fp8Weight:
+    """Per-output-channel OCP e4m3fn weight, quantised once at load time, plus its fp32 scales [N]."""
+
+    __slots__ = ("q", "scale")
+
+    def __init__(self, q: torch.Tensor, scale: torch.Tensor):
+        self.q, self.scale = q, scale
+
+    @classmethod
+    def quantize(cls, w: torch.Tensor) -> "Fp8Weight":
+        q, s = quant_fp8(w)
+        return cls(q, s)
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def device(self):
+        return self.q.device
+
+    def data_ptr(self) -> int:
+        return self.q.data_ptr()
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def dequantize(self, dtype=torch.bfloat16) -> torch.Tensor:
+        return (self.q.float() * self.scale[:, None]).to(dtype)
+
+
+def quant_fp8(x: torch.Tensor):
+    """Per-row dynamic quantisation -> (q float8_e4m3fn [.., K], scale fp32 [rows])."""
+    if not x.is_cuda:
+        return ref.quant_rows_fp8(x)
+    K = x.shape[-1]
+    M = x.numel() // K
+    x2 = x.reshape(M, K)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(M, dtype=torch.float32, device=x.device)
+    native().quant_rows_fp8(x2, q, s)
+    return q, s
+
+
+def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias=None, residual=None, act=None, out_dtype=None, out=None):
+    """``linear`` with fp8 operands: x is quantised per token on the fly (one fused pass), the K-loop
+    runs on the block-scaled fp8 MFMA and the scales are applied in the fp32 epilogue."""
+    out_dtype = out_dtype or x.dtype
+    K = x.shape[-1]
+    M = x.numel() // K
+    xq, sx = quant_fp8(x)
+    if not x.is_cuda:
+        return _into(out, ref.linear_fp8(xq, sx, w.q, w.scale, bias, residual, act, out_dtype))
+    N = w.q.shape[0]
+    if act == "swiglu":
+        epi, ncol = EPI["swiglu"], N // 2
+    elif act in ("gelu", "relu", "quick_gelu"):
+        assert bias is not None and residual is None
+        epi, ncol = EPI[act], N
+    elif residual is not None:
+        epi, ncol = (EPI["bias_residual"] if bias is not None else EPI["residual"]), N
+    else:
+        epi, ncol = (EPI["bias"] if bias is not None else 0), N
+    if out is None:
+        out = torch.empty(*x.shape[:-1], ncol, dtype=out_dtype, device=x.device)
+    if M:
+        native().gemm_fp8(xq.reshape(M, K), w.q, sx, w.scale, out, bias, residual, epi, _FP8_FORCE)
+    return out
 
 
 class GemmTuner:
@@ -399,3 +479,25 @@ def gelu(x):
     y = torch.empty_like(x)
     native().gelu(x, y)
     return y
+
+
+# ---------------------------------------------------------------------------------------------- vision
+def patchify(img: torch.Tensor, patch: int, mean: torch.Tensor, inv_std: torch.Tensor, Kp: int) -> torch.Tensor:
+    """Normalise + im2col an image batch [B, C, H, W] fp32 into bf16 patch rows [B * gh * gw, Kp]."""
+    if not img.is_cuda:
+        return ref.patchify(img, patch, mean, inv_std, Kp)
+    B, C, H, W = img.shape
+    out = torch.empty(B * (H // patch) * (W // patch), Kp, dtype=torch.bfloat16, device=img.device)
+    native().patchify(img.contiguous(), patch, mean, inv_std, out)
+    return out
+
+
+def vit_embed(patches: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, B: int) -> torch.Tensor:
+    """[CLS | patch embeddings] + position embeddings -> packed token rows [B * (NP + 1), D]."""
+    if not patches.is_cuda:
+        return ref.vit_embed(patches, cls, pos, B)
+    D = cls.numel()
+    NP = patches.numel() // (B * D)
+    out = torch.empty(B * (NP + 1), D, dtype=torch.bfloat16, device=patches.device)
+    native().vit_embed(patches, cls, pos, out, B)
+    return out

@@ -38,7 +38,7 @@ def layer_norm(x, w, b, eps, residual=None):
 
 
 def linear(x, w, bias=None, residual=None, act=None, out_dtype=None):
-    """y = act(x @ w^T + bias) + residual; act in {None, 'gelu', 'relu', 'swiglu'}.
+    """y = act(x @ w^T + bias) + residual; act in {None, 'gelu', 'relu', 'quick_gelu', 'swiglu'}.
 
     'swiglu' expects w interleaved per 16 rows [gate16 | up16 | ...] (see
     ``interleave_gate_up``) and returns width N/2.
@@ -50,6 +50,8 @@ def linear(x, w, bias=None, residual=None, act=None, out_dtype=None):
         y = F.gelu(y)
     elif act == "relu":
         y = F.relu(y)
+    elif act == "quick_gelu":
+        y = y * torch.sigmoid(1.702 * y)
     elif act == "swiglu":
         n = y.shape[-1]
         y4 = y.reshape(*y.shape[:-1], n // 32, 2, 16)
@@ -283,3 +285,41 @@ def silu_mul(x):
 
 def gelu(x):
     return F.gelu(x.float()).to(x.dtype)
+
+
+# ---------------------------------------------------------------------------------------------- fp8
+FP8_MAX = 448.0
+
+
+def quant_rows_fp8(x: torch.Tensor):
+    """Per-row dynamic e4m3fn quantisation: (q [.., K] float8_e4m3fn, scale [rows] fp32 = amax/448)."""
+    xf = x.float().reshape(-1, x.shape[-1])
+    s = xf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX
+    q = (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q.reshape(x.shape), s
+
+
+def linear_fp8(xq, sx, wq, sw, bias=None, residual=None, act=None, out_dtype=torch.bfloat16):
+    """fp32 reference of the fp8 GEMM: dequantise both operands, then ``linear``."""
+    x = xq.float().reshape(-1, xq.shape[-1]) * sx.reshape(-1, 1)
+    w = wq.float() * sw.reshape(-1, 1)
+    y = linear(x, w, bias, None if residual is None else residual.reshape(x.shape[0], -1), act, torch.float32)
+    return y.reshape(*xq.shape[:-1], y.shape[-1]).to(out_dtype)
+
+
+# ---------------------------------------------------------------------------------------------- vision
+def patchify(img: torch.Tensor, P: int, mean: torch.Tensor, inv_std: torch.Tensor, Kp: int) -> torch.Tensor:
+    """[B, C, H, W] fp32 -> normalised patches [B * gh * gw, Kp] bf16, (c, ky, kx) order, zero padded."""
+    B, C, H, W = img.shape
+    x = (img.float() - mean[:C].view(1, C, 1, 1)) * inv_std[:C].view(1, C, 1, 1)
+    x = x.reshape(B, C, H // P, P, W // P, P).permute(0, 2, 4, 1, 3, 5).reshape(B * (H // P) * (W // P), C * P * P)
+    out = torch.zeros(x.shape[0], Kp, dtype=torch.bfloat16)
+    out[:, : C * P * P] = x.to(torch.bfloat16)
+    return out
+
+
+def vit_embed(patches: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, B: int) -> torch.Tensor:
+    D = cls.numel()
+    p = patches.float().reshape(B, -1, D)
+    x = torch.cat([cls.float().view(1, 1, D).expand(B, 1, D), p], 1) + pos.float()[: p.shape[1] + 1]
+    return x.reshape(-1, D).to(torch.bfloat16)

@@ -45,6 +45,32 @@ def bench_gemm(rows, shapes):
                          ours_gbs=by / t_ours / 1e6, speedup=t_blas / t_ours))
 
 
+def bench_fp8(rows, shapes):
+    """fp8 GEMM (block-scaled MFMA) alone and with the fused per-token quantiser, vs bf16 hipBLASLt and
+    (when this torch build has it) hipBLASLt fp8 via torch._scaled_mm."""
+    for M, N, K, tag in shapes:
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+        W = ops.Fp8Weight.quantize(w)
+        xq, sx = ops.quant_fp8(x)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        nat = ops.native()
+        t_gemm = timeit(lambda: nat.gemm_fp8(xq, W.q, sx, W.scale, out, None, None, 0, 0))
+        t_lin = timeit(lambda: ops.linear_fp8(x, W))
+        t_bf16 = timeit(lambda: torch.matmul(x, w.t()))
+        t_sm = None
+        try:
+            one = torch.ones((), device="cuda")
+            t_sm = timeit(lambda: torch._scaled_mm(xq, W.q.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16))
+        except Exception:
+            pass
+        fl = 2 * M * N * K
+        rows.append(dict(op="gemm_fp8", tag=tag, M=M, N=N, K=K, gemm_ms=t_gemm, linear_ms=t_lin, bf16_blas_ms=t_bf16,
+                         scaled_mm_ms=t_sm, gemm_tflops=fl / t_gemm / 1e9, linear_tflops=fl / t_lin / 1e9,
+                         bf16_blas_tflops=fl / t_bf16 / 1e9,
+                         scaled_mm_tflops=(fl / t_sm / 1e9) if t_sm else None))
+
+
 def bench_prefill(rows, B, S, Hq, Hkv, D):
     nb = B * ((S + 15) // 16)
     kc = torch.randn(nb, Hkv, 16, D, device="cuda", dtype=torch.bfloat16)
@@ -119,6 +145,10 @@ def main():
             (16384, 1024, 1024, "e5 qkv-ish"), (16384, 4096, 1024, "e5 ffn up"),
         ]
         bench_gemm(rows, shapes)
+    if "fp8" in only:
+        bench_fp8(rows, [(4096, 6144, 4096, "qkv prefill"), (4096, 28672, 4096, "gate_up prefill"),
+                         (4096, 4096, 14336, "down prefill"), (8192, 8192, 8192, "square 8k"),
+                         (1601 * 8, 4096, 1024, "clip-L mlp up b8"), (64, 28672, 4096, "gate_up decode b64")])
     if "prefill" in only:
         bench_prefill(rows, 4, 2048, 32, 8, 128)
         bench_prefill(rows, 64, 512, 16, 16, 64)
