@@ -95,14 +95,17 @@ class LLMEngine:
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
         nb = cfg.num_blocks or self._blocks_from_memory()
         # one extra block, never handed out, is the scratch page of padded graph rows
-        self.kv = KVCache(mc.num_layers, nb + 1, model.hkv, mc.head_dim, self.device, model.dtype)
+        # models with non-KV layers (cross-attention) report how many layers own a paged KV cache
+        self.kv = KVCache(self._kv_layers(), nb + 1, model.hkv, mc.head_dim, self.device, model.dtype)
         self.pad_block = nb
         self.sched = _rt().Scheduler(nb, cfg.max_num_seqs, cfg.max_batched_tokens, cfg.max_model_len,
                                      cfg.prefix_cache, cfg.prefill_chunk)
         self.decode_ws = None
         if self.device.type == "cuda":
             self.decode_ws = ops.DecodeWorkspace(max(cfg.max_num_seqs, max(cfg.graph_batch_sizes)), model.hq,
-                                                 mc.head_dim, cfg.max_model_len, self.device)
+                                                 mc.head_dim, max(cfg.max_model_len,
+                                                                  getattr(model, "max_cross_tokens", 0)),
+                                                 self.device)
         self.requests: Dict[int, Request] = {}
         self.by_rid: Dict[str, Request] = {}
         self._ids = itertools.count(1)
@@ -113,6 +116,9 @@ class LLMEngine:
         self.eos = set(mc.eos_token_ids) | set(getattr(tokenizer, "eos_ids", ()) or ())
 
     # ------------------------------------------------------------------ memory
+    def _kv_layers(self) -> int:
+        return getattr(self.model, "num_kv_layers", self.model.cfg.num_layers)
+
     def _blocks_from_memory(self) -> int:
         mc = self.model.cfg
         if self.cfg.kv_memory_bytes:
@@ -122,12 +128,13 @@ class LLMEngine:
             nbytes = int(free * self.cfg.kv_memory_fraction)
         else:
             nbytes = 256 << 20
-        nb = KVCache.blocks_for_memory(nbytes, mc.num_layers, self.model.hkv, mc.head_dim, self.model.dtype)
+        nb = KVCache.blocks_for_memory(nbytes, self._kv_layers(), self.model.hkv, mc.head_dim, self.model.dtype)
         return max(nb, 2 * self.max_blocks_per_seq)
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_ids: List[int], params: SamplingParams | None = None,
-                    request_id: Optional[str] = None) -> Request:
+                    request_id: Optional[str] = None, images: Optional[list] = None) -> Request:
+        """images: inputs for a multimodal model (encoded once here by ``model.register_request``)."""
         params = params or SamplingParams()
         with self.lock:
             sid = next(self._ids)
@@ -141,7 +148,12 @@ class LLMEngine:
                           seed=params.seed if params.seed is not None else (sid * 7919) & 0x7FFFFFFF)
             self.requests[sid] = req
             self.by_rid[rid] = req
+            if images:
+                if not hasattr(self.model, "register_request"):
+                    raise ValueError(f"{self.model.cfg.name} does not accept image inputs")
+                self.model.register_request(sid, images)
             if max_new == 0:
+                self._release(sid)
                 req.finished, req.finish_reason = True, "length"
                 return req
             self.sched.add(sid, req.prompt_ids, max_new)
@@ -154,8 +166,13 @@ class LLMEngine:
                 return False
             self.sched.abort(req.seq_id)
             self.requests.pop(req.seq_id, None)
+            self._release(req.seq_id)
             req.finished, req.finish_reason = True, "abort"
             return True
+
+    def _release(self, sid: int):
+        if hasattr(self.model, "release_request"):
+            self.model.release_request(sid)
 
     def has_work(self) -> bool:
         return self.sched.has_work()
@@ -202,6 +219,9 @@ class LLMEngine:
             fb.decode_ctx, fb.decode_block_tables = dev[6], dev[7]
             fb.max_decode_ctx = int(b.decode_ctx.max())
         fb.sample_rows = dev[8].long()
+        fb.seq_ids = list(b.prefill_seq_ids) + list(b.decode_seq_ids)
+        if hasattr(self.model, "prepare_batch"):
+            self.model.prepare_batch(fb)
         return fb, seq_order
 
     # ------------------------------------------------------------------ HIP graphs (decode)
@@ -221,6 +241,8 @@ class LLMEngine:
         bt = torch.full((bs, self.max_blocks_per_seq), self.pad_block, dtype=torch.int32, device=d)
         fb = ForwardBatch(token_ids=ids, positions=pos, slots=slots, num_prefill_tokens=0, decode_ctx=ctx,
                           decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
+        if hasattr(self.model, "graph_static_inputs"):
+            fb.extra = self.model.graph_static_inputs(bs)
         s = torch.cuda.Stream(device=d)
         s.wait_stream(torch.cuda.current_stream(d))
         with torch.cuda.stream(s):
@@ -257,6 +279,8 @@ class LLMEngine:
             fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
             fb.decode_ctx[n:].fill_(1)
             fb.decode_block_tables[n:, 0].fill_(self.pad_block)
+        if fb.extra is not None:
+            self.model.fill_graph_inputs(fb.extra, list(b.decode_seq_ids), n)
         g.replay()
         self.stats["graph_steps"] += 1
         return logits[:n]
@@ -345,6 +369,7 @@ class LLMEngine:
                 req.finished, req.finish_reason, req.finish_time = True, reason, now
                 self.sched.finish(sid)
                 self.requests.pop(sid, None)
+                self._release(sid)
                 self.by_rid.pop(req.request_id, None)
             else:
                 cont_ids.append(sid)

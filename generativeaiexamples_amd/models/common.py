@@ -30,6 +30,10 @@ class ForwardBatch:
     max_decode_ctx: int = 0
     # rows of the flat token dim whose logits are needed (in output order)
     sample_rows: Optional[torch.Tensor] = None     # [S] int64
+    # host-side sequence ids of the rows (prefill sequences, then decode sequences) and model-specific
+    # per-step inputs built by the model's prepare_batch hook (e.g. cross-attention tables)
+    seq_ids: Optional[list] = None
+    extra: Optional[dict] = None
 
     @property
     def num_tokens(self) -> int:
