@@ -89,6 +89,53 @@ class Embedder:
         return self.embed_ids([self.tokenize(t, input_type, truncate) for t in texts])
 
 
+class ClipEmbedder:
+    """NV-CLIP-style multimodal embedder over :class:`~..models.clip.ClipModel` (BASELINE config 4,
+    SURVEY W14 "NV-CLIP search"): each ``/v1/embeddings`` input is either text or an image given as a
+    ``data:image/...;base64,`` URI, and both land in the same normalised projection space. Images are
+    batched through the vision tower (patchify kernel + MFMA GEMMs + packed bidirectional attention),
+    texts through the causal text tower."""
+
+    accepts_images = True
+
+    def __init__(self, model, tokenizer: Tokenizer, model_name: str | None = None, max_batch_images: int = 64):
+        self.model, self.tok = model, tokenizer
+        self.name = model_name or model.cfg.name
+        self.dim = model.cfg.projection_dim
+        self.max_len = model.cfg.max_text_len
+        self.max_batch_images = max_batch_images
+        self.lock = threading.Lock()
+
+    @staticmethod
+    def is_image(x) -> bool:
+        return not isinstance(x, str) or x.startswith("data:image")
+
+    def tokenize(self, text, input_type: str = "query", truncate: str = "END") -> List[int]:
+        if self.is_image(text):
+            return [0] * (self.model.cfg.num_patches + 1)  # usage accounting: one token per patch + CLS
+        body = self.tok.encode(text)
+        bos = [self.tok.bos_id] if self.tok.bos_id is not None else []
+        eos = [self.tok.eos_ids[0]] if self.tok.eos_ids else []
+        body = _truncate(body, self.max_len - len(bos) - len(eos), truncate)
+        return bos + body + eos
+
+    @torch.inference_mode()
+    def embed(self, inputs: Sequence, input_type: str = "query", truncate: str = "END") -> torch.Tensor:
+        dev = self.model.device
+        out = torch.empty(len(inputs), self.dim, dtype=torch.float32, device=dev)
+        img_idx = [i for i, x in enumerate(inputs) if self.is_image(x)]
+        txt_idx = [i for i, x in enumerate(inputs) if not self.is_image(x)]
+        with self.lock:
+            for s in range(0, len(img_idx), self.max_batch_images):
+                idx = img_idx[s:s + self.max_batch_images]
+                px = self.model.preprocess([inputs[i] for i in idx])
+                out[torch.tensor(idx, device=dev)] = self.model.encode_image(px)
+            if txt_idx:
+                toks = [self.tokenize(inputs[i], input_type, truncate) for i in txt_idx]
+                out[torch.tensor(txt_idx, device=dev)] = self.model.encode_text(toks)
+        return out
+
+
 class Reranker:
     def __init__(self, model: BertModel, tokenizer: Tokenizer, max_len: int | None = None,
                  max_batch_tokens: int = 65536, model_name: str | None = None):

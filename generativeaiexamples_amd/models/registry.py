@@ -9,7 +9,10 @@ import torch
 
 from ..engine.tokenizer import Tokenizer, bert_byte_tokenizer, load_tokenizer, llama3_byte_tokenizer, small_byte_tokenizer
 from .bert import BertConfig, BertModel
+from .clip import ClipConfig, ClipModel
 from .llama import LlamaConfig, LlamaModel
+from .mixtral import MixtralConfig, MixtralModel
+from .mllama import MllamaConfig, MllamaModel
 from .opt import OPTConfig, OPTModel
 
 LLM_PRESETS = {
@@ -19,12 +22,19 @@ LLM_PRESETS = {
     "mistral-7b": ("mistralai/mistral-7b-instruct-v0.3", lambda: LlamaConfig.mistral_7b()),
     "tiny-llama": ("tiny-llama", lambda: LlamaConfig.tiny(max_position=4096)),
     "opt-125m": ("facebook/opt-125m", lambda: OPTConfig.opt_125m()),
+    "mixtral-8x7b": ("mistralai/mixtral-8x7b-instruct-v0.1", lambda: MixtralConfig.mixtral_8x7b()),
+    "tiny-moe": ("tiny-moe", lambda: MixtralConfig.tiny_moe()),
+    "llama3.2-11b-vision": ("meta/llama-3.2-11b-vision-instruct", lambda: MllamaConfig.llama32_11b_vision()),
+    "tiny-mllama": ("tiny-mllama", lambda: MllamaConfig.tiny()),
 }
+# any LLM preset + "-fp8": e4m3fn per-channel weights on the fp8 MFMA GEMM (BASELINE config 4)
 
 ENCODER_PRESETS = {
     "e5-large-v2": ("nvidia/nv-embedqa-e5-v5", lambda: BertConfig.e5_large_v2()),
     "e5-base-v2": ("intfloat/e5-base-v2", lambda: BertConfig.e5_base_v2()),
     "tiny-e5": ("tiny-e5", lambda: BertConfig.tiny()),
+    "nvclip": ("nvidia/nvclip", lambda: ClipConfig.vit_l_14()),
+    "tiny-clip": ("tiny-clip", lambda: ClipConfig.tiny()),
 }
 
 RERANKER_PRESETS = {
@@ -50,15 +60,31 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
         m.load_safetensors_dir(weights) if hasattr(m, "load_safetensors_dir") else _load_st(m, weights)
         tok = load_tokenizer(weights, "llama3", m.cfg.vocab_size)
         return m, tok, os.path.basename(weights.rstrip("/"))
-    name, mk = LLM_PRESETS[preset]
+    fp8 = preset.endswith("-fp8")
+    name, mk = LLM_PRESETS[preset[:-4] if fp8 else preset]
     cfg = mk()
     if isinstance(cfg, OPTConfig):
         m = OPTModel(cfg, device=device).random_init(seed)
         tok: Tokenizer = small_byte_tokenizer(512) if cfg.vocab_size < 1000 else _opt_tok(cfg.vocab_size)
+        return m, tok, name
+    if isinstance(cfg, MllamaConfig):
+        m = MllamaModel(cfg, device=device).random_init(seed)
+        vocab = cfg.text.vocab_size
+    elif isinstance(cfg, MixtralConfig):
+        m = MixtralModel(cfg, device=device).random_init(seed)
+        vocab = cfg.vocab_size
     else:
         m = LlamaModel(cfg, device=device).random_init(seed)
-        tok = llama3_byte_tokenizer(cfg.vocab_size) if cfg.vocab_size >= 128256 else small_byte_tokenizer(cfg.vocab_size) \
-            if cfg.vocab_size <= 4096 else _generic_tok(cfg)
+        vocab = cfg.vocab_size
+    if fp8:
+        if hasattr(m, "quantize_fp8"):
+            m.quantize_fp8()
+        else:
+            from .common import quantize_linear_weights_fp8
+            quantize_linear_weights_fp8(m.w, [k for k in m.w if k.split(".")[-1] in ("qkv", "o", "gate_up", "down")])
+        name += "-fp8"
+    tok = llama3_byte_tokenizer(vocab) if vocab >= 128256 else small_byte_tokenizer(vocab) \
+        if vocab <= 4096 else _generic_tok(m.cfg)
     return m, tok, name
 
 
@@ -94,8 +120,27 @@ def build_encoder(preset: str = "e5-large-v2", weights: Optional[str] = None, de
     table = RERANKER_PRESETS if reranker else ENCODER_PRESETS
     name, mk = table[preset]
     cfg = mk()
+    if isinstance(cfg, ClipConfig):
+        m = ClipModel(cfg, device=device).random_init(seed)
+        return m, small_byte_tokenizer(cfg.vocab_size) if cfg.vocab_size <= 4096 else _clip_tok(cfg.vocab_size), name
     m = BertModel(cfg, device=device).random_init(seed)
     return m, bert_byte_tokenizer(cfg.vocab_size), name
+
+
+def build_embedder_service(preset: str = "e5-large-v2", weights: Optional[str] = None, device=None, seed: int = 0):
+    """-> (Embedder | ClipEmbedder, served_name) ready for the /v1/embeddings route."""
+    from ..engine.embedder import ClipEmbedder, Embedder
+    m, tok, name = build_encoder(preset, weights, device, seed)
+    if isinstance(m, ClipModel):
+        return ClipEmbedder(m, tok, model_name=name), name
+    return Embedder(m, tok, model_name=name), name
+
+
+def _clip_tok(vocab):
+    from ..engine.tokenizer import ByteTokenizer
+
+    return ByteTokenizer(vocab, 3, {"<|startoftext|>": vocab - 2, "<|endoftext|>": vocab - 1},
+                         bos="<|startoftext|>", eos=("<|endoftext|>",))
 
 
 def default_device():

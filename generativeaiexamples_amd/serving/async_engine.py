@@ -71,7 +71,7 @@ class AsyncLLMEngine:
                     self.queues.pop(o.request_id, None)
 
     async def generate(self, prompt_ids: List[int], params: SamplingParams,
-                       request_id: Optional[str] = None) -> AsyncIterator[StreamItem]:
+                       request_id: Optional[str] = None, images: Optional[list] = None) -> AsyncIterator[StreamItem]:
         rid = request_id or f"cmpl-{uuid.uuid4().hex}"
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
@@ -79,7 +79,7 @@ class AsyncLLMEngine:
         t0 = time.perf_counter()
         first = True
         with self.cv:
-            req = self.engine.add_request(prompt_ids, params, rid)
+            req = self.engine.add_request(prompt_ids, params, rid, images=images)
             self.cv.notify()
         METRICS.requests_total.inc()
         METRICS.prompt_tokens.inc(len(prompt_ids))
@@ -148,9 +148,10 @@ class AsyncLLMEngine:
                 with self.cv:
                     self.engine.abort(rid)
 
-    async def complete(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None):
+    async def complete(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None,
+                       images: Optional[list] = None):
         text, ids, reason = [], [], None
-        async for it in self.generate(prompt_ids, params, request_id):
+        async for it in self.generate(prompt_ids, params, request_id, images):
             text.append(it.delta)
             if it.token_id >= 0:
                 ids.append(it.token_id)

@@ -170,6 +170,19 @@ def parse_tool_calls(text: str, tools: List[Dict[str, Any]]) -> Optional[List[Di
     return calls or None
 
 
+def _images_of(req: ChatRequest) -> List[str]:
+    """OpenAI/NIM vision content parts: {"type": "image_url", "image_url": {"url": "data:image/...;base64,..."}}
+    (W12 image_url chat); also accepts a bare string url field."""
+    out = []
+    for m in req.messages:
+        if isinstance(m.content, list):
+            for p in m.content:
+                if p.get("type") == "image_url":
+                    u = p.get("image_url")
+                    out.append(u.get("url") if isinstance(u, dict) else u)
+    return out
+
+
 def _messages_for_template(req: ChatRequest) -> List[dict]:
     msgs = []
     for m in req.messages:
@@ -256,6 +269,9 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
         tok = llm.tokenizer
         ids = apply_chat_template(_messages_for_template(req), tok)
         params = _params(req, hub.default_max_tokens)
+        images = _images_of(req) or None
+        if images and not hasattr(llm.engine.model, "register_request"):
+            return _err(400, f"model '{req.model or hub.default_llm_name}' does not accept image inputs")
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         created = int(time.time())
         model = req.model or hub.default_llm_name
@@ -270,7 +286,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
                 yield f"data: {json.dumps(head)}\n\n"
                 n = 0
                 try:
-                    async for it in llm.generate(ids, params, rid):
+                    async for it in llm.generate(ids, params, rid, images):
                         n += it.token_id >= 0
                         ch = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
                               "choices": [{"index": 0, "delta": {"content": it.delta} if it.delta else {},
@@ -288,7 +304,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
 
             return StreamingResponse(gen(), media_type="text/event-stream")
 
-        text, out_ids, reason = await llm.complete(ids, params, rid)
+        text, out_ids, reason = await llm.complete(ids, params, rid, images)
         msg: Dict[str, Any] = {"role": "assistant", "content": text}
         if use_tools:
             calls = parse_tool_calls(text, req.tools)
@@ -350,6 +366,8 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
         if emb is None:
             return _err(404, f"embedding model '{req.model}' is not served here")
         texts = [req.input] if isinstance(req.input, str) else list(req.input)
+        if any(isinstance(t, str) and t.startswith("data:image") for t in texts) and not getattr(emb, "accepts_images", False):
+            return _err(400, f"embedding model '{req.model or emb.name}' does not accept image inputs")
         itype = (req.input_type or "query").lower()
         if itype not in ("query", "passage"):
             return _err(400, "input_type must be 'query' or 'passage'")
