@@ -42,11 +42,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="concurrent queries per GPU per step")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="BASELINE.json config: 2 = headline (default), 3 = 70B TP + rerank + 10M sharded index, "
+                         "4 = multimodal CLIP + Llama-3.2-Vision fp8, 5 = agentic Mixtral tool loop")
+    ap.add_argument("--batch", type=int, default=None, help="concurrent queries per GPU per step (default 64)")
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--top-k", type=int, default=4)
     ap.add_argument("--chunk-tokens", type=int, default=506)
-    ap.add_argument("--index-size", type=int, default=1_000_000, help="vectors per GPU shard")
+    ap.add_argument("--index-size", type=int, default=None, help="vectors per GPU shard (default 1M)")
     ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "tiny"])
     ap.add_argument("--embedder", default="e5-large-v2", choices=["e5-large-v2", "e5-base-v2", "tiny"])
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
@@ -56,6 +59,9 @@ def parse():
                          "chunks for every query, so caching would skip most of the prefill work)")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache size per rank (default: 50%% of free HBM)")
     ap.add_argument("--json-out", default=None)
+    from generativeaiexamples_amd.benchmarks import CONFIGS, module
+    for c in CONFIGS:
+        module(c).add_args(ap)
     return ap.parse_args()
 
 
@@ -64,8 +70,31 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def run_other_config(args):
+    """Configs 3-5: generativeaiexamples_amd.benchmarks.<module>.run, same JSON contract."""
+    from generativeaiexamples_amd.benchmarks import module
+    from generativeaiexamples_amd.parallel.dist import init_distributed
+
+    mod = module(args.config)
+    ctx = init_distributed(tp_size=mod.tp_size(args) if hasattr(mod, "tp_size") else 1)
+    torch.manual_seed(1234 + ctx.rank)
+    out = mod.run(args, ctx)
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(out, f)
+    if ctx.world_size > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config != 2:
+        return run_other_config(args)
+    args.batch = args.batch or 64
+    args.index_size = args.index_size or 1_000_000
     from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from generativeaiexamples_amd.engine.embedder import Embedder
     from generativeaiexamples_amd.engine.tokenizer import (apply_chat_template, bert_byte_tokenizer,
@@ -110,9 +139,14 @@ def main():
     log(f"index ready: {args.index_size} x {bcfg.hidden_size} per shard, {world} shard(s)")
 
     # ---------------- engine
-    prompt_est = 60 + args.top_k * (args.chunk_tokens + 2) + 80
+    # size max_model_len from a real prompt of this pipeline (+25% slack for longer questions) so no
+    # request is ever cut short: every query must generate exactly max_tokens
+    sample_ctx = "\n\n".join(synthetic.chunk_document(r, args.chunk_tokens).page_content for r in range(args.top_k))
+    sample = apply_chat_template([{"role": "system", "content": RAG_TEMPLATE},
+                                  {"role": "user", "content": rag_user_message(sample_ctx, synthetic.question(0))}], ltok)
+    prompt_est = int(len(sample) * 1.25) + 64
     ecfg = EngineConfig(max_num_seqs=max(args.batch, 1), max_batched_tokens=args.max_batched_tokens,
-                        max_model_len=min(lcfg.max_position, prompt_est + args.max_tokens + 64),
+                        max_model_len=min(lcfg.max_position, prompt_est + args.max_tokens),
                         prefill_chunk=args.max_batched_tokens, use_graphs=not args.no_graphs,
                         prefix_cache=args.prefix_cache,
                         kv_memory_fraction=0.5,
@@ -151,6 +185,8 @@ def main():
         t1 = time.perf_counter()
         ttft = [r.first_token_time - t0 for r in reqs]
         ntok = sum(len(r.output_ids) for r in reqs)
+        short = [len(r.output_ids) for r in reqs if len(r.output_ids) != args.max_tokens]
+        assert not short, f"{len(short)} queries generated != max_tokens ({short[:4]}): work would be skipped"
         plen = statistics.mean(len(r.prompt_ids) for r in reqs)
         return t1 - t0, ttft, ntok, plen, t_retrieved - t0
 
@@ -206,6 +242,7 @@ def main():
         "p50_ttft_s": round(p50, 4),
         "p90_ttft_s": round(p90, 4),
         "output_tokens_per_s": round(toks / total, 1),
+        "tokens_per_query": args.max_tokens,
         "retrieval_ms": round(1000 * statistics.mean(rtimes), 2),
         "unique_chunks_retrieved": len(uniq),
         "prefix_cache": bool(args.prefix_cache),

@@ -158,6 +158,9 @@ class Reranker:
         types = [0] * (len(q) + 2) + [1] * (len(p) + 1)
         return ids, types
 
+    def score_many(self, items: Sequence[Tuple[str, Sequence[str]]], truncate: str = "END") -> List[List[float]]:
+        return [self.score(q, ps, truncate) for q, ps in items]
+
     @torch.inference_mode()
     def score(self, query: str, passages: Sequence[str], truncate: str = "END") -> List[float]:
         if not passages:
@@ -236,3 +239,53 @@ class DynamicBatcher:
         with self.cv:
             self.stop = True
             self.cv.notify_all()
+
+
+class DecoderReranker:
+    """Service over :class:`~..models.decoder_reranker.DecoderRerankerModel` (NV-RerankQA-Mistral-4B class):
+    pairs are formatted ``"question:{q} \\n \\n passage:{p}"`` (BOS first), passages truncated to fit
+    ``max_length``, and every pair of one or many queries is packed into varlen micro-batches under a
+    token budget (one bidirectional encoder pass per micro-batch, no padding)."""
+
+    def __init__(self, model, tokenizer: Tokenizer, model_name: str | None = None, max_batch_tokens: int = 65536):
+        self.model, self.tok = model, tokenizer
+        self.name = model_name or model.cfg.name
+        self.max_len = model.cfg.max_length
+        self.max_batch_tokens = max_batch_tokens
+        self.lock = threading.Lock()
+
+    def pair_ids(self, query: str, passage: str, truncate: str = "END") -> List[int]:
+        bos = [self.tok.bos_id] if self.tok.bos_id is not None else []
+        q = self.tok.encode(f"question:{query} \n \n passage:")[: self.max_len // 2]
+        p = _truncate(self.tok.encode(passage), max(1, self.max_len - len(q) - len(bos)), truncate)
+        return bos + q + p
+
+    @torch.inference_mode()
+    def score_many(self, items: Sequence[Tuple[str, Sequence[str]]], truncate: str = "END") -> List[List[float]]:
+        pairs = [(qi, self.pair_ids(q, p, truncate)) for qi, (q, ps) in enumerate(items) for p in ps]
+        flat_scores = [0.0] * len(pairs)
+        dev = self.model.device
+        order = sorted(range(len(pairs)), key=lambda i: len(pairs[i][1]))
+        i = 0
+        with self.lock:
+            while i < len(order):
+                j, tot = i, 0
+                while j < len(order) and (tot + len(pairs[order[j]][1]) <= self.max_batch_tokens or j == i):
+                    tot += len(pairs[order[j]][1])
+                    j += 1
+                idx = order[i:j]
+                lens = [len(pairs[k][1]) for k in idx]
+                flat = torch.tensor([t for k in idx for t in pairs[k][1]], dtype=torch.int32).to(dev)
+                cu = torch.zeros(len(idx) + 1, dtype=torch.int32)
+                cu[1:] = torch.tensor(lens).cumsum(0)
+                sc = self.model.score(flat, cu.to(dev), lens).float().cpu().tolist()
+                for k, v in zip(idx, sc):
+                    flat_scores[k] = v
+                i = j
+        out: List[List[float]] = [[] for _ in items]
+        for (qi, _), v in zip(pairs, flat_scores):
+            out[qi].append(v)
+        return out
+
+    def score(self, query: str, passages: Sequence[str], truncate: str = "END") -> List[float]:
+        return self.score_many([(query, passages)], truncate)[0] if passages else []

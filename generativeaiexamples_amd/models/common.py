@@ -89,7 +89,8 @@ class PackedAttention:
     """
 
     def __init__(self, q_lens: Sequence[int], num_heads: int, head_dim: int, device, dtype=torch.bfloat16,
-                 causal: bool = False, num_kv_heads: Optional[int] = None, kv_lens: Optional[Sequence[int]] = None):
+                 causal: bool = False, num_kv_heads: Optional[int] = None, kv_lens: Optional[Sequence[int]] = None,
+                 cos_sin: Optional[torch.Tensor] = None):
         from .. import ops
         self.H, self.Hkv, self.hd = num_heads, num_kv_heads or num_heads, head_dim
         self.causal, self.dtype, self.device = causal, dtype, torch.device(device)
@@ -123,13 +124,15 @@ class PackedAttention:
         self.k_cache = torch.zeros(offs[-1] + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
         self.v_cache = torch.zeros(offs[-1] + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)
         self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)
-        self.cs = torch.zeros(1, head_dim, dtype=torch.float32, device=dev)  # never read (rope off)
+        # RoPE table [max_pos, hd] (decoder-based encoders, e.g. the Mistral reranker) or none
+        self.rope = cos_sin is not None
+        self.cs = cos_sin if self.rope else torch.zeros(1, head_dim, dtype=torch.float32, device=dev)
 
     def __call__(self, qkv: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """qkv [T, (H + 2 Hkv) * hd] -> attention output [T, H * hd]."""
         from .. import ops
         ops.rope_kv_write(qkv, self.positions, self.cs, self.slots, self.q, self.k_cache, self.v_cache, self.H,
-                          self.Hkv, self.hd, rope=False)
+                          self.Hkv, self.hd, rope=self.rope)
         o = torch.empty_like(self.q) if out is None else out.view(self.T, self.H, self.hd)
         ops.attention_prefill(self.q, self.k_cache, self.v_cache, self.block_tables, self.cu_q, self.ctx, scale,
                               causal=self.causal, tiles=self.tiles, q_lens=self.q_lens, out=o)

@@ -448,12 +448,17 @@ class MllamaModel(LlamaModel):
 
     @torch.no_grad()
     def register_request(self, sid: int, images: Sequence) -> int:
-        """Encode the request's image(s) and write the cross K/V of every cross layer. Returns #tokens."""
+        """Encode the request's image(s) and write the cross K/V of every cross layer. Returns #tokens.
+        ``images`` holds raw images / :class:`ImageInput` or already-encoded cross states [n, hidden]
+        (``encode_images`` batches many requests' images through one vision forward)."""
         if not images:
             return 0
         cc, c, w = self._ensure_cross(), self.cfg, self.w
-        ims = [im if isinstance(im, ImageInput) else self.preprocess(im) for im in images]
-        states = torch.cat(self.encode_images(ims))
+        if all(isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[1] == c.hidden_size for x in images):
+            states = torch.cat(list(images))  # cross states already encoded (batched by the caller)
+        else:
+            ims = [im if isinstance(im, ImageInput) else self.preprocess(im) for im in images]
+            states = torch.cat(self.encode_images(ims))
         n = states.shape[0]
         blocks = cc.alloc(sid, n)
         slots = (torch.tensor(blocks, dtype=torch.int32)[:, None] * ops.BLOCK +

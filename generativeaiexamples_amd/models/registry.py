@@ -10,6 +10,7 @@ import torch
 from ..engine.tokenizer import Tokenizer, bert_byte_tokenizer, load_tokenizer, llama3_byte_tokenizer, small_byte_tokenizer
 from .bert import BertConfig, BertModel
 from .clip import ClipConfig, ClipModel
+from .decoder_reranker import DecoderRerankerConfig, DecoderRerankerModel
 from .llama import LlamaConfig, LlamaModel
 from .mixtral import MixtralConfig, MixtralModel
 from .mllama import MllamaConfig, MllamaModel
@@ -38,7 +39,9 @@ ENCODER_PRESETS = {
 }
 
 RERANKER_PRESETS = {
-    "bge-reranker-large": ("nv-rerank-qa-mistral-4b:1", lambda: BertConfig.bge_reranker_large()),
+    "nv-rerankqa-mistral-4b": ("nvidia/nv-rerankqa-mistral-4b-v3", lambda: DecoderRerankerConfig.nv_rerankqa_mistral_4b()),
+    "tiny-decoder-reranker": ("tiny-decoder-reranker", lambda: DecoderRerankerConfig.tiny()),
+    "bge-reranker-large": ("BAAI/bge-reranker-large", lambda: BertConfig.bge_reranker_large()),
     "tiny-reranker": ("tiny-reranker", lambda: BertConfig.tiny(num_labels=1, pooling="cls", normalize=False)),
 }
 
@@ -134,6 +137,30 @@ def build_embedder_service(preset: str = "e5-large-v2", weights: Optional[str] =
     if isinstance(m, ClipModel):
         return ClipEmbedder(m, tok, model_name=name), name
     return Embedder(m, tok, model_name=name), name
+
+
+def build_reranker_service(preset: str = "nv-rerankqa-mistral-4b", weights: Optional[str] = None, device=None,
+                           seed: int = 0):
+    """-> (Reranker | DecoderReranker, served_name) for /v1/ranking."""
+    from ..engine.embedder import DecoderReranker, Reranker
+    if _is_hf_dir(weights):
+        import json
+        arch = json.load(open(os.path.join(weights, "config.json"))).get("model_type", "bert")
+        if arch in ("mistral", "llama"):
+            cfg = DecoderRerankerConfig.nv_rerankqa_mistral_4b()
+            m = DecoderRerankerModel(cfg, device=device)
+            _load_st(m, weights)
+            return DecoderReranker(m, load_tokenizer(weights, "llama3", cfg.vocab_size)), os.path.basename(weights.rstrip("/"))
+        m, tok, name = build_encoder(preset, weights, device, seed, reranker=True)
+        return Reranker(m, tok, model_name=name), name
+    name, mk = RERANKER_PRESETS[preset]
+    cfg = mk()
+    if isinstance(cfg, DecoderRerankerConfig):
+        m = DecoderRerankerModel(cfg, device=device).random_init(seed)
+        tok = small_byte_tokenizer(cfg.vocab_size) if cfg.vocab_size <= 4096 else _generic_tok(cfg)
+        return DecoderReranker(m, tok, model_name=name), name
+    m = BertModel(cfg, device=device).random_init(seed)
+    return Reranker(m, bert_byte_tokenizer(cfg.vocab_size), model_name=name), name
 
 
 def _clip_tok(vocab):

@@ -40,3 +40,26 @@ def question(i: int) -> str:
     rng = np.random.default_rng(i + 12345)
     a, b = (_WORDS[int(x)] for x in rng.integers(len(_WORDS), size=2))
     return f"What does the report say about the {a} of the {b} in section {i % 97}?"
+
+
+def page_image(row: int, h: int = 720, w: int = 960) -> np.ndarray:
+    """Deterministic synthetic 'slide / chart page' (HWC uint8): light background, a title band and
+    a bar chart whose bar heights/colours derive from the row id (multimodal RAG corpus)."""
+    rng = np.random.default_rng(row * 40503 % (1 << 32))
+    img = np.full((h, w, 3), 245, dtype=np.uint8)
+    img[: h // 10] = rng.integers(20, 120, size=3, dtype=np.uint8)
+    nb = int(rng.integers(3, 9))
+    bw = w // (2 * nb + 1)
+    base = h - h // 12
+    for i in range(nb):
+        bh = int(rng.integers(h // 8, h // 2))
+        x0 = (2 * i + 1) * bw
+        img[base - bh:base, x0:x0 + bw] = rng.integers(0, 255, size=3, dtype=np.uint8)
+    img[base:base + 2, bw // 2: w - bw // 2] = 30
+    return img
+
+
+def image_question(i: int) -> str:
+    rng = np.random.default_rng(i + 777)
+    a = _WORDS[int(rng.integers(len(_WORDS)))]
+    return f"Which bar in the {a} chart is the tallest, and what trend does slide {i % 53} show?"

@@ -4,7 +4,7 @@ Equivalent of the reference's ``nemollm-inference`` + ``nemollm-embedding`` + ``
 containers in one MI355X process. Example:
 
     python -m generativeaiexamples_amd.serving --llm llama3-8b --embedder e5-large-v2 \\
-        --reranker bge-reranker-large --port 8000
+        --reranker nv-rerankqa-mistral-4b --port 8000
 """
 from __future__ import annotations
 

@@ -130,7 +130,7 @@ class ServiceHub:
     # ---------------------------------------------------------------- construction
     @classmethod
     def build(cls, spec: HubSpec) -> "ServiceHub":
-        from ..models.registry import build_embedder_service, build_encoder, build_llm, default_device
+        from ..models.registry import build_embedder_service, build_llm, build_reranker_service, default_device
 
         import torch
 
@@ -149,6 +149,6 @@ class ServiceHub:
             emb, name = build_embedder_service(spec.embedder, spec.embedder_weights, device=dev)
             hub.add_embedder(spec.served_embedder_name or name, emb)
         if spec.reranker:
-            m, tok, name = build_encoder(spec.reranker, spec.reranker_weights, device=dev, reranker=True)
-            hub.add_reranker(spec.served_reranker_name or name, Reranker(m, tok, model_name=name))
+            rr, name = build_reranker_service(spec.reranker, spec.reranker_weights, device=dev)
+            hub.add_reranker(spec.served_reranker_name or name, rr)
         return hub
