@@ -223,6 +223,32 @@ void vit_embed(const Tensor& patches, const Tensor& cls, const Tensor& pos, Tens
   gai_vit_embed(patches.data_ptr(), cls.data_ptr(), pos.data_ptr(), out.data_ptr(), B, NP, D, cur_stream());
 }
 
+void gemm_splitk(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
+                 int64_t epi, Tensor& ws) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_dev(C, "C");
+  const int K = A.size(-1);
+  const int M = A.numel() / K;
+  const int N = B.size(0);
+  TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm_splitk: A and B must be contiguous");
+  TORCH_CHECK(B.size(1) == K, "gemm_splitk: K mismatch");
+  TORCH_CHECK(M <= 64 && K % 512 == 0, "gemm_splitk: needs M <= 64 and K % 512 == 0");
+  const bool f32 = C.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm_splitk: C must be bf16 or fp32");
+  const int ldc = epi == 4 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm_splitk: C has wrong size");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_cuda() &&
+                  (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K), "gemm_splitk: workspace too small");
+  if (bias) check_bf16(*bias, "bias");
+  if (R) {
+    check_bf16(*R, "residual");
+    TORCH_CHECK(R->numel() == (int64_t)M * N, "gemm_splitk: residual has wrong size");
+  }
+  gai_gemm_splitk(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr(bias), opt_ptr(R), M, N, K, ldc, (int)epi,
+                  f32 ? 1 : 0, ws.data_ptr<float>(), cur_stream());
+}
+
 void quant_rows_fp8(const Tensor& x, Tensor& q, Tensor& scale) {
   check_bf16(x, "x");
   check_dev(q, "q");
@@ -332,6 +358,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_write", &rope_kv_write);
   m.def("gemm", &gemm);
   m.def("gemm_fp8", &gemm_fp8);
+  m.def("gemm_splitk", &gemm_splitk);
+  m.def("gemm_splitk_ws_floats", [](int64_t M, int64_t N, int64_t K) {
+    return (int64_t)(gai_gemm_splitk_ws_bytes(M, N, K) / 4);
+  });
   m.def("patchify", &patchify);
   m.def("vit_embed", &vit_embed);
   m.def("quant_rows_fp8", &quant_rows_fp8);

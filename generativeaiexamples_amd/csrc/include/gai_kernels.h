@@ -26,6 +26,12 @@ void gai_gemm_fp8(const void* A, const void* B, const float* sa, const float* sb
                   const void* R, int M, int N, int K, int ldc, int epi, int out_f32, int force, hipStream_t st);
 void gai_quant_rows_fp8(const void* x, int M, int K, long ldx, void* q, float* scale, hipStream_t st);
 
+// gemm_splitk.hip (decode M <= 64: weight-streaming split-K; ws = fp32 [KS, M, N] partials)
+int gai_gemm_splitk_ks(int M, int N, int K);
+size_t gai_gemm_splitk_ws_bytes(int M, int N, int K);
+void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                     int ldc, int epi, int out_f32, float* ws, hipStream_t st);
+
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,

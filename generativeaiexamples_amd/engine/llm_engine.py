@@ -28,6 +28,7 @@ from .. import ops
 from ..models.common import ForwardBatch
 from .kv_cache import KVCache
 from .sampling import SamplingBatch, SamplingParams
+from .staging import HostStager
 from .tokenizer import IncrementalDetokenizer, Tokenizer
 
 
@@ -106,6 +107,10 @@ class LLMEngine:
                                                  mc.head_dim, max(cfg.max_model_len,
                                                                   getattr(model, "max_cross_tokens", 0)),
                                                  self.device)
+        self.stager = HostStager(self.device)
+        self._timing = os.environ.get("GAI_STEP_TIMING") == "1"
+        self.phase_ms: Dict[str, float] = {}
+        self._t_mark = 0.0
         self.requests: Dict[int, Request] = {}
         self.by_rid: Dict[str, Request] = {}
         self._ids = itertools.count(1)
@@ -179,16 +184,8 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ batch construction
     def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
-        sizes = [a.size for a in arrays]
-        flat = np.concatenate([a.reshape(-1).astype(np.int32, copy=False) for a in arrays]) if arrays else np.zeros(0, np.int32)
-        t = torch.from_numpy(flat)
-        if self.device.type == "cuda":
-            t = t.pin_memory().to(self.device, non_blocking=True)
-        out, o = [], 0
-        for a, n in zip(arrays, sizes):
-            out.append(t[o:o + n].view(*a.shape) if a.ndim > 1 else t[o:o + n])
-            o += n
-        return out
+        return self.stager.stage([np.asarray(a, dtype=np.int32) if np.asarray(a).dtype != np.int32 else a
+                                  for a in arrays])
 
     def _make_batch(self, b) -> tuple:
         P = b.num_prefill_tokens
@@ -267,14 +264,13 @@ class LLMEngine:
         if bs not in self.graphs:
             self._capture(bs)
         g, fb, logits = self.graphs[bs]
-        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx])
+        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx, b.decode_block_tables])
         fb.token_ids[:n].copy_(src[0])
         fb.positions[:n].copy_(src[1])
         fb.slots[:n].copy_(src[2])
         fb.decode_ctx[:n].copy_(src[3])
         mb = b.max_blocks
-        bt = self._to_device([b.decode_block_tables])[0]
-        fb.decode_block_tables[:n, :mb].copy_(bt)
+        fb.decode_block_tables[:n, :mb].copy_(src[4])
         if n < bs:  # padded rows: scratch page, ctx 1
             fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
             fb.decode_ctx[n:].fill_(1)
@@ -289,7 +285,11 @@ class LLMEngine:
     @torch.inference_mode()
     def step(self) -> List[RequestOutput]:
         with self.lock:
+            if self._timing:
+                self._t_mark = time.perf_counter()
             b = self.sched.schedule()
+            self.stager.reset()  # the previous step ended with a sync on its sampled tokens
+            self._mark("schedule")
             n_tok = b.num_tokens
             if n_tok == 0:
                 return []
@@ -309,13 +309,28 @@ class LLMEngine:
                     self.model.forward(fb, self.kv, self.decode_ws)
                     return []
                 logits = self.model.forward(fb, self.kv, self.decode_ws)
+            self._mark("forward")
             reqs = [self.requests.get(s) for s in seq_order]
             params = [r.params if r else SamplingParams() for r in reqs]
             self._penalize(logits, reqs)
-            sb = SamplingBatch(params, [r.seed if r else 0 for r in reqs], self.device)
+            sb = SamplingBatch(params, [r.seed if r else 0 for r in reqs], self.device, self.stager)
+            self._mark("penalize_pack")
             toks = ops.sample(logits, sb.temperature, sb.top_p, sb.top_k, sb.seeds, self.step_count)
+            self._mark("sample")
             toks = toks.cpu().tolist()
-            return self._process(seq_order, reqs, toks)
+            out = self._process(seq_order, reqs, toks)
+            self._mark("process")
+            return out
+
+    def _mark(self, phase: str):
+        """GAI_STEP_TIMING=1: synchronise and accumulate wall time per step phase in ``self.phase_ms``."""
+        if not self._timing:
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        self.phase_ms[phase] = self.phase_ms.get(phase, 0.0) + 1000 * (now - self._t_mark)
+        self._t_mark = now
 
     def _penalize(self, logits, reqs):
         rows = [i for i, r in enumerate(reqs) if r is not None and r.params.has_penalty and r.token_counts]
@@ -335,9 +350,7 @@ class LLMEngine:
             cnt[i, : len(k)] = [c for _, c in k]
             n[i] = len(k)
             f[i], p[i], rp[i] = r.params.frequency_penalty, r.params.presence_penalty, r.params.repetition_penalty
-        d = self.device
-        ops.apply_penalties(logits, *(torch.from_numpy(a).to(d) for a in (ids, cnt, n)),
-                            *(torch.from_numpy(a).to(d) for a in (f, p, rp)))
+        ops.apply_penalties(logits, *self.stager.stage([ids, cnt, n, f, p, rp]))
 
     def _process(self, seq_order, reqs, toks) -> List[RequestOutput]:
         outs: List[RequestOutput] = []

@@ -33,23 +33,15 @@ class SamplingParams:
 
 
 class SamplingBatch:
-    """Packs the per-row sampling parameters of one step into device tensors (one H2D copy)."""
+    """Packs the per-row sampling parameters of one step into device tensors (one staged H2D copy)."""
 
-    def __init__(self, params: List[SamplingParams], seeds: List[int], device):
-        n = len(params)
-        f = torch.empty(n, 2, dtype=torch.float32)
-        k = torch.empty(n, dtype=torch.int32)
-        s = torch.empty(n, dtype=torch.int64)
-        for i, p in enumerate(params):
-            f[i, 0] = 0.0 if p.top_k == 1 else p.temperature
-            f[i, 1] = p.top_p
-            k[i] = p.top_k
-            s[i] = seeds[i]
-        pin = device.type == "cuda"
-        if pin:
-            f, k, s = f.pin_memory(), k.pin_memory(), s.pin_memory()
-        f = f.to(device, non_blocking=True)
-        self.temperature = f[:, 0].contiguous()
-        self.top_p = f[:, 1].contiguous()
-        self.top_k = k.to(device, non_blocking=True)
-        self.seeds = s.to(device, non_blocking=True)
+    def __init__(self, params: List[SamplingParams], seeds: List[int], device, stager=None):
+        import numpy as np
+        temp = np.fromiter((0.0 if p.top_k == 1 else p.temperature for p in params), np.float32, len(params))
+        top_p = np.fromiter((p.top_p for p in params), np.float32, len(params))
+        top_k = np.fromiter((p.top_k for p in params), np.int32, len(params))
+        sd = np.asarray(seeds, dtype=np.int64)
+        if stager is None:
+            from .staging import HostStager
+            stager = HostStager(device, 1024)
+        self.temperature, self.top_p, self.top_k, self.seeds = stager.stage([temp, top_p, top_k, sd])

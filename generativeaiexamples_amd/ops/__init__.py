@@ -122,8 +122,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
     if out is None:
         out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
-    native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE)
+    _native_gemm(x2, w, out, bias, residual, epi)
     return out
+
+
+_SPLITK = os.environ.get("GAI_SPLITK", "1") == "1"
+
+
+def _native_gemm(x2, w, out, bias, residual, epi):
+    """Hand-written MFMA GEMM: the weight-streaming split-K kernel for decode-sized M (<= 64),
+    otherwise the skinny / 128x128 / 256x256 kernels chosen inside gai_gemm."""
+    M, K = x2.shape
+    if _SPLITK and _GEMM_FORCE == 0 and M <= 64 and K % 512 == 0:
+        nat = native()
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x2.device)
+        nat.gemm_splitk(x2, w, out, bias, residual, epi, ws)
+    else:
+        native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE)
 
 
 def _blas_linear(x2, w, bias, act, out_dtype):
@@ -264,7 +279,7 @@ class GemmTuner:
         epi = EPI[act] if act else (EPI["bias"] if has_bias else 0)
 
         def run_native():
-            native().gemm(x2, w, out, bias, None, epi, _GEMM_FORCE)
+            _native_gemm(x2, w, out, bias, None, epi)
 
         def run_blas():
             _blas_linear(x2, w, bias, act, out_dtype)

@@ -45,6 +45,23 @@ def bench_gemm(rows, shapes):
                          ours_gbs=by / t_ours / 1e6, speedup=t_blas / t_ours))
 
 
+def bench_decode_gemm(rows, shapes):
+    """Decode GEMMs: split-K weight-streaming kernel vs the skinny kernel vs hipBLASLt (weight bytes / time)."""
+    nat = ops.native()
+    for M, N, K, tag in shapes:
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), device="cuda", dtype=torch.float32)
+        t_sk = timeit(lambda: nat.gemm_splitk(x, w, out, None, None, 0, ws))
+        t_sn = timeit(lambda: nat.gemm(x, w, out, None, None, 0, 1))
+        t_bl = timeit(lambda: torch.matmul(x, w.t()))
+        wb = N * K * 2
+        rows.append(dict(op="decode_gemm", tag=tag, M=M, N=N, K=K, splitk_ms=t_sk, skinny_ms=t_sn, hipblaslt_ms=t_bl,
+                         splitk_tbs=wb / t_sk / 1e9, skinny_tbs=wb / t_sn / 1e9, hipblaslt_tbs=wb / t_bl / 1e9,
+                         speedup_vs_blas=t_bl / t_sk))
+
+
 def bench_fp8(rows, shapes):
     """fp8 GEMM (block-scaled MFMA) alone and with the fused per-token quantiser, vs bf16 hipBLASLt and
     (when this torch build has it) hipBLASLt fp8 via torch._scaled_mm."""
@@ -145,6 +162,13 @@ def main():
             (16384, 1024, 1024, "e5 qkv-ish"), (16384, 4096, 1024, "e5 ffn up"),
         ]
         bench_gemm(rows, shapes)
+    if "decode_gemm" in only:
+        sh = []
+        for M in (1, 16, 32, 64):
+            sh += [(M, 6144, 4096, f"qkv b{M}"), (M, 4096, 4096, f"o b{M}"), (M, 28672, 4096, f"gate_up b{M}"),
+                   (M, 4096, 14336, f"down b{M}")]
+        sh += [(64, 128256, 4096, "lm_head b64")]
+        bench_decode_gemm(rows, sh)
     if "fp8" in only:
         bench_fp8(rows, [(4096, 6144, 4096, "qkv prefill"), (4096, 28672, 4096, "gate_up prefill"),
                          (4096, 4096, 14336, "down prefill"), (8192, 8192, 8192, "square 8k"),
