@@ -26,7 +26,8 @@ def main(argv=None):
     ap.add_argument("--evaluate", type=_bool, nargs="?", const=True, default=True)
     ap.add_argument("--generate_synthetic", type=_bool, nargs="?", const=True, default=False)
     ap.add_argument("--docs", type=str, default="")
-    ap.add_argument("--ga_input", type=str, default="")
+    ap.add_argument("--ga_input", type=str, default="", help="QA JSON, or a ground-truth .txt in the medical-device "
+                    "example's 'Example n: / Question: / Answer:' format")
     ap.add_argument("--ga_output", type=str, default="")
     ap.add_argument("--sd_output", type=str, default="qa_generation.json")
     ap.add_argument("--ev_input", type=str, default="")
@@ -45,7 +46,13 @@ def main(argv=None):
         generate_synthetic_data(a.docs, a.sd_output, ChatFn(a.judge_base_url, a.judge_llm_model, temperature=0.2))
     if a.generate_answer:
         from .answer_generator import generate_answers
-        generate_answers(a.base_url, a.docs or None, a.ga_input, a.ga_output)
+        qa_file = a.ga_input
+        if qa_file.endswith(".txt"):
+            from ..examples.medical_device import parse_gt_qa_txt
+            qa_file = a.ga_input[:-4] + ".json"
+            with open(a.ga_input, encoding="utf-8") as f, open(qa_file, "w", encoding="utf-8") as g:
+                json.dump(parse_gt_qa_txt(f.read()), g, indent=2)
+        generate_answers(a.base_url, a.docs or None, qa_file, a.ga_output)
     if a.evaluate and a.ev_input:
         import os
         os.makedirs(os.path.dirname(a.ev_result) or ".", exist_ok=True)

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _services():
-    for f in glob.glob(f"{ROOT}/deploy/compose/*.yaml") + glob.glob(f"{ROOT}/RAG/examples/*/*/docker-compose.yaml"):
+    for f in glob.glob(f"{ROOT}/deploy/compose/*.yaml") + glob.glob(f"{ROOT}/RAG/examples/**/docker-compose.yaml", recursive=True):
         doc = yaml.safe_load(open(f))
         for name, svc in (doc.get("services") or {}).items():
             yield f, name, svc
