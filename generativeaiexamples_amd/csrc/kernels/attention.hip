@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
 // ----------------------------------------------------------------------------------------------
 // Decode
 // ----------------------------------------------------------------------------------------------
-template <int D>
+template <int D, bool PIPE>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
@@ -250,32 +250,41 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   float m_run = kNeg, l_run = 0.f;
   const float sl2 = scale * kLog2e;
 
-  for (int kb = kstart + 32 * wid; kb < kend; kb += 128) {
-    const int p0 = kb / kBS;
+  // K/V of one 32-key chunk (2 pages) per wave: K rows for the QK^T MFMA (lane: key lane&15, 16 B of
+  // dims 32t + 8gq) and the V^T columns for the PV MFMA. Software-pipelined one chunk ahead with a
+  // register double buffer: the next chunk's loads are in flight while this chunk's MFMAs / softmax run.
+  // Addresses of a chunk past the split are clamped to its last page (unconditional loads: a
+  // data-dependent branch around them would force vmcnt(0) waits), and such a chunk is never computed.
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  struct Chunk {
+    bf16x8 k[2][D / 32];
+    bf16x4_t vlo[D / 16], vhi[D / 16];
+  };
+  const int last_page = (kend - 1) / kBS;
+  auto load_chunk = [&](int kb, Chunk& c) {
+    const int p0 = min(kb / kBS, last_page);
     const int blk0 = bt[p0];
     const int blk1 = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : blk0;
     const size_t pb0 = ((size_t)blk0 * Hkv + g) * kBS * D, pb1 = ((size_t)blk1 * Hkv + g) * kBS * D;
-    // issue all loads of the chunk first
-    bf16x8 kf[2][D / 32];
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
-      kf[0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
-      kf[1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+      c.k[0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+      c.k[1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
     }
-    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-    bf16x4_t vlo[D / 16], vhi[D / 16];
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       const size_t off = (size_t)(16 * dt + (lane & 15)) * kBS + 4 * gq;
-      vlo[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
-      vhi[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
+      c.vlo[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
+      c.vhi[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
     }
+  };
+  auto compute_chunk = [&](int kb, const Chunk& c) {
     f32x4 s[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       s[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < D / 32; ++t) s[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[i][t], qf[t], s[i], 0, 0, 0);
+      for (int t = 0; t < D / 32; ++t) s[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[i][t], qf[t], s[i], 0, 0, 0);
     }
     float mt = kNeg;
 #pragma unroll
@@ -297,9 +306,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[i][r] - m_new);
-        rs += p;
-        pf[4 * i + r] = (bf16)p;
+        const float pv = exp2f(s[i][r] - m_new);
+        rs += pv;
+        pf[4 * i + r] = (bf16)pv;
       }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
@@ -308,8 +317,33 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       acc_o[dt] *= alpha;
-      const bf16x8 vf = {vlo[dt][0], vlo[dt][1], vlo[dt][2], vlo[dt][3], vhi[dt][0], vhi[dt][1], vhi[dt][2], vhi[dt][3]};
+      const bf16x8 vf = {c.vlo[dt][0], c.vlo[dt][1], c.vlo[dt][2], c.vlo[dt][3],
+                         c.vhi[dt][0], c.vhi[dt][1], c.vhi[dt][2], c.vhi[dt][3]};
       acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, acc_o[dt], 0, 0, 0);
+    }
+  };
+
+  int kb = kstart + 32 * wid;
+  if (PIPE) {
+    if (kb < kend) {
+      Chunk ca, cb;
+      load_chunk(kb, ca);
+      for (;;) {
+        load_chunk(kb + 128, cb);
+        compute_chunk(kb, ca);
+        kb += 128;
+        if (kb >= kend) break;
+        load_chunk(kb + 128, ca);
+        compute_chunk(kb, cb);
+        kb += 128;
+        if (kb >= kend) break;
+      }
+    }
+  } else {
+    for (; kb < kend; kb += 128) {
+      Chunk c;
+      load_chunk(kb, c);
+      compute_chunk(kb, c);
     }
   }
 
@@ -419,9 +453,11 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
   if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
   const dim3 grid(max_splits, Hkv, B);
+  static const bool pipe = getenv("GAI_DECODE_PIPE") && atoi(getenv("GAI_DECODE_PIPE")) != 0;
 #define GAI_DEC(DD)                                                                                             \
   if (D == DD) {                                                                                                \
-    attn_decode_kernel<DD><<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,    \
+    auto kern = pipe ? attn_decode_kernel<DD, true> : attn_decode_kernel<DD, false>;                           \
+    kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,    \
                                                  block_tables, max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, \
                                                  Hq, Hkv, scale, split_keys, max_splits);                       \
     GAI_LAUNCH_CHECK();                                                                                         \

@@ -340,19 +340,37 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
 
 
 class DecodeWorkspace:
-    """Split-KV partial buffers for attention_decode (sized once; graph-capture safe)."""
+    """Split-KV partial buffers for attention_decode, sized once for the finest split (128 keys) so the
+    split can be chosen per call / per captured batch bucket (graph-capture safe)."""
+
+    MIN_SPLIT = 128
 
     def __init__(self, max_batch: int, Hq: int, D: int, max_ctx: int, device, split_keys: int | None = None):
-        self.split_keys = split_keys or self.choose_split(max_ctx)
-        self.max_splits = max(1, (max_ctx + self.split_keys - 1) // self.split_keys)
+        self.fixed_split = split_keys
+        self.max_ctx = max_ctx
+        self.max_splits = max(1, (max_ctx + self.MIN_SPLIT - 1) // self.MIN_SPLIT)
         self.o = torch.empty(self.max_splits * max_batch * Hq * D, dtype=torch.float32, device=device)
         self.ml = torch.empty(self.max_splits * max_batch * Hq * 2, dtype=torch.float32, device=device)
 
+    @property
+    def split_keys(self) -> int:
+        return self.fixed_split or self.choose_split(self.max_ctx)
+
     @staticmethod
-    def choose_split(max_ctx: int) -> int:
-        # ~8-16 splits over the longest context, each a multiple of 128 keys (4 waves x 32)
-        s = max(128, ((max_ctx // 12) + 127) // 128 * 128)
-        return min(s, 2048)
+    def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int = 2048) -> int:
+        """Split length (multiple of 128) giving ~target_wgs workgroups of (split, kv-head, sequence):
+        measured on MI355X (B=64, 8 KV heads, ctx 2.6k) 4.5 TB/s at 256-key splits vs 5.1 TB/s at 1024 -
+        long per-wave streams amortise the per-workgroup prologue/combine, while small batches still
+        need many splits to fill 256 CUs."""
+        nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
+        s = -(-max_ctx // nsplit)
+        s = (s + 127) // 128 * 128
+        return int(min(max(s, 128), 2048))
+
+    def split_for(self, batch: int, hkv: int, max_ctx: int) -> int:
+        if self.fixed_split:
+            return self.fixed_split
+        return self.choose_split(max_ctx, batch, hkv)
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
@@ -360,12 +378,14 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
     if not q.is_cuda:
         return _into(out, ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale))
     B, Hq, D = q.shape
+    mc = max_ctx if max_ctx is not None else int(ctx_lens.max())
     if ws is None:
-        mc = max_ctx if max_ctx is not None else int(ctx_lens.max())
         ws = DecodeWorkspace(B, Hq, D, mc, q.device)
+    split = ws.split_for(B, k_cache.shape[1], mc)
+    nsplit = (mc + split - 1) // split
+    assert nsplit <= ws.max_splits, "decode workspace too small for this context"
     out = torch.empty_like(q) if out is None else out
-    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, ws.split_keys,
-                         ws.max_splits)
+    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, split, nsplit)
     return out
 
 

@@ -107,7 +107,7 @@ def bench_prefill(rows, B, S, Hq, Hkv, D):
                      ours_tflops=fl / t / 1e9, sdpa_tflops=fl / t_sdpa / 1e9))
 
 
-def bench_decode(rows, B, ctx, Hq, Hkv, D):
+def bench_decode(rows, B, ctx, Hq, Hkv, D, split=None):
     nbps = (ctx + 15) // 16
     nb = B * nbps
     kc = torch.randn(nb, Hkv, 16, D, device="cuda", dtype=torch.bfloat16)
@@ -115,10 +115,10 @@ def bench_decode(rows, B, ctx, Hq, Hkv, D):
     bt = torch.randperm(nb, device="cuda").int().reshape(B, nbps)
     q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
     cl = torch.full((B,), ctx, device="cuda", dtype=torch.int32)
-    ws = ops.DecodeWorkspace(B, Hq, D, ctx, "cuda")
+    ws = ops.DecodeWorkspace(B, Hq, D, ctx, "cuda", split_keys=split)
     t = timeit(lambda: ops.attention_decode(q, kc, vc, bt, cl, 1 / math.sqrt(D), ws=ws))
     by = 2 * B * ctx * Hkv * D * 2
-    rows.append(dict(op="attn_decode", B=B, ctx=ctx, Hq=Hq, Hkv=Hkv, D=D, split=ws.split_keys, ours_ms=t,
+    rows.append(dict(op="attn_decode", B=B, ctx=ctx, Hq=Hq, Hkv=Hkv, D=D, split=ws.split_for(B, Hkv, ctx), ours_ms=t,
                      ours_gbs=by / t / 1e6))
 
 
@@ -176,6 +176,9 @@ def main():
     if "prefill" in only:
         bench_prefill(rows, 4, 2048, 32, 8, 128)
         bench_prefill(rows, 64, 512, 16, 16, 64)
+    if "decode_sweep" in only:
+        for sp in (128, 256, 512, 1024, 2048):
+            bench_decode(rows, 64, 2600, 32, 8, 128, sp)
     if "decode" in only:
         bench_decode(rows, 64, 2304, 32, 8, 128)
         bench_decode(rows, 1, 2304, 32, 8, 128)
