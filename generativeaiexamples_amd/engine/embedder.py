@@ -20,6 +20,7 @@ import torch
 
 from ..models.bert import BertModel
 from .tokenizer import Tokenizer
+from ..utils.profiling import roctx_range
 
 
 class TruncationError(ValueError):
@@ -86,7 +87,8 @@ class Embedder:
         return out
 
     def embed(self, texts: Sequence[str], input_type: str = "passage", truncate: str = "END") -> torch.Tensor:
-        return self.embed_ids([self.tokenize(t, input_type, truncate) for t in texts])
+        with roctx_range("embed"):
+            return self.embed_ids([self.tokenize(t, input_type, truncate) for t in texts])
 
 
 class ClipEmbedder:

@@ -29,6 +29,7 @@ from ..models.common import ForwardBatch
 from .kv_cache import KVCache
 from .sampling import SamplingBatch, SamplingParams
 from .staging import HostStager
+from ..utils.profiling import roctx_range
 from .tokenizer import IncrementalDetokenizer, Tokenizer
 
 
@@ -299,16 +300,17 @@ class LLMEngine:
             self.stats["prefill_tokens"] += P
             self.stats["decode_tokens"] += n_tok - P
             nd = len(b.decode_seq_ids)
-            if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
-                    and self._graph_bucket(nd) is not None):
-                seq_order = list(b.decode_seq_ids)
-                logits = self._run_graph(b, nd)
-            else:
-                fb, seq_order = self._make_batch(b)
-                if not seq_order:
-                    self.model.forward(fb, self.kv, self.decode_ws)
-                    return []
-                logits = self.model.forward(fb, self.kv, self.decode_ws)
+            with roctx_range("prefill" if P else "decode"):
+                if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
+                        and self._graph_bucket(nd) is not None):
+                    seq_order = list(b.decode_seq_ids)
+                    logits = self._run_graph(b, nd)
+                else:
+                    fb, seq_order = self._make_batch(b)
+                    if not seq_order:
+                        self.model.forward(fb, self.kv, self.decode_ws)
+                        return []
+                    logits = self.model.forward(fb, self.kv, self.decode_ws)
             self._mark("forward")
             reqs = [self.requests.get(s) for s in seq_order]
             params = [r.params if r else SamplingParams() for r in reqs]

@@ -170,6 +170,11 @@ class HBMIndex:
 
     def search_raw(self, queries: torch.Tensor, k: int):
         """-> (relevance [nq, k'], rows [nq, k']) on device."""
+        from ..utils.profiling import roctx_range
+        with roctx_range("index_search"):
+            return self._search_raw(queries, k)
+
+    def _search_raw(self, queries: torch.Tensor, k: int):
         q = self._prep(queries if queries.ndim == 2 else queries[None])
         with self.lock:
             if self.n == 0:

@@ -16,6 +16,7 @@ from typing import List, Tuple
 import torch
 import torch.distributed as dist
 
+from ..parallel.fault import guard
 from .hbm_index import HBMIndex
 
 
@@ -43,7 +44,8 @@ class ShardedIndex:
         if src.dtype == torch.bfloat16 and dev.type == "cpu":
             src = src.float()
         parts = [torch.empty_like(src) for _ in range(self.world)]
-        dist.all_gather(parts, src.contiguous(), group=self.group)
+        with guard("index_all_gather", self.rank):
+            dist.all_gather(parts, src.contiguous(), group=self.group)
         return [p.to(t.device, t.dtype) for p in parts]
 
     def _gather_var(self, t: torch.Tensor) -> Tuple[torch.Tensor, List[int]]:

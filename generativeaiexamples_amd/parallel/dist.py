@@ -18,6 +18,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from .fault import RankFailure, guard  # noqa: F401  (re-exported)
+
 
 @dataclass
 class DistContext:
@@ -47,12 +49,13 @@ class DistContext:
     # ---------------- collectives (no-ops when the group has one member) ----------------
     def tp_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
-            if t.is_cuda or t.dtype in (torch.float32, torch.float64):
-                dist.all_reduce(t, group=self.tp_group)
-            else:  # gloo (CPU test tier): reduce reduced-precision tensors in fp32
-                f = t.float()
-                dist.all_reduce(f, group=self.tp_group)
-                t.copy_(f)
+            with guard("tp_all_reduce", self.rank):
+                if t.is_cuda or t.dtype in (torch.float32, torch.float64):
+                    dist.all_reduce(t, group=self.tp_group)
+                else:  # gloo (CPU test tier): reduce reduced-precision tensors in fp32
+                    f = t.float()
+                    dist.all_reduce(f, group=self.tp_group)
+                    t.copy_(f)
         return t
 
     def tp_all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
@@ -60,22 +63,25 @@ class DistContext:
         if self.tp_size == 1:
             return t
         parts = [torch.empty_like(t) for _ in range(self.tp_size)]
-        dist.all_gather(parts, t.contiguous(), group=self.tp_group)
+        with guard("tp_all_gather", self.rank):
+            dist.all_gather(parts, t.contiguous(), group=self.tp_group)
         return torch.cat(parts, dim=-1)
 
     def all_gather_obj(self, obj, group=None):
         if not self.is_distributed:
             return [obj]
         out = [None] * (dist.get_world_size(group) if group is not None else self.world_size)
-        dist.all_gather_object(out, obj, group=group)
+        with guard("all_gather_object", self.rank):
+            dist.all_gather_object(out, obj, group=group)
         return out
 
     def barrier(self):
         if self.is_distributed:
-            if self.backend == "nccl":
-                dist.barrier(device_ids=[self.local_rank])
-            else:
-                dist.barrier()
+            with guard("barrier", self.rank):
+                if self.backend == "nccl":
+                    dist.barrier(device_ids=[self.local_rank])
+                else:
+                    dist.barrier()
 
 
 _CTX: DistContext | None = None
@@ -90,12 +96,15 @@ def get_context() -> DistContext:
     return _CTX
 
 
-def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int = 600) -> DistContext:
+def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int | None = None) -> DistContext:
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 
     Falls back to a single-process context when WORLD_SIZE is unset or 1.
     """
     global _CTX
+    timeout_s = timeout_s or int(os.environ.get("GAI_DIST_TIMEOUT_S", "600"))
+    # a hung RCCL collective aborts the communicator (-> RankFailure) instead of blocking forever
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))

@@ -9,6 +9,10 @@ disconnect aborts its request (frees its KV blocks) immediately.
 from __future__ import annotations
 
 import asyncio
+import faulthandler
+import logging
+import os
+import sys
 import threading
 import time
 import uuid
@@ -28,16 +32,44 @@ class StreamItem:
     finish_reason: Optional[str]
 
 
+log = logging.getLogger(__name__)
+
+
 class AsyncLLMEngine:
-    def __init__(self, engine: LLMEngine):
+    """``watchdog_s`` (env GAI_WATCHDOG_S, default 300): a step running longer than this (hung kernel or
+    collective) marks the engine unhealthy - /v1/health/ready turns 503 so a router drains it - dumps
+    every thread's stack and fails the waiting requests instead of leaving clients hanging."""
+
+    def __init__(self, engine: LLMEngine, watchdog_s: Optional[float] = None):
         self.engine = engine
         self.queues: Dict[str, tuple] = {}
         self.cv = threading.Condition()
         self.running = True
         self.healthy = True
         self.error: Optional[BaseException] = None
+        self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("GAI_WATCHDOG_S", "300"))
+        self._step_started: Optional[float] = None
         self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
         self.thread.start()
+        self.watchdog = threading.Thread(target=self._watch, daemon=True, name="llm-watchdog")
+        self.watchdog.start()
+
+    def _fail_all(self, e: BaseException):
+        for rid, (loop, q) in list(self.queues.items()):
+            loop.call_soon_threadsafe(q.put_nowait, e)
+        self.queues.clear()
+
+    def _watch(self):
+        period = max(0.05, min(1.0, self.watchdog_s / 4))
+        while self.running:
+            time.sleep(period)
+            t = self._step_started
+            if t is not None and self.healthy and time.perf_counter() - t > self.watchdog_s:
+                err = TimeoutError(f"engine step exceeded the {self.watchdog_s:.1f}s watchdog")
+                self.error, self.healthy = err, False
+                log.error("%s; dumping thread stacks", err)
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                self._fail_all(err)
 
     @property
     def tokenizer(self):
@@ -52,14 +84,14 @@ class AsyncLLMEngine:
             if not self.running:
                 break
             try:
-                t0 = time.perf_counter()
+                t0 = self._step_started = time.perf_counter()
                 outs = eng.step()
-                METRICS.observe_step(time.perf_counter() - t0, len(outs))
+                self._step_started = None
+                METRICS.observe_step(time.perf_counter() - t0, len(outs), eng)
             except BaseException as e:  # engine failure: fail every pending request, keep serving health
+                self._step_started = None
                 self.error, self.healthy = e, False
-                for rid, (loop, q) in list(self.queues.items()):
-                    loop.call_soon_threadsafe(q.put_nowait, e)
-                self.queues.clear()
+                self._fail_all(e)
                 continue
             for o in outs:
                 ent = self.queues.get(o.request_id)

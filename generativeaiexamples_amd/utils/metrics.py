@@ -44,15 +44,40 @@ class Metrics:
                                     registry=r)
             self.rerank = Histogram("gai_rerank_seconds", "rerank latency", buckets=_BUCKETS, registry=r)
             self.api_requests = Counter("api_requests_total", "HTTP API requests", ["route"], registry=r)
+            self.tpot = Histogram("gai_tpot_seconds", "time per output token (decode step latency)",
+                                  buckets=(0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5), registry=r)
+            self.prefill_tokens = Counter("gai_prefill_tokens_total", "prompt tokens prefilled", registry=r)
+            self.decode_tokens = Counter("gai_decode_tokens_total", "tokens decoded", registry=r)
+            self.queue = Gauge("gai_waiting_requests", "requests waiting for admission", registry=r)
+            self.collective = Histogram("gai_collective_seconds", "host-observed collective latency", ["op"],
+                                        buckets=(1e-5, 1e-4, 1e-3, 1e-2, 0.1, 1.0), registry=r)
         else:  # pragma: no cover
             self.registry = None
             for n in ("requests_total", "prompt_tokens", "generation_tokens", "ttft", "e2e", "step", "batch",
-                      "kv_usage", "embed", "search", "rerank", "api_requests"):
+                      "kv_usage", "embed", "search", "rerank", "api_requests", "tpot", "prefill_tokens",
+                      "decode_tokens", "queue", "collective"):
                 setattr(self, n, _Null())
 
-    def observe_step(self, dt: float, n: int):
+    def observe_step(self, dt: float, n: int, engine=None):
         self.step.observe(dt)
         self.batch.set(n)
+        if engine is not None:  # token counters / KV usage / TPOT from the engine's running stats
+            st = engine.stats
+            last = getattr(engine, "_metrics_last", (0, 0))
+            dp, dd = st["prefill_tokens"] - last[0], st["decode_tokens"] - last[1]
+            engine._metrics_last = (st["prefill_tokens"], st["decode_tokens"])
+            if dp:
+                self.prefill_tokens.inc(dp)
+            if dd:
+                self.decode_tokens.inc(dd)
+                if not dp:
+                    self.tpot.observe(dt)
+            try:
+                sch = engine.sched
+                self.kv_usage.set(1.0 - sch.num_free_blocks() / max(1, sch.num_blocks()))
+                self.queue.set(sch.num_waiting())
+            except Exception:  # pragma: no cover - scheduler without counters
+                pass
 
     def render(self) -> bytes:
         return generate_latest(self.registry) if self.registry is not None else b""

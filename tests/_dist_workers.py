@@ -88,3 +88,32 @@ def sharded_index_worker(rank, world, port, out_dir):
                os.path.join(out_dir, f"idx_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def fault_worker(rank, world, port, out_dir, mode):
+    """mode 'kill': rank 1 dies at its 3rd collective; rank 0 must get RankFailure (not hang).
+    mode 'delay': rank 1 sleeps 300 ms before every collective; rank 0 observes the delay."""
+    import time
+
+    if mode == "kill":
+        os.environ.update(FI_KILL_RANK="1", FI_KILL_AT_CALL="3", GAI_DIST_TIMEOUT_S="30")
+    else:
+        os.environ.update(FI_DELAY_ALLREDUCE_MS="300", FI_DELAY_RANK="1")
+    from generativeaiexamples_amd.parallel import fault
+
+    fault.INJECTOR.reload()
+    ctx = _init(rank, world, port, 2)
+    t = torch.ones(8)
+    status, t0 = "ok", time.perf_counter()
+    try:
+        for _ in range(6):
+            ctx.tp_all_reduce(t)
+    except fault.RankFailure as e:
+        status = "rank_failure: " + str(e)[:200]
+    dt = time.perf_counter() - t0
+    with open(os.path.join(out_dir, f"fault_{mode}_{rank}.txt"), "w") as f:
+        f.write(f"{status}\n{dt}\n{t[0].item()}\n")
+    if mode == "delay":
+        dist.destroy_process_group()
+    else:
+        os._exit(0)  # the peer is gone: skip teardown of the broken group

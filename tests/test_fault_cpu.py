@@ -1,0 +1,84 @@
+"""Failure detection / fault injection on the CPU tier: a rank killed mid-run is
+detected as RankFailure by its peer (no hang), injected collective delays are observed, and the
+serving engine's watchdog fails requests of a hung step and reports unhealthy."""
+import asyncio
+import socket
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+from tests import _dist_workers as W
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(180)
+def test_killed_rank_is_detected(tmp_path):
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=W.fault_worker, args=(r, 2, port, str(tmp_path), "kill")) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert procs[1].exitcode == 17  # injected crash
+    status = (tmp_path / "fault_kill_0.txt").read_text().splitlines()
+    assert status[0].startswith("rank_failure"), status
+    assert "tp_all_reduce" in status[0]
+
+
+@pytest.mark.timeout(180)
+def test_injected_delay(tmp_path):
+    mp.spawn(W.fault_worker, args=(2, _port(), str(tmp_path), "delay"), nprocs=2, join=True)
+    s0 = (tmp_path / "fault_delay_0.txt").read_text().splitlines()
+    assert s0[0] == "ok" and float(s0[1]) > 6 * 0.3 * 0.9  # rank 0 waited for the delayed peer
+    assert float(s0[2]) == 2.0 ** 6
+
+
+def test_watchdog_fails_hung_step():
+    from generativeaiexamples_amd.engine.llm_engine import RequestOutput
+    from generativeaiexamples_amd.serving.async_engine import AsyncLLMEngine
+
+    class Req:
+        finished = False
+
+    class HungEngine:
+        tok = None
+
+        def __init__(self):
+            self.work = False
+
+        def add_request(self, ids, params, rid, images=None):
+            self.work = True
+            return Req()
+
+        def has_work(self):
+            return self.work
+
+        def step(self):
+            time.sleep(3.0)
+            return [RequestOutput("x", 1, "a", True, "stop")]
+
+        def abort(self, rid):
+            return True
+
+    eng = AsyncLLMEngine(HungEngine(), watchdog_s=0.5)
+
+    async def go():
+        out = []
+        with pytest.raises(RuntimeError, match="watchdog"):
+            async for it in eng.generate([1, 2, 3], None, "r1"):
+                out.append(it)
+
+    t0 = time.perf_counter()
+    asyncio.run(go())
+    assert time.perf_counter() - t0 < 2.5  # failed by the watchdog, not after the 3 s step
+    assert not eng.healthy
+    eng.running = False
