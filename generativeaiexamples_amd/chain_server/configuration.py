@@ -20,6 +20,8 @@ class VectorStoreConfig(ConfigWizard):
     index_type: str = configfield("indexType", default="FLAT", help_txt="exact brute-force (FLAT)")
     metric: str = configfield("metric", default="cosine", help_txt="cosine | ip | l2")
     persist_dir: str = configfield("persistDir", default="", help_txt="directory for index snapshots + WAL")
+    hybrid: bool = configfield("hybrid", default=False,
+                               help_txt="also keep a BM25 sparse index (enables retriever nrPipeline hybrid / ranked_hybrid)")
 
 
 @configclass

@@ -169,7 +169,8 @@ def get_vectorstore(embeddings: Optional[Embeddings] = None, collection: Optiona
             dev = embeddings.e.model.device
     except Exception:
         dev = None
-    return get_store(collection or collection_name(), embeddings, c.metric, c.persist_dir or None, device=dev)
+    return get_store(collection or collection_name(), embeddings, c.metric, c.persist_dir or None, device=dev,
+                     hybrid=bool(c.hybrid))
 
 
 def get_docs_vectorstore(store: VectorStore) -> List[str]:

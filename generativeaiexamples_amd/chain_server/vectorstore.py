@@ -10,6 +10,7 @@ import os
 import threading
 from typing import Dict, List, Optional, Tuple
 
+from ..index.bm25 import BM25Index, rrf
 from ..index.hbm_index import Document, HBMIndex
 from ..utils.metrics import METRICS
 from .connectors import Embeddings
@@ -29,8 +30,9 @@ class Retriever:
 
 class VectorStore:
     def __init__(self, name: str, embeddings: Embeddings, metric: str = "cosine", device=None,
-                 persist_dir: Optional[str] = None, batch: int = 256):
+                 persist_dir: Optional[str] = None, batch: int = 256, hybrid: bool = False):
         self.name, self.emb, self.batch = name, embeddings, batch
+        self.bm25: Optional[BM25Index] = BM25Index() if hybrid else None
         self.persist = os.path.join(persist_dir, name) if persist_dir else None
         self.lock = threading.Lock()
         if self.persist and os.path.exists(os.path.join(self.persist, "index.json")):
@@ -40,6 +42,9 @@ class VectorStore:
             self.index = HBMIndex(embeddings.dim or 1024, metric, device=device, name=name)
         if self.persist:
             self.index.attach_wal(self.persist)
+        if self.bm25 is not None and len(self.index):  # rebuild the sparse side from the restored documents
+            live = self.index.live_rows()
+            self.bm25.add(live, [self.index.document(r).page_content for r in live])
 
     def add_documents(self, docs: List[Document]) -> List[int]:
         rows: List[int] = []
@@ -48,7 +53,10 @@ class VectorStore:
             vecs = self.emb.embed_tensor([d.page_content for d in part], "passage")
             if self.index.dim != vecs.shape[1] and len(self.index) == 0:
                 self.index = HBMIndex(vecs.shape[1], self.index.metric, device=self.index.device, name=self.name)
-            rows += self.index.add(vecs, part)
+            new_rows = self.index.add(vecs, part)
+            rows += new_rows
+            if self.bm25 is not None:
+                self.bm25.add(new_rows, [d.page_content for d in part])
         if self.persist:
             self.index.save(self.persist)
         return rows
@@ -66,6 +74,20 @@ class VectorStore:
         METRICS.search.observe(time.perf_counter() - t0)
         return [(h.document, h.score) for h in hits]
 
+    def hybrid_search(self, query: str, k: int = 4, candidates: int = 40) -> List[Tuple[Document, float]]:
+        """Dense (HBM cosine top-``candidates``) + sparse (BM25 top-``candidates``) fused by reciprocal rank."""
+        import time
+
+        if self.bm25 is None:
+            return self.similarity_search_with_relevance_scores(query, k)
+        t0 = time.perf_counter()
+        q = self.emb.embed_tensor([query], "query")
+        dense = [h.row for h in self.index.search(q, candidates)[0]]
+        sparse = [r for r, _ in self.bm25.search(query, candidates)]
+        fused = rrf([dense, sparse], k)
+        METRICS.search.observe(time.perf_counter() - t0)
+        return [(self.index.document(r), s) for r, s in fused]
+
     def similarity_search(self, query: str, k: int = 4) -> List[Document]:
         return [d for d, _ in self.similarity_search_with_relevance_scores(query, k)]
 
@@ -74,6 +96,10 @@ class VectorStore:
 
     def delete_filename(self, filename: str) -> bool:
         n = self.index.delete_filename(filename)
+        if self.bm25 is not None and n:  # deletes may compact (renumber) the dense rows: rebuild the sparse side
+            self.bm25 = BM25Index()
+            live = self.index.live_rows()
+            self.bm25.add(live, [self.index.document(r).page_content for r in live])
         if self.persist and n:
             self.index.save(self.persist)
         return n > 0
@@ -90,10 +116,10 @@ _LOCK = threading.Lock()
 
 
 def get_store(name: str, embeddings: Embeddings, metric: str = "cosine", persist_dir: Optional[str] = None,
-              device=None) -> VectorStore:
+              device=None, hybrid: bool = False) -> VectorStore:
     with _LOCK:
         if name not in _STORES:
-            _STORES[name] = VectorStore(name, embeddings, metric, device, persist_dir)
+            _STORES[name] = VectorStore(name, embeddings, metric, device, persist_dir, hybrid=hybrid)
         return _STORES[name]
 
 

@@ -69,7 +69,18 @@ class BasicRAG(BaseExample):
         return get_llm(**kwargs).stream(msgs)
 
     def retrieve(self, query: str):
+        """Dense top-k with the score threshold; with a hybrid store (APP_VECTORSTORE_HYBRID=true) the
+        retriever's nrPipeline selects BM25+dense reciprocal-rank fusion ('hybrid') or fusion of 40
+        candidates reranked to top-k ('ranked_hybrid', the reference NeMo-Retriever default)."""
         r = self.cfg.retriever
+        if self.store.bm25 is not None and r.nr_pipeline in ("hybrid", "ranked_hybrid"):
+            from ..chain_server.utils import get_ranking_model
+            ranker = get_ranking_model() if r.nr_pipeline == "ranked_hybrid" else None
+            hits = self.store.hybrid_search(query, 40 if ranker else r.top_k)
+            if ranker and hits:
+                docs = ranker.compress_documents([d for d, _ in hits], query)
+                return [(d, d.metadata.get("relevance_score", 0.0)) for d in docs]
+            return hits
         return self.store.similarity_search_with_relevance_scores(query, r.top_k, r.score_threshold)
 
     def rag_chain(self, query: str, chat_history: List[Dict[str, str]], **kwargs) -> Generator[str, None, None]:

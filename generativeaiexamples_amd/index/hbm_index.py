@@ -147,6 +147,10 @@ class HBMIndex:
         return self.delete(lambda d: d.metadata.get("filename") == filename or
                            os.path.basename(str(d.metadata.get("source", ""))) == filename)
 
+    def live_rows(self) -> List[int]:
+        """Rows holding a stored document (not deleted)."""
+        return [i for i, d in enumerate(self.docs[: self.n]) if d is not None]
+
     def compact(self):
         with self.lock:
             keep = torch.nonzero(torch.isfinite(self.bias[: self.n])).flatten().tolist()
