@@ -117,3 +117,76 @@ def fault_worker(rank, world, port, out_dir, mode):
         dist.destroy_process_group()
     else:
         os._exit(0)  # the peer is gone: skip teardown of the broken group
+
+
+def lora_tp_worker(rank, world, port, out_dir):
+    """TP=2 differentiable forward + LoRA grads vs the single-process values of the same weights."""
+    ctx = _init(rank, world, port, 2)
+    from generativeaiexamples_amd.models.llama import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd.training.forward import lm_loss
+    from generativeaiexamples_amd.training.lora import LoRAAdapter, LoRAConfig
+
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny(num_layers=2)
+    full = LlamaModel(cfg, device="cpu", dist_ctx=DistContext()).random_init(seed=3)
+    for t in full.w.values():
+        t.data = t.data.float()
+    sd = full.export_hf_state()
+    tp = LlamaModel(cfg, device="cpu", dist_ctx=ctx, dtype=torch.float32).load_hf_state(sd)
+    lcfg = LoRAConfig(r=4, alpha=8, targets=("qkv", "o", "gate_up", "down"))
+    ad_full = LoRAAdapter(full, lcfg, seed=1)
+    ad_tp = LoRAAdapter(tp, lcfg, seed=1)
+    with torch.no_grad():  # non-zero B so the LoRA path matters; shard full adapters the way weights are
+        for j, (k, v) in enumerate(ad_full.params.items()):
+            if k.endswith(".B"):  # deterministic across processes (str hash is randomised per process)
+                v.normal_(0, 0.05, generator=torch.Generator().manual_seed(j))
+        for k, v in ad_tp.params.items():
+            src = ad_full.params[k]
+            t = k.split(".")[1]
+            if src.shape == v.shape:
+                v.copy_(src)
+            elif t in ("qkv", "gate_up"):  # column-parallel: B rows sharded like the weight rows
+                if t == "qkv":
+                    hd, H, Hkv = cfg.head_dim, cfg.num_heads, cfg.num_kv_heads
+                    q, kk, vv = src.split([H * hd, Hkv * hd, Hkv * hd])
+                    parts = [x.chunk(world)[rank] for x in (q, kk, vv)]
+                    v.copy_(torch.cat(parts))
+                else:
+                    v.copy_(src.view(world, -1, src.shape[1])[rank])
+            else:  # row-parallel A: columns sharded
+                v.copy_(src.view(src.shape[0], world, -1)[:, rank])
+    ids = torch.randint(3, cfg.vocab_size, (2, 24), generator=torch.Generator().manual_seed(5))
+    labels = ids.clone()
+    labels[:, :8] = -100
+    l_full = lm_loss(full, ad_full, ids, labels)
+    l_full.backward()
+    l_tp = lm_loss(tp, ad_tp, ids, labels)
+    l_tp.backward()
+    for p in ad_tp.tp_replicated():
+        dist.all_reduce(p.grad, group=ctx.tp_group)
+    # compare the gradient of one replicated and one sharded factor
+    g_rep = ad_tp.params["l1.o.B"].grad
+    g_rep_ref = ad_full.params["l1.o.B"].grad
+    torch.save({"loss": l_tp.detach(), "loss_ref": l_full.detach(), "g": g_rep, "g_ref": g_rep_ref,
+                "gA": ad_tp.params["l0.qkv.A"].grad, "gA_ref": ad_full.params["l0.qkv.A"].grad},
+               os.path.join(out_dir, f"lora_tp_{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def lora_dp_worker(rank, world, port, out_dir):
+    """DP=2 LoRA SFT with the overlapped gradient bucketer: replicas stay identical, loss falls."""
+    ctx = _init(rank, world, port, 1)
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.llama import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.training.lora import LoRAConfig
+    from generativeaiexamples_amd.training.trainer import LoRATrainer, TrainConfig
+
+    cfg = LlamaConfig.tiny(num_layers=2)
+    m = LlamaModel(cfg, device="cpu", dist_ctx=ctx, dtype=torch.float32).random_init(seed=3)
+    tr = LoRATrainer(m, small_byte_tokenizer(cfg.vocab_size), LoRAConfig(r=4, alpha=8),
+                     TrainConfig(steps=12, global_batch=4, micro_batch=1, seq_len=64, lr=3e-3, warmup=2))
+    hist = tr.train()
+    torch.save({"hist": torch.tensor(hist), "A": tr.lora.params["l0.qkv.A"].detach().clone(),
+                "launched": tr.bucketer.launched}, os.path.join(out_dir, f"lora_dp_{rank}.pt"))
+    dist.destroy_process_group()
