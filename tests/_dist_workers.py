@@ -171,7 +171,8 @@ def lora_tp_worker(rank, world, port, out_dir):
     torch.save({"loss": l_tp.detach(), "loss_ref": l_full.detach(), "g": g_rep, "g_ref": g_rep_ref,
                 "gA": ad_tp.params["l0.qkv.A"].grad, "gA_ref": ad_full.params["l0.qkv.A"].grad},
                os.path.join(out_dir, f"lora_tp_{rank}.pt"))
-    dist.destroy_process_group()
+    dist.barrier()
+    os._exit(0)  # skip gloo teardown (sporadic abort after autograd-issued collectives); results are saved
 
 
 def lora_dp_worker(rank, world, port, out_dir):
@@ -189,4 +190,5 @@ def lora_dp_worker(rank, world, port, out_dir):
     hist = tr.train()
     torch.save({"hist": torch.tensor(hist), "A": tr.lora.params["l0.qkv.A"].detach().clone(),
                 "launched": tr.bucketer.launched}, os.path.join(out_dir, f"lora_dp_{rank}.pt"))
-    dist.destroy_process_group()
+    dist.barrier()
+    os._exit(0)
