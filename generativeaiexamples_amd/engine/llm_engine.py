@@ -68,6 +68,7 @@ class Request:
     finish_reason: Optional[str] = None
     seed: int = 0
     token_counts: Dict[int, int] = field(default_factory=dict)
+    lora_slot: int = 0
 
     @property
     def text(self) -> str:
@@ -139,8 +140,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_ids: List[int], params: SamplingParams | None = None,
-                    request_id: Optional[str] = None, images: Optional[list] = None) -> Request:
-        """images: inputs for a multimodal model (encoded once here by ``model.register_request``)."""
+                    request_id: Optional[str] = None, images: Optional[list] = None,
+                    lora: Optional[str] = None) -> Request:
+        """images: inputs for a multimodal model (encoded once here by ``model.register_request``);
+        lora: name of an adapter registered with ``model.add_lora`` (multi-LoRA serving)."""
         params = params or SamplingParams()
         with self.lock:
             sid = next(self._ids)
@@ -152,6 +155,8 @@ class LLMEngine:
                 max_new = 1
             req = Request(rid, list(prompt_ids), params, sid, IncrementalDetokenizer(self.tok, params.stop),
                           seed=params.seed if params.seed is not None else (sid * 7919) & 0x7FFFFFFF)
+            if lora:
+                req.lora_slot = self.model.lora_slot(lora)
             self.requests[sid] = req
             self.by_rid[rid] = req
             if images:
@@ -175,6 +180,14 @@ class LLMEngine:
             self._release(req.seq_id)
             req.finished, req.finish_reason = True, "abort"
             return True
+
+    def add_lora(self, name: str, adapter) -> int:
+        """Register a LoRA adapter (object or directory) for per-request selection. Captured decode graphs
+        are dropped and re-captured lazily so they include the new adapter's deltas."""
+        with self.lock:
+            slot = self.model.add_lora(name, adapter)
+            self.graphs.clear()
+            return slot
 
     def _release(self, sid: int):
         if hasattr(self.model, "release_request"):
@@ -218,11 +231,19 @@ class LLMEngine:
             fb.max_decode_ctx = int(b.decode_ctx.max())
         fb.sample_rows = dev[8].long()
         fb.seq_ids = list(b.prefill_seq_ids) + list(b.decode_seq_ids)
+        if getattr(self.model, "lora_names", None):
+            per_seq = [self._slot(s) for s in fb.seq_ids]
+            qlen = list(b.prefill_qlen) + [1] * len(b.decode_seq_ids)
+            fb.lora_slots = self._to_device([np.repeat(np.asarray(per_seq, np.int32), qlen)])[0]
         if hasattr(self.model, "prepare_batch"):
             self.model.prepare_batch(fb)
         return fb, seq_order
 
     # ------------------------------------------------------------------ HIP graphs (decode)
+    def _slot(self, sid: int) -> int:
+        r = self.requests.get(sid)
+        return r.lora_slot if r is not None else 0
+
     def _graph_bucket(self, n: int) -> Optional[int]:
         for s in self.cfg.graph_batch_sizes:
             if s >= n:
@@ -241,6 +262,8 @@ class LLMEngine:
                           decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
         if hasattr(self.model, "graph_static_inputs"):
             fb.extra = self.model.graph_static_inputs(bs)
+        if getattr(self.model, "lora_names", None):
+            fb.lora_slots = torch.zeros(bs, dtype=torch.int32, device=d)
         s = torch.cuda.Stream(device=d)
         s.wait_stream(torch.cuda.current_stream(d))
         with torch.cuda.stream(s):
@@ -278,6 +301,9 @@ class LLMEngine:
             fb.decode_block_tables[n:, 0].fill_(self.pad_block)
         if fb.extra is not None:
             self.model.fill_graph_inputs(fb.extra, list(b.decode_seq_ids), n)
+        if fb.lora_slots is not None:
+            fb.lora_slots.zero_()
+            fb.lora_slots[:n].copy_(self._to_device([np.asarray([self._slot(s) for s in b.decode_seq_ids], np.int32)])[0])
         g.replay()
         self.stats["graph_steps"] += 1
         return logits[:n]

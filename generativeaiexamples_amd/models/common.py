@@ -34,6 +34,7 @@ class ForwardBatch:
     # per-step inputs built by the model's prepare_batch hook (e.g. cross-attention tables)
     seq_ids: Optional[list] = None
     extra: Optional[dict] = None
+    lora_slots: Optional[torch.Tensor] = None  # [T] int32 adapter slot per token (multi-LoRA), None = none
 
     @property
     def num_tokens(self) -> int:

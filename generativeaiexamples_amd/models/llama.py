@@ -106,6 +106,8 @@ class LlamaModel:
         self.vstart = self.ctx.tp_rank * self.vocab_local
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.w: Dict[str, torch.Tensor] = {}
+        self.lora_names: list = []          # slot s (1-based) -> adapter name; slot 0 = base model
+        self.lora_w: Dict[tuple, tuple] = {}  # (slot, layer, target) -> (A [r, in] bf16, B [out, r] bf16, scale)
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling,
                                         device=self.device)
         self._alloc()
@@ -230,6 +232,51 @@ class LlamaModel:
                 n += t.numel()
         return n
 
+    # ------------------------------------------------------------------ multi-LoRA serving
+    def add_lora(self, name: str, adapter) -> int:
+        """Register a trained :class:`~..training.lora.LoRAAdapter` (or a path to one) under ``name``;
+        requests select it per sequence (``lora`` argument / the OpenAI ``model`` field). Adapters are
+        applied unmerged: y += mask_slot * ((x A^T) B^T) * scale for every adapted projection, so
+        requests for different adapters (and the base model) share one batch and one HIP graph."""
+        if isinstance(adapter, str):
+            from ..training.lora import LoRAAdapter
+            adapter = LoRAAdapter.load(adapter, self, device=self.device)
+        if name in self.lora_names:
+            slot = self.lora_names.index(name) + 1
+        else:
+            self.lora_names.append(name)
+            slot = len(self.lora_names)
+        for key, a in adapter.params.items():
+            if not key.endswith(".A"):
+                continue
+            base = key[:-2]
+            li, t = base.split(".", 1)
+            b = adapter.params[base + ".B"]
+            self.lora_w[(slot, int(li[1:]), t)] = (a.detach().to(self.device, self.dtype).contiguous(),
+                                                   b.detach().to(self.device, self.dtype).contiguous(),
+                                                   float(adapter.cfg.scale))
+        return slot
+
+    def lora_slot(self, name: Optional[str]) -> int:
+        if not name:
+            return 0
+        if name not in self.lora_names:
+            raise KeyError(f"unknown LoRA adapter '{name}'")
+        return self.lora_names.index(name) + 1
+
+    def _lora(self, y: torch.Tensor, x: torch.Tensor, layer: int, target: str, fb: ForwardBatch) -> torch.Tensor:
+        slots = getattr(fb, "lora_slots", None)
+        if not self.lora_names or slots is None:
+            return y
+        for s in range(1, len(self.lora_names) + 1):
+            ab = self.lora_w.get((s, layer, target))
+            if ab is None:
+                continue
+            a, b, scale = ab
+            m = (slots == s).to(x.dtype)[:, None]
+            y += ((x * m) @ a.t() @ b.t()) * scale
+        return y
+
     # ------------------------------------------------------------------ forward
     def kv_shape(self, num_blocks: int):
         return (num_blocks, self.hkv, ops.BLOCK, self.cfg.head_dim), (num_blocks, self.hkv, self.cfg.head_dim, ops.BLOCK)
@@ -250,7 +297,7 @@ class LlamaModel:
             p = f"l{i}."
             x = ops.rms_norm(res, w[p + "attn_norm"], c.rms_eps) if h is None else \
                 ops.rms_norm(h, w[p + "attn_norm"], c.rms_eps, residual=res)
-            qkv = ops.linear(x, w[p + "qkv"])
+            qkv = self._lora(ops.linear(x, w[p + "qkv"]), x, i, "qkv", fb)
             kc, vc = kv.layer(i)
             ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True)
             if P > 0:
@@ -259,7 +306,7 @@ class LlamaModel:
             if T > P:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
                                      max_ctx=fb.max_decode_ctx, out=attn[P:])
-            h = ops.linear(attn.view(T, -1), w[p + "o"])
+            h = self._lora(ops.linear(attn.view(T, -1), w[p + "o"]), attn.view(T, -1), i, "o", fb)
             ctx.tp_all_reduce(h)
             x = ops.rms_norm(h, w[p + "mlp_norm"], c.rms_eps, residual=res)
             g = ops.linear(x, w[p + "gate_up"], act="swiglu")

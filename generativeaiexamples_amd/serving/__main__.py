@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--served-model-name", default=None)
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=8192)
-    ap.add_argument("--lora", action="append", default=[], help="adapter name served as an alias of the base model")
+    ap.add_argument("--lora", action="append", default=[],
+                    help="NAME=DIR serves a trained LoRA adapter (unmerged, per request); NAME alone aliases the base model")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None)
     a = ap.parse_args()
@@ -40,7 +41,7 @@ def main():
     spec = HubSpec(llm=a.llm or None, llm_weights=a.llm_weights, embedder=a.embedder or None,
                    embedder_weights=a.embedder_weights, reranker=a.reranker, reranker_weights=a.reranker_weights,
                    served_llm_name=a.served_model_name, max_num_seqs=a.max_num_seqs, max_model_len=a.max_model_len,
-                   use_graphs=not a.no_graphs, lora_adapters={n: "" for n in a.lora}, device=a.device)
+                   use_graphs=not a.no_graphs, lora_adapters=dict((x.split("=", 1) + [""])[:2] for x in a.lora), device=a.device)
     hub = ServiceHub.build(spec)
     uvicorn.run(create_openai_app(hub), host=a.host, port=a.port, log_level="info")
 

@@ -49,6 +49,7 @@ class AsyncLLMEngine:
         self.error: Optional[BaseException] = None
         self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("GAI_WATCHDOG_S", "300"))
         self._step_started: Optional[float] = None
+        self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
         self.thread.start()
         self.watchdog = threading.Thread(target=self._watch, daemon=True, name="llm-watchdog")
@@ -61,8 +62,7 @@ class AsyncLLMEngine:
 
     def _watch(self):
         period = max(0.05, min(1.0, self.watchdog_s / 4))
-        while self.running:
-            time.sleep(period)
+        while not self._stop.wait(period):
             t = self._step_started
             if t is not None and self.healthy and time.perf_counter() - t > self.watchdog_s:
                 err = TimeoutError(f"engine step exceeded the {self.watchdog_s:.1f}s watchdog")
@@ -103,7 +103,8 @@ class AsyncLLMEngine:
                     self.queues.pop(o.request_id, None)
 
     async def generate(self, prompt_ids: List[int], params: SamplingParams,
-                       request_id: Optional[str] = None, images: Optional[list] = None) -> AsyncIterator[StreamItem]:
+                       request_id: Optional[str] = None, images: Optional[list] = None,
+                       lora: Optional[str] = None) -> AsyncIterator[StreamItem]:
         rid = request_id or f"cmpl-{uuid.uuid4().hex}"
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
@@ -111,7 +112,7 @@ class AsyncLLMEngine:
         t0 = time.perf_counter()
         first = True
         with self.cv:
-            req = self.engine.add_request(prompt_ids, params, rid, images=images)
+            req = self.engine.add_request(prompt_ids, params, rid, images=images, lora=lora)
             self.cv.notify()
         METRICS.requests_total.inc()
         METRICS.prompt_tokens.inc(len(prompt_ids))
@@ -181,9 +182,9 @@ class AsyncLLMEngine:
                     self.engine.abort(rid)
 
     async def complete(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None,
-                       images: Optional[list] = None):
+                       images: Optional[list] = None, lora: Optional[str] = None):
         text, ids, reason = [], [], None
-        async for it in self.generate(prompt_ids, params, request_id, images):
+        async for it in self.generate(prompt_ids, params, request_id, images, lora):
             text.append(it.delta)
             if it.token_id >= 0:
                 ids.append(it.token_id)
@@ -192,6 +193,8 @@ class AsyncLLMEngine:
 
     def shutdown(self):
         self.running = False
+        self._stop.set()
         with self.cv:
             self.cv.notify_all()
-        self.thread.join(timeout=5)
+        self.thread.join(timeout=30)
+        self.watchdog.join(timeout=5)

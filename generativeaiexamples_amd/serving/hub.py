@@ -61,6 +61,7 @@ class ServiceHub:
         self.llms: Dict[str, AsyncLLMEngine] = {}
         self.embedders: Dict[str, Embedder] = {}
         self.rerankers: Dict[str, Reranker] = {}
+        self.loras: Dict[str, str] = {}
         self.aliases: Dict[str, str] = {}
         self.default_llm_name: Optional[str] = None
         self.default_embedder_name: Optional[str] = None
@@ -83,6 +84,10 @@ class ServiceHub:
 
     def add_alias(self, alias: str, base: str):
         self.aliases[alias] = base
+
+    def lora_for(self, name: Optional[str]) -> Optional[str]:
+        """Adapter to apply when a request names ``name`` (None for base-model names)."""
+        return self.loras.get(name) if name else None
 
     # ---------------------------------------------------------------- lookup
     def _pick(self, table: dict, name: Optional[str], default: Optional[str]):
@@ -143,8 +148,11 @@ class ServiceHub:
                                                  use_graphs=spec.use_graphs and dev.type == "cuda",
                                                  kv_memory_fraction=spec.kv_memory_fraction))
             hub.add_llm(spec.served_llm_name or name, eng)
-            for alias in spec.lora_adapters:
+            for alias, path in spec.lora_adapters.items():
                 hub.add_alias(alias, spec.served_llm_name or name)
+                if path:  # a trained adapter directory: served unmerged, selected by model name
+                    eng.add_lora(alias, path)
+                    hub.loras[alias] = alias
         if spec.embedder:
             emb, name = build_embedder_service(spec.embedder, spec.embedder_weights, device=dev)
             hub.add_embedder(spec.served_embedder_name or name, emb)

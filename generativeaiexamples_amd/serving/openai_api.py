@@ -270,6 +270,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
         ids = apply_chat_template(_messages_for_template(req), tok)
         params = _params(req, hub.default_max_tokens)
         images = _images_of(req) or None
+        lora = hub.lora_for(req.model)
         if images and not hasattr(llm.engine.model, "register_request"):
             return _err(400, f"model '{req.model or hub.default_llm_name}' does not accept image inputs")
         rid = f"chatcmpl-{uuid.uuid4().hex}"
@@ -286,7 +287,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
                 yield f"data: {json.dumps(head)}\n\n"
                 n = 0
                 try:
-                    async for it in llm.generate(ids, params, rid, images):
+                    async for it in llm.generate(ids, params, rid, images, lora):
                         n += it.token_id >= 0
                         ch = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
                               "choices": [{"index": 0, "delta": {"content": it.delta} if it.delta else {},
@@ -304,7 +305,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
 
             return StreamingResponse(gen(), media_type="text/event-stream")
 
-        text, out_ids, reason = await llm.complete(ids, params, rid, images)
+        text, out_ids, reason = await llm.complete(ids, params, rid, images, lora)
         msg: Dict[str, Any] = {"role": "assistant", "content": text}
         if use_tools:
             calls = parse_tool_calls(text, req.tools)

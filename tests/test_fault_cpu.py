@@ -55,7 +55,7 @@ def test_watchdog_fails_hung_step():
         def __init__(self):
             self.work = False
 
-        def add_request(self, ids, params, rid, images=None):
+        def add_request(self, ids, params, rid, images=None, lora=None):
             self.work = True
             return Req()
 
@@ -81,4 +81,4 @@ def test_watchdog_fails_hung_step():
     asyncio.run(go())
     assert time.perf_counter() - t0 < 2.5  # failed by the watchdog, not after the 3 s step
     assert not eng.healthy
-    eng.running = False
+    eng.shutdown()
