@@ -21,7 +21,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import ops
-from .common import randn_like_
+from .common import PackedAttention, randn_like_
 
 
 @dataclass
@@ -43,6 +43,12 @@ class BertConfig:
     def head_dim(self) -> int:
         return self.hidden_size // self.num_heads
 
+    @property
+    def head_dim_padded(self) -> int:
+        """Attention kernels run D = 64 / 128: smaller heads (MiniLM: 32) are zero-padded inside the
+        QKV / O weights (padded q/k dims add 0 to the scores, padded v dims feed zero O columns)."""
+        return 64 if self.head_dim <= 64 else 128
+
     @staticmethod
     def e5_large_v2(**kw):
         return BertConfig(name="intfloat/e5-large-v2", **kw)
@@ -51,6 +57,12 @@ class BertConfig:
     def e5_base_v2(**kw):
         return BertConfig(name="intfloat/e5-base-v2", hidden_size=768, intermediate_size=3072, num_layers=12,
                           num_heads=12, **kw)
+
+    @staticmethod
+    def minilm_l6_v2(**kw):
+        # sentence-transformers/all-MiniLM-L6-v2: the reference's Triton streaming-ingest embedder (S8)
+        return BertConfig(name="sentence-transformers/all-MiniLM-L6-v2", hidden_size=384, intermediate_size=1536,
+                          num_layers=6, num_heads=12, **kw)
 
     @staticmethod
     def bge_reranker_large(**kw):
@@ -93,8 +105,9 @@ class BertModel:
         self.w["emb_ln_w"], self.w["emb_ln_b"] = e(D), e(D)
         for i in range(c.num_layers):
             p = f"l{i}."
-            self.w[p + "qkv"], self.w[p + "qkv_b"] = e(3 * D, D), e(3 * D)
-            self.w[p + "o"], self.w[p + "o_b"] = e(D, D), e(D)
+            HP = c.num_heads * c.head_dim_padded
+            self.w[p + "qkv"], self.w[p + "qkv_b"] = e(3 * HP, D), e(3 * HP)
+            self.w[p + "o"], self.w[p + "o_b"] = e(D, HP), e(D)
             self.w[p + "ln1_w"], self.w[p + "ln1_b"] = e(D), e(D)
             self.w[p + "up"], self.w[p + "up_b"] = e(c.intermediate_size, D), e(c.intermediate_size)
             self.w[p + "down"], self.w[p + "down_b"] = e(D, c.intermediate_size), e(D)
@@ -103,6 +116,22 @@ class BertModel:
             # classifier padded to 16 rows so the MFMA GEMM path applies; only num_labels are used
             self.w["cls_dense"], self.w["cls_dense_b"] = e(D, D), e(D)
             self.w["cls_out"], self.w["cls_out_b"] = e(16, D), e(16)
+
+    def _pad_heads(self, t: torch.Tensor, rows: bool) -> torch.Tensor:
+        """[3*H*hd, D] / [3*H*hd] (rows=True) or [D, H*hd] (rows=False) -> zero-padded head dims."""
+        c = self.cfg
+        hd, hp, H = c.head_dim, c.head_dim_padded, c.num_heads
+        if hp == hd:
+            return t
+        if rows:
+            src = t.reshape(3, H, hd, *t.shape[1:])
+            out = t.new_zeros(3, H, hp, *t.shape[1:])
+            out[:, :, :hd] = src
+            return out.reshape(3 * H * hp, *t.shape[1:])
+        src = t.reshape(t.shape[0], H, hd)
+        out = t.new_zeros(t.shape[0], H, hp)
+        out[:, :, :hd] = src
+        return out.reshape(t.shape[0], H * hp)
 
     def random_init(self, seed: int = 0):
         s = seed * 1000
@@ -116,6 +145,14 @@ class BertModel:
             else:
                 randn_like_(t, s, 1.0 / math.sqrt(t.shape[1]))
             s += 1
+        c = self.cfg
+        if c.head_dim_padded != c.head_dim:
+            hd, H = c.head_dim, c.num_heads
+            for i in range(c.num_layers):
+                p = f"l{i}."
+                self.w[p + "qkv"].view(3, H, -1, c.hidden_size)[:, :, hd:].zero_()
+                self.w[p + "qkv_b"].view(3, H, -1)[:, :, hd:].zero_()
+                self.w[p + "o"].view(c.hidden_size, H, -1)[:, :, hd:].zero_()
         return self
 
     def load_hf_state(self, sd: Dict[str, torch.Tensor]):
@@ -135,9 +172,11 @@ class BertModel:
         put("emb_ln_b", g("embeddings.LayerNorm.bias"))
         for i in range(c.num_layers):
             p, h = f"l{i}.", f"encoder.layer.{i}."
-            put(p + "qkv", torch.cat([g(h + f"attention.self.{n}.weight") for n in ("query", "key", "value")]))
-            put(p + "qkv_b", torch.cat([g(h + f"attention.self.{n}.bias") for n in ("query", "key", "value")]))
-            put(p + "o", g(h + "attention.output.dense.weight"))
+            put(p + "qkv", self._pad_heads(torch.cat([g(h + f"attention.self.{n}.weight")
+                                                     for n in ("query", "key", "value")]), True))
+            put(p + "qkv_b", self._pad_heads(torch.cat([g(h + f"attention.self.{n}.bias")
+                                                       for n in ("query", "key", "value")]), True))
+            put(p + "o", self._pad_heads(g(h + "attention.output.dense.weight"), False))
             put(p + "o_b", g(h + "attention.output.dense.bias"))
             put(p + "ln1_w", g(h + "attention.output.LayerNorm.weight"))
             put(p + "ln1_b", g(h + "attention.output.LayerNorm.bias"))
@@ -160,42 +199,20 @@ class BertModel:
                       type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """ids [T] int32 (varlen packed), cu_seqlens [B+1] int32 (device), seq_lens host list -> hidden [T, D]."""
         c, w = self.cfg, self.w
-        T, D, H, hd = ids.numel(), c.hidden_size, c.num_heads, c.head_dim
+        T, D, H, hp = ids.numel(), c.hidden_size, c.num_heads, c.head_dim_padded
         dev = ids.device
-        # positions restart at 0 for every sequence
-        pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in seq_lens]).to(dev, non_blocking=True)
-        # transient paged cache: sequence b owns blocks [off_b, off_b + ceil(n/16))
-        nbs = [(n + 15) // 16 for n in seq_lens]
-        offs = [0]
-        for n in nbs:
-            offs.append(offs[-1] + n)
-        maxb = max(nbs) if nbs else 1
-        bt = torch.zeros(len(seq_lens), maxb, dtype=torch.int32)
-        slots = torch.empty(T, dtype=torch.int32)
-        t0 = 0
-        for b, n in enumerate(seq_lens):
-            bt[b, : nbs[b]] = torch.arange(offs[b], offs[b] + nbs[b], dtype=torch.int32)
-            slots[t0:t0 + n] = offs[b] * 16 + torch.arange(n, dtype=torch.int32)
-            t0 += n
-        bt, slots = bt.to(dev, non_blocking=True), slots.to(dev, non_blocking=True)
-        ctx = torch.tensor(seq_lens, dtype=torch.int32).to(dev, non_blocking=True)
-        tiles = ops.build_prefill_tiles(seq_lens, H, H, dev) if dev.type == "cuda" else None
-        kc = torch.zeros(offs[-1] + 1, H, ops.BLOCK, hd, device=dev, dtype=self.dtype)
-        vc = torch.zeros(offs[-1] + 1, H, hd, ops.BLOCK, device=dev, dtype=self.dtype)
-
+        attn = PackedAttention(seq_lens, H, hp, dev, self.dtype)
+        pos = attn.positions  # restart at 0 for every sequence
         h = ops.embedding(ids, w["word"])
         h = h + w["pos"][pos.long()]
         h = h + (w["type"][0] if type_ids is None else w["type"][type_ids.long()])
         h = ops.layer_norm(h, w["emb_ln_w"], w["emb_ln_b"], c.ln_eps)
-        q = torch.empty(T, H, hd, device=dev, dtype=self.dtype)
-        attn = torch.empty_like(q)
+        out = torch.empty(T, H * hp, device=dev, dtype=self.dtype)
         for i in range(c.num_layers):
             p = f"l{i}."
             qkv = ops.linear(h, w[p + "qkv"], bias=w[p + "qkv_b"])
-            ops.rope_kv_write(qkv, pos, _dummy_cs(dev, hd), slots, q, kc, vc, H, H, hd, rope=False)
-            ops.attention_prefill(q, kc, vc, bt, cu_seqlens, ctx, self.scale, causal=False, tiles=tiles,
-                                  q_lens=seq_lens, out=attn)
-            x = ops.linear(attn.view(T, D), w[p + "o"], bias=w[p + "o_b"], residual=h)
+            a = attn(qkv, self.scale, out=out)
+            x = ops.linear(a, w[p + "o"], bias=w[p + "o_b"], residual=h)
             h = ops.layer_norm(x, w[p + "ln1_w"], w[p + "ln1_b"], c.ln_eps)
             f = ops.linear(h, w[p + "up"], bias=w[p + "up_b"], act="gelu")
             x = ops.linear(f, w[p + "down"], bias=w[p + "down_b"], residual=h)
@@ -217,14 +234,3 @@ class BertModel:
         x = torch.tanh(x.float()).to(self.dtype)
         logits = ops.linear(x, w["cls_out"], bias=w["cls_out_b"], out_dtype=torch.float32)
         return logits[:, 0]
-
-
-_CS_CACHE: dict = {}
-
-
-def _dummy_cs(dev, hd):
-    """RoPE table placeholder for rope=False launches (never read)."""
-    key = (str(dev), hd)
-    if key not in _CS_CACHE:
-        _CS_CACHE[key] = torch.zeros(1, hd, dtype=torch.float32, device=dev)
-    return _CS_CACHE[key]

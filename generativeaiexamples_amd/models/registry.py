@@ -34,6 +34,7 @@ ENCODER_PRESETS = {
     "e5-large-v2": ("nvidia/nv-embedqa-e5-v5", lambda: BertConfig.e5_large_v2()),
     "e5-base-v2": ("intfloat/e5-base-v2", lambda: BertConfig.e5_base_v2()),
     "tiny-e5": ("tiny-e5", lambda: BertConfig.tiny()),
+    "all-minilm-l6-v2": ("sentence-transformers/all-MiniLM-L6-v2", lambda: BertConfig.minilm_l6_v2()),
     "nvclip": ("nvidia/nvclip", lambda: ClipConfig.vit_l_14()),
     "tiny-clip": ("tiny-clip", lambda: ClipConfig.tiny()),
 }
