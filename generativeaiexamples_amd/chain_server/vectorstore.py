@@ -46,17 +46,24 @@ class VectorStore:
             live = self.index.live_rows()
             self.bm25.add(live, [self.index.document(r).page_content for r in live])
 
+    def add_embedded(self, vecs, docs: List[Document]) -> List[int]:
+        """Insert already-embedded chunks (the streaming-ingest write stage)."""
+        with self.lock:
+            if self.index.dim != vecs.shape[1] and len(self.index) == 0:
+                self.index = HBMIndex(vecs.shape[1], self.index.metric, device=self.index.device, name=self.name)
+                if self.persist:
+                    self.index.attach_wal(self.persist)
+            rows = self.index.add(vecs, docs)
+            if self.bm25 is not None:
+                self.bm25.add(rows, [d.page_content for d in docs])
+            return rows
+
     def add_documents(self, docs: List[Document]) -> List[int]:
         rows: List[int] = []
         for i in range(0, len(docs), self.batch):
             part = docs[i:i + self.batch]
             vecs = self.emb.embed_tensor([d.page_content for d in part], "passage")
-            if self.index.dim != vecs.shape[1] and len(self.index) == 0:
-                self.index = HBMIndex(vecs.shape[1], self.index.metric, device=self.index.device, name=self.name)
-            new_rows = self.index.add(vecs, part)
-            rows += new_rows
-            if self.bm25 is not None:
-                self.bm25.add(new_rows, [d.page_content for d in part])
+            rows += self.add_embedded(vecs, part)
         if self.persist:
             self.index.save(self.persist)
         return rows
