@@ -1,0 +1,61 @@
+"""Bash tool-calling agent loop (W11/W12), PandasAI adapter (C8), API client script (C9)."""
+import json
+import os
+import subprocess
+import sys
+
+from generativeaiexamples_amd.examples.agents.bash_agent import BashTool, run_agent, system_prompt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bash_tool_allowlist_and_jail(tmp_path):
+    (tmp_path / "a.txt").write_text("x")
+    (tmp_path / "b.txt").write_text("y")
+    t = BashTool(str(tmp_path))
+    assert "a.txt" in t("ls")
+    assert t("rm a.txt").startswith("error") and (tmp_path / "a.txt").exists()
+    assert t("ls | wc -l").startswith("error")
+    assert t("cat a.txt; rm b.txt").startswith("error") and (tmp_path / "b.txt").exists()
+    assert BashTool(str(tmp_path), confirm=lambda c: False)("ls").startswith("error: the user declined")
+
+
+def test_agent_loop_executes_tool_calls(tmp_path):
+    for i in range(3):
+        (tmp_path / f"f{i}.txt").write_text("z")
+    script = [{"content": None, "tool_calls": [{"id": "c1", "type": "function",
+                                                "function": {"name": "exec_bash_command", "arguments": json.dumps({"cmd": "ls"})}}]},
+              {"content": "There are 3 text files."}]
+    seen = []
+
+    def chat(messages, tools):
+        seen.append([dict(m) for m in messages])
+        return script[len(seen) - 1]
+    ans = run_agent("how many txt files?", chat, BashTool(str(tmp_path)), thinking="off")
+    assert ans == "There are 3 text files."
+    tool_msg = seen[1][-1]
+    assert tool_msg["role"] == "tool" and "f2.txt" in tool_msg["content"]
+    assert seen[0][0]["content"].startswith("detailed thinking off")
+    assert system_prompt("/x", None).startswith("You are")
+
+
+def test_pandasai_adapter_routes_to_llm():
+    from generativeaiexamples_amd.integrations.pandasai_llm import MI355XPandasLLM
+
+    class FakeLLM:
+        def invoke(self, msgs):
+            return "df.shape[0]"
+
+    class Prompt:
+        def to_string(self):
+            return "Write pandas code counting rows"
+
+    llm = MI355XPandasLLM(model="m", llm=FakeLLM())
+    assert llm.call(Prompt()) == "df.shape[0]" and llm.last_prompt == "Write pandas code counting rows"
+    assert llm.type == "mi355x-llm" and llm._default_params["model"] == "m"
+
+
+def test_api_client_script_help():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "RAG/src/chain_server/api_client.py"), "--help"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "--docs" in r.stdout
