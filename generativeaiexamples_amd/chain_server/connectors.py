@@ -30,6 +30,9 @@ def _base(url: str) -> str:
 
 
 # ------------------------------------------------------------------------------------------ LLM
+from . import tracing  # noqa: E402
+
+
 class ChatLLM:
     model: str = ""
 
@@ -40,6 +43,12 @@ class ChatLLM:
 
     def stream(self, messages: List[Dict[str, Any]], **override) -> Iterator[str]:
         raise NotImplementedError
+
+    def traced_stream(self, messages: List[Dict[str, Any]], **override) -> Iterator[str]:
+        """stream() inside an 'llm' span with model, prompt size and first_token_time_ms (TTFT)."""
+        n_prompt = sum(len(str(m.get("content") or "")) for m in messages)
+        return tracing.traced_stream("llm.stream", self.stream(messages, **override),
+                                     **{"llm.model": getattr(self, "model", ""), "llm.prompt_chars": n_prompt})
 
     def invoke(self, messages: List[Dict[str, Any]], **override) -> str:
         return "".join(self.stream(messages, **override))
@@ -159,6 +168,7 @@ class Ranker:
     def rank(self, query: str, passages: List[str]) -> List[tuple]:
         raise NotImplementedError
 
+    @tracing.traced("reranker")
     def compress_documents(self, documents: Sequence[Document], query: str) -> List[Document]:
         """Reorders documents by relevance, keeps top_n, stores ``relevance_score`` in metadata."""
         docs = list(documents)

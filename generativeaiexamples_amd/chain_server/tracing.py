@@ -140,8 +140,25 @@ def span(name: str, headers=None, **attrs) -> Iterator[Optional[Span]]:
         yield s
     finally:
         s.end = time.time_ns()
+        _process_metrics(s)
         _current.reset(tok)
         EXPORTER.export(s)
+
+
+_PROC = None
+
+
+def _process_metrics(s: "Span"):
+    """psutil process metrics at span end (the reference's LangChain callback records them, T5)."""
+    global _PROC
+    try:
+        import psutil
+        _PROC = _PROC or psutil.Process()
+        s.set_attribute("process.memory.rss_bytes", int(_PROC.memory_info().rss))
+        s.set_attribute("process.cpu.percent", float(_PROC.cpu_percent(None)))
+        s.set_attribute("process.threads", int(_PROC.num_threads()))
+    except Exception:  # noqa: BLE001 - metrics are best-effort
+        pass
 
 
 def inject(headers: dict) -> dict:
@@ -161,6 +178,28 @@ def instrumentation_wrapper(func):
             return await func(*args, **kwargs)
 
     return wrapper
+
+
+def traced(kind: str):
+    """Decorator for component calls (callback-handler role, T5/T6): one span per call named
+    ``<kind>.<function>`` with the call's scalar kwargs as attributes; result-size attribute when the
+    result is a sized collection (retrieved documents, embeddings)."""
+
+    def deco(func):
+        @functools.wraps(func)
+        def wrapper(*args, **kwargs):
+            if not ENABLED:
+                return func(*args, **kwargs)
+            attrs = {f"{kind}.{k}": v for k, v in kwargs.items() if isinstance(v, (int, float, str, bool))}
+            with span(f"{kind}.{func.__name__}", **attrs) as sp:
+                out = func(*args, **kwargs)
+                if sp is not None and hasattr(out, "__len__"):
+                    sp.set_attribute(f"{kind}.result_count", len(out))
+                    if kind == "retriever" and out and isinstance(out[0], tuple):
+                        sp.set_attribute("retriever.scores", [float(x[1]) for x in out][:16])
+                return out
+        return wrapper
+    return deco
 
 
 def traced_stream(name: str, it: Iterator[str], **attrs) -> Iterator[str]:

@@ -13,6 +13,7 @@ from typing import Dict, List, Optional, Tuple
 from ..index.bm25 import BM25Index, rrf
 from ..index.hbm_index import Document, HBMIndex
 from ..utils.metrics import METRICS
+from . import tracing
 from .connectors import Embeddings
 
 log = logging.getLogger(__name__)
@@ -71,6 +72,7 @@ class VectorStore:
     add_texts = lambda self, texts, metadatas=None: self.add_documents(  # noqa: E731
         [Document(t, (metadatas or [{}] * len(texts))[i]) for i, t in enumerate(texts)])
 
+    @tracing.traced("retriever")
     def similarity_search_with_relevance_scores(self, query: str, k: int = 4,
                                                 score_threshold: Optional[float] = None) -> List[Tuple[Document, float]]:
         import time
@@ -81,6 +83,7 @@ class VectorStore:
         METRICS.search.observe(time.perf_counter() - t0)
         return [(h.document, h.score) for h in hits]
 
+    @tracing.traced("retriever")
     def hybrid_search(self, query: str, k: int = 4, candidates: int = 40) -> List[Tuple[Document, float]]:
         """Dense (HBM cosine top-``candidates``) + sparse (BM25 top-``candidates``) fused by reciprocal rank."""
         import time

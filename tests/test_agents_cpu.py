@@ -59,3 +59,30 @@ def test_api_client_script_help():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "RAG/src/chain_server/api_client.py"), "--help"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "--docs" in r.stdout
+
+
+def test_faiss_compat_roundtrip(tmp_path):
+    """Notebook-style FAISS usage with a LangChain-style embeddings object (embed_documents/embed_query)."""
+    import hashlib
+
+    from generativeaiexamples_amd.integrations.faiss_compat import FAISS
+
+    class LCEmb:
+        def _v(self, t):
+            h = hashlib.sha256(t.encode()).digest()
+            return [b / 255.0 for b in h[:16]]
+
+        def embed_documents(self, texts):
+            return [self._v(t) for t in texts]
+
+        def embed_query(self, text):
+            return self._v(text)
+
+    texts = [f"fact number {i}" for i in range(20)]
+    db = FAISS.from_texts(texts, LCEmb(), metadatas=[{"i": i} for i in range(20)], device="cpu")
+    top = db.similarity_search("fact number 7", k=1)[0]
+    assert top.page_content == "fact number 7" and top.metadata["i"] == 7  # exact match has distance 0
+    db.save_local(str(tmp_path / "faiss"))
+    db2 = FAISS.load_local(str(tmp_path / "faiss"), LCEmb(), allow_dangerous_deserialization=True, device="cpu")
+    assert db2.similarity_search("fact number 13", k=1)[0].page_content == "fact number 13"
+    assert len(db2.as_retriever(search_kwargs={"k": 3}).invoke("fact number 2")) == 3
