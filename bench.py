@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--embedder", default="e5-large-v2", choices=["e5-large-v2", "e5-base-v2", "tiny"])
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--decode-steps", type=int, default=8,
+                    help="decode tokens per captured multi-step HIP graph run (1 = one host round trip per token)")
     ap.add_argument("--prefix-cache", action="store_true",
                     help="enable KV prefix caching (off by default: random-init embeddings retrieve the same "
                          "chunks for every query, so caching would skip most of the prefill work)")
@@ -148,6 +150,7 @@ def main():
     ecfg = EngineConfig(max_num_seqs=max(args.batch, 1), max_batched_tokens=args.max_batched_tokens,
                         max_model_len=min(lcfg.max_position, prompt_est + args.max_tokens),
                         prefill_chunk=args.max_batched_tokens, use_graphs=not args.no_graphs,
+                        decode_steps=args.decode_steps,
                         prefix_cache=args.prefix_cache,
                         kv_memory_fraction=0.5,
                         kv_memory_bytes=int(args.kv_gb * (1 << 30)) if args.kv_gb else None)

@@ -319,6 +319,24 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   gai_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), D, vstart, vend, cur_stream());
 }
 
+void decode_advance(const Tensor& toks, Tensor& ids, Tensor& pos, Tensor& ctx, Tensor& slots, const Tensor& bt,
+                    const Tensor& n_valid, int64_t block) {
+  check_i32(toks, "toks");
+  check_i32(ids, "token_ids");
+  check_i32(pos, "positions");
+  check_i32(ctx, "ctx_lens");
+  check_i32(slots, "slots");
+  check_i32(bt, "block_tables");
+  check_i32(n_valid, "n_valid");
+  const int B = ids.numel();
+  TORCH_CHECK(toks.numel() >= B && pos.numel() == B && ctx.numel() == B && slots.numel() == B && bt.size(0) == B,
+              "decode_advance: row counts differ");
+  TORCH_CHECK(bt.is_contiguous(), "decode_advance: block table must be contiguous");
+  gai_decode_advance(toks.data_ptr<int>(), ids.data_ptr<int>(), pos.data_ptr<int>(), ctx.data_ptr<int>(),
+                     slots.data_ptr<int>(), bt.data_ptr<int>(), bt.size(1), n_valid.data_ptr<int>(), B, block,
+                     cur_stream());
+}
+
 void pool(const Tensor& h, const Tensor& cu, Tensor& out, int64_t mode, bool normalize) {
   check_bf16(h, "hidden");
   check_i32(cu, "cu_seqlens");
@@ -376,6 +394,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("embedding", &embedding);
+  m.def("decode_advance", &decode_advance);
   m.def("pool", &pool);
   m.def("silu_mul", &silu_mul);
   m.def("gelu", &gelu);

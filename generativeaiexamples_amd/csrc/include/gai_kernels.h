@@ -65,6 +65,8 @@ void gai_pool(const void* h, const int* cu, float* out, int B, int D, int mode, 
 void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_gelu(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t st);
+void gai_decode_advance(const int* toks, int* ids, int* pos, int* ctx, int* slots, const int* bt, int max_blocks,
+                        const int* n_valid, int B, int block, hipStream_t st);
 
 // vision.hip
 void gai_patchify(const float* img, int B, int C, int H, int W, int P, int Kp, const float* mean,

@@ -90,7 +90,33 @@ __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf
   store8(y + (size_t)t * I + u * 8, o);
 }
 
+// Multi-step decode: feed the token sampled at step j back as step j+1's input, inside one HIP
+// graph. Row r < *n_valid: ids <- toks, pos += 1, ctx = pos + 1, slot from the block table
+// (pages for the whole run are reserved by Scheduler.reserve_decode). Padded rows stay frozen
+// on the scratch page.
+__global__ __launch_bounds__(256) void decode_advance_kernel(const int* __restrict__ toks, int* __restrict__ ids,
+                                                             int* __restrict__ pos, int* __restrict__ ctx,
+                                                             int* __restrict__ slots, const int* __restrict__ bt,
+                                                             int max_blocks, const int* __restrict__ n_valid, int B,
+                                                             int block) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= B || r >= *n_valid) return;
+  const int p = pos[r] + 1;
+  ids[r] = toks[r];
+  pos[r] = p;
+  ctx[r] = p + 1;
+  slots[r] = bt[(size_t)r * max_blocks + p / block] * block + p % block;
+}
+
 }  // namespace
+
+void gai_decode_advance(const int* toks, int* ids, int* pos, int* ctx, int* slots, const int* bt, int max_blocks,
+                        const int* n_valid, int B, int block, hipStream_t st) {
+  if (B == 0) return;
+  decode_advance_kernel<<<(B + 255) / 256, 256, 0, st>>>(toks, ids, pos, ctx, slots, bt, max_blocks, n_valid, B,
+                                                         block);
+  GAI_LAUNCH_CHECK();
+}
 
 void gai_embedding(const int* ids, const void* table, void* out, int T, int D, int vstart, int vend, hipStream_t st) {
   if (T == 0) return;

@@ -76,6 +76,16 @@ PYBIND11_MODULE(_rt, m) {
       .def("finish", &Scheduler::finish)
       .def("append_tokens", &Scheduler::append_tokens)
       .def("schedule", &Scheduler::schedule, py::call_guard<py::gil_scoped_release>())
+      .def("reserve_decode",
+           [](Scheduler& s, const std::vector<int64_t>& ids, int steps) -> py::object {
+             std::vector<int32_t> bt;
+             int mb = 0;
+             if (!s.reserve_decode(ids, steps, bt, mb)) return py::none();
+             return arr2(bt, mb);
+           },
+           py::arg("ids"), py::arg("steps"),
+           "reserve KV pages for a multi-step decode run; [len(ids), max_blocks] int32 block tables or None")
+      .def("advance_decode", &Scheduler::advance_decode, py::arg("ids"), py::arg("toks"), py::arg("steps"))
       .def("num_waiting", &Scheduler::num_waiting)
       .def("num_running", &Scheduler::num_running)
       .def("num_free_blocks", &Scheduler::num_free_blocks)

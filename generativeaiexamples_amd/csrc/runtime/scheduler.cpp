@@ -206,4 +206,45 @@ StepBatch Scheduler::schedule() {
   return b;
 }
 
+bool Scheduler::reserve_decode(const std::vector<int64_t>& ids, int steps, std::vector<int32_t>& block_tables,
+                               int& max_blocks) {
+  if (steps < 1) throw std::runtime_error("reserve_decode: steps must be >= 1");
+  int need = 0;
+  for (int64_t id : ids) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) throw std::runtime_error("reserve_decode: unknown sequence");
+    const Sequence& s = *it->second;
+    const int upto = s.num_computed + steps - 1;
+    if (upto > max_model_len_) return false;
+    need += std::max(0, (upto + kBlockSize - 1) / kBlockSize - (int)s.blocks.size());
+  }
+  if (need > 0 && !bm_.can_allocate(need)) return false;
+  max_blocks = 1;
+  for (int64_t id : ids) {
+    Sequence& s = *seqs_[id];
+    ensure_blocks(s, s.num_computed + steps - 1);
+    max_blocks = std::max(max_blocks, (int)s.blocks.size());
+  }
+  block_tables.assign(ids.size() * (size_t)max_blocks, 0);
+  for (size_t i = 0; i < ids.size(); ++i) {
+    const Sequence& s = *seqs_[ids[i]];
+    std::copy(s.blocks.begin(), s.blocks.end(), block_tables.begin() + i * (size_t)max_blocks);
+  }
+  return true;
+}
+
+void Scheduler::advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps) {
+  if (toks.size() != ids.size() * (size_t)steps) throw std::runtime_error("advance_decode: size mismatch");
+  for (size_t i = 0; i < ids.size(); ++i) {
+    auto it = seqs_.find(ids[i]);
+    if (it == seqs_.end()) continue;  // finished / aborted during the run
+    Sequence& s = *it->second;
+    s.tokens.insert(s.tokens.end(), toks.begin() + i * steps, toks.begin() + (i + 1) * steps);
+    s.num_computed += steps - 1;
+    if ((int)s.blocks.size() * kBlockSize < s.num_computed)
+      throw std::runtime_error("advance_decode: sequence advanced past its reserved pages");
+    commit_full_blocks(s);
+  }
+}
+
 }  // namespace gai

@@ -66,6 +66,16 @@ class Scheduler {
 
   StepBatch schedule();
 
+  // Multi-step decode. After schedule() returned a pure-decode batch for `ids`, reserve KV pages so
+  // each of them can run `steps` tokens (positions num_computed-1 .. num_computed+steps-2) with no
+  // further scheduling; fills the [ids.size(), max_blocks] block tables. All-or-nothing: returns
+  // false and allocates nothing when the free pool is short.
+  bool reserve_decode(const std::vector<int64_t>& ids, int steps, std::vector<int32_t>& block_tables,
+                      int& max_blocks);
+  // After such a run: appends `steps` sampled tokens per id (toks is [ids.size(), steps] row-major)
+  // and marks steps-1 more of them as computed (the last sampled token is the next step's input).
+  void advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps);
+
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   int num_free_blocks() const { return bm_.num_free(); }

@@ -11,6 +11,13 @@ One :meth:`LLMEngine.step`:
   4. the gfx950 sampler draws one token per finished-prompt / decode row;
   5. tokens come back to the host, stop conditions (EOS, stop ids, stop strings, max_tokens) are
      applied and text deltas are produced by the incremental detokenizer.
+
+Multi-step decode (``EngineConfig.decode_steps``): once every running sequence is decoding and none
+is waiting, the scheduler reserves KV pages for K tokens per sequence and ONE captured HIP graph runs
+K x (forward -> sample -> ``decode_advance``), feeding each sampled token back as the next input on
+the device. The host syncs once per K tokens instead of once per token, so the per-token Python /
+launch / H2D cost (~1 ms per step at batch 64) leaves the decode loop; tokens past a stop condition
+are discarded.
 """
 from __future__ import annotations
 
@@ -51,6 +58,10 @@ class EngineConfig:
     prefix_cache: bool = True
     use_graphs: bool = True
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+    # multi-step decode: when every running sequence is decoding (nothing waiting), run this many
+    # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)
+    # and return to the host once per run. 1 disables it.
+    decode_steps: int = 8
 
 
 @dataclass
@@ -118,8 +129,9 @@ class LLMEngine:
         self._ids = itertools.count(1)
         self.step_count = 0
         self.graphs: Dict[int, tuple] = {}
+        self.multi_graphs: Dict[int, tuple] = {}
         self.lock = threading.RLock()
-        self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0)
+        self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0, multi_step_runs=0)
         self.eos = set(mc.eos_token_ids) | set(getattr(tokenizer, "eos_ids", ()) or ())
 
     # ------------------------------------------------------------------ memory
@@ -282,6 +294,125 @@ class LLMEngine:
         for bs in self.cfg.graph_batch_sizes:
             if bs <= (max_bs or self.cfg.max_num_seqs):
                 self._capture(bs)
+                if self._multi_step_capable():
+                    self._capture_multi(bs)
+
+    # ------------------------------------------------------------------ multi-step decode
+    def _multi_step_capable(self) -> bool:
+        return (self.cfg.decode_steps > 1 and not hasattr(self.model, "graph_static_inputs")
+                and not getattr(self.model, "lora_names", None))
+
+    def _capture_multi(self, bs: int):
+        K = self.cfg.decode_steps
+        d = self.device
+        ids = torch.zeros(bs, dtype=torch.int32, device=d)
+        pos = torch.zeros(bs, dtype=torch.int32, device=d)
+        slots = torch.full((bs,), self.pad_block * ops.BLOCK, dtype=torch.int32, device=d)
+        ctx = torch.ones(bs, dtype=torch.int32, device=d)
+        bt = torch.full((bs, self.max_blocks_per_seq), self.pad_block, dtype=torch.int32, device=d)
+        samp = dict(temperature=torch.zeros(bs, dtype=torch.float32, device=d),
+                    top_p=torch.ones(bs, dtype=torch.float32, device=d),
+                    top_k=torch.zeros(bs, dtype=torch.int32, device=d),
+                    seeds=torch.zeros(bs, dtype=torch.int64, device=d))
+        n_valid = torch.zeros(1, dtype=torch.int32, device=d)
+        toks = torch.zeros(K, bs, dtype=torch.int32, device=d)
+        fb = ForwardBatch(token_ids=ids, positions=pos, slots=slots, num_prefill_tokens=0, decode_ctx=ctx,
+                          decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
+
+        def run():
+            for j in range(K):
+                logits = self.model.forward(fb, self.kv, self.decode_ws)
+                ops.sample(logits, samp["temperature"], samp["top_p"], samp["top_k"], samp["seeds"], j,
+                           out=toks[j])
+                if j + 1 < K:
+                    ops.decode_advance(toks[j], ids, pos, ctx, slots, bt, n_valid)
+
+        g = None
+        if d.type == "cuda" and self.cfg.use_graphs:
+            s = torch.cuda.Stream(device=d)
+            s.wait_stream(torch.cuda.current_stream(d))
+            with torch.cuda.stream(s):
+                run()  # warm-up (n_valid = 0: the advance kernel touches no row)
+            torch.cuda.current_stream(d).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                run()
+        self.multi_graphs[bs] = (g, run, fb, samp, n_valid, toks)
+
+    def _multi_steps_for(self, b, reqs) -> int:
+        """K if this pure-decode batch can run a K-step graph, else 1."""
+        K = self.cfg.decode_steps
+        if K <= 1 or not self._multi_step_capable() or self.sched.num_waiting() > 0:
+            return 1
+        if self._graph_bucket(len(reqs)) is None:
+            return 1
+        lim = self.cfg.max_model_len
+        for r in reqs:
+            if r is None or r.finished or r.params.has_penalty:
+                return 1
+            n = len(r.output_ids)
+            if r.params.max_tokens - n < K or len(r.prompt_ids) + n + K > lim:
+                return 1
+        return K
+
+    def _run_multi(self, b, reqs, K: int) -> Optional[List[RequestOutput]]:
+        ids_list = list(b.decode_seq_ids)
+        n = len(ids_list)
+        bt_np = self.sched.reserve_decode(ids_list, K)
+        if bt_np is None:
+            return None
+        bs = self._graph_bucket(n)
+        if bs not in self.multi_graphs:
+            self._capture_multi(bs)
+        g, run, fb, samp, n_valid, toks = self.multi_graphs[bs]
+        params = [r.params for r in reqs]
+        temp = np.fromiter((0.0 if p.top_k == 1 else p.temperature for p in params), np.float32, n)
+        top_p = np.fromiter((p.top_p for p in params), np.float32, n)
+        top_k = np.fromiter((p.top_k for p in params), np.int32, n)
+        # per-run seed stream: the graph bakes the in-run step index, the host mixes in the engine step
+        seeds = (np.asarray([r.seed for r in reqs], np.int64) * np.int64(0x9E3779B1)
+                 + np.int64(self.step_count) * np.int64(0x632BE5AB)) & np.int64(0x7FFFFFFFFFFFFFFF)
+        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx, bt_np, temp, top_p, top_k, seeds,
+                               np.asarray([n], np.int32)])
+        fb.token_ids[:n].copy_(src[0])
+        fb.positions[:n].copy_(src[1])
+        fb.slots[:n].copy_(src[2])
+        fb.decode_ctx[:n].copy_(src[3])
+        mb = bt_np.shape[1]
+        fb.decode_block_tables[:n, :mb].copy_(src[4])
+        if n < bs:
+            fb.token_ids[n:].zero_()
+            fb.positions[n:].zero_()
+            fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
+            fb.decode_ctx[n:].fill_(1)
+            fb.decode_block_tables[n:, 0].fill_(self.pad_block)
+        samp["temperature"][:n].copy_(src[5])
+        samp["top_p"][:n].copy_(src[6])
+        samp["top_k"][:n].copy_(src[7])
+        samp["seeds"][:n].copy_(src[8])
+        n_valid.copy_(src[9])
+        if g is not None:
+            g.replay()
+            self.stats["graph_steps"] += K
+        else:
+            run()  # eager (CPU / graphs off): same device-side feedback, no host round trip per token
+        self.stats["multi_step_runs"] += 1
+        self.step_count += K - 1
+        self.stats["decode_tokens"] += n * (K - 1)
+        host = toks[:, :n].cpu().numpy()  # [K, n]
+        self._mark("forward")
+        outs: List[RequestOutput] = []
+        alive = list(range(n))
+        for j in range(K):
+            outs += self._process([ids_list[i] for i in alive], [reqs[i] for i in alive],
+                                  host[j, alive].tolist(), defer_append=True)
+            alive = [i for i in alive if not reqs[i].finished]
+            if not alive:
+                break
+        if alive:
+            self.sched.advance_decode([ids_list[i] for i in alive], host[:, alive].T.reshape(-1).tolist(), K)
+        self._mark("process")
+        return outs
 
     def _run_graph(self, b, n: int):
         bs = self._graph_bucket(n)
@@ -326,6 +457,14 @@ class LLMEngine:
             self.stats["prefill_tokens"] += P
             self.stats["decode_tokens"] += n_tok - P
             nd = len(b.decode_seq_ids)
+            if P == 0 and nd and self.cfg.decode_steps > 1:
+                dreqs = [self.requests.get(s) for s in b.decode_seq_ids]
+                K = self._multi_steps_for(b, dreqs)
+                if K > 1:
+                    with roctx_range("decode_multi"):
+                        outs = self._run_multi(b, dreqs, K)
+                    if outs is not None:
+                        return outs
             with roctx_range("prefill" if P else "decode"):
                 if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
                         and self._graph_bucket(nd) is not None):
@@ -380,7 +519,9 @@ class LLMEngine:
             f[i], p[i], rp[i] = r.params.frequency_penalty, r.params.presence_penalty, r.params.repetition_penalty
         ops.apply_penalties(logits, *self.stager.stage([ids, cnt, n, f, p, rp]))
 
-    def _process(self, seq_order, reqs, toks) -> List[RequestOutput]:
+    def _process(self, seq_order, reqs, toks, defer_append: bool = False) -> List[RequestOutput]:
+        """Apply one sampled token per sequence. defer_append: the caller hands the tokens of
+        continuing sequences to the scheduler itself (multi-step runs)."""
         outs: List[RequestOutput] = []
         cont_ids, cont_toks = [], []
         now = time.perf_counter()
@@ -416,7 +557,7 @@ class LLMEngine:
                 cont_ids.append(sid)
                 cont_toks.append(t)
             outs.append(RequestOutput(req.request_id, t, delta, reason is not None, reason))
-        if cont_ids:
+        if cont_ids and not defer_append:
             self.sched.append_tokens(cont_ids, cont_toks)
         return outs
 

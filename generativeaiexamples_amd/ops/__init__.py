@@ -394,7 +394,7 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
 # ---------------------------------------------------------------------------------------------
 def sample(logits, temperature, top_p, top_k, seeds, step: int, out=None):
     if not logits.is_cuda:
-        return ref.sample(logits, temperature, top_p, top_k, seeds, step)
+        return _into(out, ref.sample(logits, temperature, top_p, top_k, seeds, step).to(torch.int32))
     out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device) if out is None else out
     native().sample(logits, temperature, top_p, top_k, seeds, int(step), out)
     return out
@@ -444,6 +444,14 @@ def embedding(ids, table, vstart: int = 0, vend: int | None = None, out=None):
     out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=ids.device) if out is None else out
     native().embedding(ids.int().contiguous() if ids.dtype != torch.int32 else ids, table, out, vstart, vend)
     return out
+
+
+def decode_advance(toks, ids, pos, ctx, slots, block_tables, n_valid):
+    """In-place multi-step decode update for rows < n_valid[0]: ids <- toks, pos += 1, ctx = pos + 1,
+    slots from block_tables (int32 tensors; graph-capturable: the row count is read on device)."""
+    if not ids.is_cuda:
+        return ref.decode_advance(toks, ids, pos, ctx, slots, block_tables, n_valid, BLOCK)
+    native().decode_advance(toks, ids, pos, ctx, slots, block_tables, n_valid, BLOCK)
 
 
 def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):

@@ -259,6 +259,16 @@ def embedding(ids, table, vstart=0, vend=None):
     return out * ok[:, None].to(out.dtype)
 
 
+def decode_advance(toks, ids, pos, ctx, slots, bt, n_valid, block):
+    n = int(n_valid.reshape(-1)[0])
+    p = pos[:n].long() + 1
+    ids[:n] = toks[:n].to(ids.dtype)
+    pos[:n] = p.to(pos.dtype)
+    ctx[:n] = (p + 1).to(ctx.dtype)
+    rows = torch.arange(n, device=bt.device)
+    slots[:n] = (bt[rows, p // block].long() * block + p % block).to(slots.dtype)
+
+
 def pool(h, cu_seqlens, mode="mean", normalize=True):
     cu = cu_seqlens.tolist()
     outs = []

@@ -85,3 +85,56 @@ def test_preemption_under_block_pressure():
     big = LLMEngine(m, tok, EngineConfig(max_num_seqs=4, max_batched_tokens=256, num_blocks=64,
                                          max_model_len=256, use_graphs=False, prefix_cache=False))
     assert [r.output_ids for r in big.generate(prompts, sp)] == [r.output_ids for r in reqs]
+
+
+def test_multi_step_decode_matches_single_step():
+    """K-step device-side decode runs (reserve_decode / decode_advance / advance_decode) must produce the
+    same greedy tokens as one-token steps, across page boundaries, mixed max_tokens, stop ids mid-run."""
+    m = _model(3)
+    tok = small_byte_tokenizer(512)
+    prompts = [list(range(30, 30 + n)) for n in (7, 15, 16, 33)]
+    sps = [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in (21, 40, 9, 33)]
+
+    def run(steps):
+        eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=8, max_batched_tokens=256, num_blocks=64,
+                                             max_model_len=256, use_graphs=False, decode_steps=steps))
+        return eng, eng.generate(prompts, sps)
+
+    e1, single = run(1)
+    e8, multi = run(8)
+    assert e1.stats["multi_step_runs"] == 0 and e8.stats["multi_step_runs"] > 0
+    for a, b, sp in zip(single, multi, sps):
+        assert a.output_ids == b.output_ids
+        assert len(b.output_ids) == sp.max_tokens and b.finish_reason == "length"
+    # every page returned to the pool once all requests finished
+    assert e8.sched.num_free_blocks() == e8.sched.num_blocks()
+
+    # a stop token that appears mid-run truncates exactly where the single-step engine stops
+    stop = single[1].output_ids[12]
+    sp_stop = [SamplingParams(temperature=0.0, max_tokens=40, stop_token_ids=[stop])] * len(prompts)
+    outs = []
+    for steps in (1, 8):
+        eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=8, max_batched_tokens=256, num_blocks=64,
+                                             max_model_len=256, use_graphs=False, decode_steps=steps))
+        outs.append(eng.generate(prompts, sp_stop))
+        assert eng.sched.num_free_blocks() == eng.sched.num_blocks()
+    for a, b in zip(*outs):
+        assert a.output_ids == b.output_ids and a.finish_reason == b.finish_reason
+
+
+def test_scheduler_reserve_and_advance_decode():
+    from generativeaiexamples_amd import _rt
+
+    s = _rt.Scheduler(8, 4, 64, 128, False, 64)
+    s.add(1, list(range(20)), 50, 0)
+    b = s.schedule()  # prefill 20 tokens: 2 pages
+    assert b.num_prefill_tokens == 20
+    s.append_tokens([1], [7])
+    b = s.schedule()  # decode position 20
+    assert list(b.decode_seq_ids) == [1] and s.num_free_blocks() == 6
+    bt = s.reserve_decode([1], 16)  # positions 20..35 -> 3 pages
+    assert bt.shape == (1, 3) and s.num_free_blocks() == 5
+    s.advance_decode([1], list(range(100, 116)), 16)
+    assert s.num_tokens(1) == 21 + 16
+    assert s.reserve_decode([1], 200) is None  # past max_model_len: nothing allocated
+    assert s.num_free_blocks() == 5

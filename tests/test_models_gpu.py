@@ -101,3 +101,27 @@ def test_hbm_index_roundtrip(cuda, tmp_path):
     l2 = HBMIndex(64, "l2", device=cuda)
     l2.add(v)
     assert l2.search(v[7:8], k=1)[0][0].row == 7
+
+
+def test_multi_step_graph_decode_equals_single_step(cuda):
+    """K=8 decode steps in one captured graph (sampler + decode_advance feedback on device, padded bucket)
+    must reproduce one-token-per-step eager decoding (greedy)."""
+    g, _ = _pair_llama(cuda)
+    tok = small_byte_tokenizer(512)
+    prompts = [list(range(9, 9 + n)) for n in (5, 17, 31)]
+    sps = [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in (26, 19, 40)]
+    res = []
+    for steps, graphs in ((1, False), (8, True)):
+        eng = LLMEngine(g, tok, EngineConfig(num_blocks=128, max_model_len=512, use_graphs=graphs,
+                                             graph_batch_sizes=(1, 2, 4, 8), decode_steps=steps))
+        reqs = eng.generate(prompts, sps)
+        res.append([r.output_ids for r in reqs])
+        if steps > 1:
+            assert eng.stats["multi_step_runs"] > 0 and eng.stats["graph_steps"] > 0
+            assert eng.sched.num_free_blocks() == eng.sched.num_blocks()
+    assert res[0] == res[1]
+    # sampled (temperature) multi-step runs stay in range and honour max_tokens
+    eng = LLMEngine(g, tok, EngineConfig(num_blocks=128, max_model_len=512, graph_batch_sizes=(1, 2, 4, 8)))
+    reqs = eng.generate(prompts, SamplingParams(temperature=0.8, top_p=0.9, max_tokens=24, ignore_eos=True))
+    for r in reqs:
+        assert len(r.output_ids) == 24 and all(0 <= t < g.cfg.vocab_size for t in r.output_ids)
