@@ -233,7 +233,7 @@ void gemm_splitk(const Tensor& A, const Tensor& B, Tensor& C, const optional<Ten
   const int N = B.size(0);
   TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm_splitk: A and B must be contiguous");
   TORCH_CHECK(B.size(1) == K, "gemm_splitk: K mismatch");
-  TORCH_CHECK(M <= 64 && K % 512 == 0, "gemm_splitk: needs M <= 64 and K % 512 == 0");
+  TORCH_CHECK(M <= 64 && gai_gemm_splitk_ks(M, N, K) > 0, "gemm_splitk: needs M <= 64 and K % 128 == 0");
   const bool f32 = C.scalar_type() == at::kFloat;
   TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm_splitk: C must be bf16 or fp32");
   const int ldc = epi == 4 ? N / 2 : N;

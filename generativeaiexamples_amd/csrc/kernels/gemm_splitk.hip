@@ -100,6 +100,156 @@ __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-streamed variant (default). The kernel above stages the WHOLE activation K-slice in LDS,
+// so at M = 64 the slice is capped at 1024 columns (128 KiB, one workgroup per CU): K is split
+// 4-8 ways, the fp32 partials add 12-25 % to the weight traffic of the K = 4096 projections, and
+// every wave streams a single 16 KiB ring fill before it drains. Here nothing is staged:
+//  * a wave owns a 16*MB x 64 output tile (MB x 4 MFMA 16x16x32 blocks), so each k32 step loads
+//    4 weight fragments from HBM and MB activation fragments (L2-resident, 1:1 with the weights at
+//    M = 64) straight into a 3-deep register ring; only ordinary loads, so the compiler's counted
+//    vmcnt keeps 3 steps in flight (no LDS-DMA / barrier in the loop);
+//  * the 4 waves of a workgroup split K four ways over the SAME 64 columns and reduce through LDS
+//    (row stride 68 floats: conflict-free), so a workgroup covers its whole K-slice with no global
+//    partials; cross-workgroup KS > 1 is used only when the column tiles give < 256 workgroups;
+//  * with KS = 1 the epilogue (SwiGLU on the [gate16|up16] interleave, bias, GELU, residual, fp32
+//    logits) is applied by the workgroup itself: no reduce launch.
+constexpr int kDepth = 3;    // k32 steps in flight per wave
+constexpr int kLdsRow = 68;  // fp32 row stride of the reduction tiles
+
+template <int MB>
+constexpr int dec_lds_bytes() { return 4 * 16 * MB * kLdsRow * 4; }
+
+template <int MB, int EPI, bool OUTF32>
+__global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                          float* __restrict__ part, void* __restrict__ C,
+                                                          const bf16* __restrict__ bias, const bf16* R, int M, int N,
+                                                          int K, int KW, int ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ROWS = 16 * MB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * 64;
+  const int ks = blockIdx.y, KS = gridDim.y;
+  const int kbeg = (ks * 4 + wid) * KW;  // this wave's K range [kbeg, kbeg + KW)
+  const int nsteps = KW / 32;
+  const int kq = 8 * (lane >> 4);
+
+  const bf16* ap[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) ap[i] = A + (size_t)min(16 * i + (lane & 15), M - 1) * K + kbeg + kq;
+  const bf16* wp[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wp[j] = W + (size_t)min(n0 + 16 * j + (lane & 15), N - 1) * K + kbeg + kq;
+
+  bf16x8 ra[kDepth][MB], rw[kDepth][4];
+  auto load = [&](int s, bf16x8 (&a)[MB], bf16x8 (&w)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = load8(wp[j] + 32 * s);
+#pragma unroll
+    for (int i = 0; i < MB; ++i) a[i] = load8(ap[i] + 32 * s);
+  };
+  f32x4 acc[MB][4];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&a)[MB], const bf16x8 (&w)[4]) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
+  };
+
+  // prologue, then per step: MFMAs on the oldest ring slot, refill that slot 3 steps ahead
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d)
+    if (d < nsteps) load(d, ra[d], rw[d]);
+  int s = 0;
+  for (; s + kDepth < nsteps; s += kDepth) {
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) {
+      mma(ra[d], rw[d]);
+      if (s + d + kDepth < nsteps) load(s + d + kDepth, ra[d], rw[d]);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d)
+    if (s + d < nsteps) mma(ra[d], rw[d]);
+
+  // in-workgroup K reduction: tile[w][m][n] (row stride kLdsRow)
+  float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        tile[(wid * ROWS + 16 * i + 4 * (lane >> 4) + r) * kLdsRow + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  // thread -> (row m, 16-column group q); ROWS * 4 items
+  for (int e = tid; e < ROWS * 4; e += 256) {
+    const int m = e >> 2, q = e & 3;
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float* t = tile + (w * ROWS + m) * kLdsRow + 16 * q;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(t + c);
+        v[c] += x.x;
+        v[c + 1] += x.y;
+        v[c + 2] += x.z;
+        v[c + 3] += x.w;
+      }
+    }
+    if (m >= M) continue;
+    if (KS > 1) {
+      float* dst = part + ((size_t)ks * M + m) * N + n0 + 16 * q;
+      if (n0 + 16 * q + 16 <= N) {
+#pragma unroll
+        for (int c = 0; c < 16; c += 4) *reinterpret_cast<float4*>(dst + c) = float4{v[c], v[c + 1], v[c + 2], v[c + 3]};
+      } else {
+        for (int c = 0; c < 16; ++c)
+          if (n0 + 16 * q + c < N) dst[c] = v[c];
+      }
+      continue;
+    }
+    if (EPI == EPI_SWIGLU) {
+      // columns [g16 u16 g16 u16]: the gate lanes (q even) pull the up half from the next group
+      if (q & 1) continue;
+      const float* up = tile + m * kLdsRow + 16 * (q + 1);
+      float u[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) u[c] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) u[c] += up[w * ROWS * kLdsRow + c];
+      const int oc = n0 / 2 + 8 * q;
+      if (n0 + 16 * q + 32 <= N && !OUTF32) {
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          o0[c] = (bf16)(silu(v[c]) * u[c]);
+          o1[c] = (bf16)(silu(v[8 + c]) * u[8 + c]);
+        }
+        store8(reinterpret_cast<bf16*>(C) + (size_t)m * ldc + oc, o0);
+        store8(reinterpret_cast<bf16*>(C) + (size_t)m * ldc + oc + 8, o1);
+      } else {
+        for (int c = 0; c < 16; ++c)
+          if (n0 + 16 * q + 16 + c < N) store_out<EPI_NONE, OUTF32>(C, nullptr, nullptr, ldc, m, oc + c, silu(v[c]) * u[c]);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (n0 + 16 * q + c < N) store_out<EPI, OUTF32>(C, bias, R, ldc, m, n0 + 16 * q + c, v[c]);
+    }
+  }
+}
+
 // Sum the KS partial slabs and apply the epilogue. One thread per output element.
 template <int EPI, bool OUTF32>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int KS, int M, int N,
@@ -136,8 +286,10 @@ void launch_reduce(const float* part, int KS, int M, int N, void* C, const void*
 
 }  // namespace
 
-// K-split chosen so the grid reaches ~2 workgroups per CU while the staged slice fits the LDS.
-int gai_gemm_splitk_ks(int M, int N, int K) {
+namespace {
+
+// Legacy (whole-slice staging) K-split: the grid reaches ~2 workgroups per CU while the slice fits LDS.
+int legacy_ks(int M, int N, int K) {
   if (K % kKAlign) return 0;
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   const int kl_max = (128 * 1024) / (16 * MB * 2);  // LDS bytes / row bytes
@@ -154,10 +306,83 @@ int gai_gemm_splitk_ks(int M, int N, int K) {
   return best;
 }
 
+// Which variant serves a shape (measured on MI355X, profiles/r1/kernel_bench_decode_gemm_v2.jsonl): the
+// register-streamed kernel wins on the wide (gate_up, lm_head: 1.1-1.3x) and deep (down: 1.1-1.4x)
+// projections; the LDS-staged one stays ahead on the square K = 4096 ones (QKV, O) by 2-10 %.
+// GAI_SPLITK_V = 1 / 2 forces the legacy / streamed variant.
+bool use_legacy(int N, int K) {
+  static const int v = getenv("GAI_SPLITK_V") ? atoi(getenv("GAI_SPLITK_V")) : 0;
+  if (v) return v == 1;
+  return K % kKAlign == 0 && K <= 4096 && N <= 8192;
+}
+
+// Register-streamed K-split across workgroups (each workgroup already splits its slice 4 ways over
+// its waves): the smallest KS with K / (4 KS) a multiple of 32 that reaches kMinWG workgroups.
+int stream_ks(int N, int K) {
+  static const int min_wg = getenv("GAI_SPLITK_MINWG") ? atoi(getenv("GAI_SPLITK_MINWG")) : 256;
+  if (K % 128) return 0;
+  const int tiles = (N + 63) / 64;
+  const int units = K / 128;
+  for (int KS = 1; KS <= units; ++KS) {
+    if (units % KS) continue;
+    if ((long)tiles * KS >= min_wg) return KS;
+  }
+  return units;
+}
+
+}  // namespace
+
+int gai_gemm_splitk_ks(int M, int N, int K) { return use_legacy(N, K) ? legacy_ks(M, N, K) : stream_ks(N, K); }
+
 size_t gai_gemm_splitk_ws_bytes(int M, int N, int K) {
   const int KS = gai_gemm_splitk_ks(M, N, K);
-  return (size_t)KS * M * N * sizeof(float);
+  return (size_t)(KS > 1 ? KS : 1) * M * N * sizeof(float);
 }
+
+namespace {
+
+template <int MB, int EPI, bool OUTF32>
+void launch_stream(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                   int ldc, int KS, float* ws, hipStream_t st) {
+  auto kern = gemm_dec_kernel<MB, EPI, OUTF32>;
+  static bool once = false;
+  if (!once) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        dec_lds_bytes<MB>());
+    once = true;
+  }
+  dim3 grid((N + 63) / 64, KS);
+  kern<<<grid, 256, dec_lds_bytes<MB>(), st>>>((const bf16*)A, (const bf16*)B, ws, C, (const bf16*)bias,
+                                               (const bf16*)R, M, N, K, K / (4 * KS), ldc);
+  GAI_LAUNCH_CHECK();
+}
+
+template <int MB>
+void dispatch_stream_ks1(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
+                         int ldc, int epi, int out_f32, hipStream_t st) {
+#define GAI_SS(E)                                                                           \
+  case E:                                                                                   \
+    if (out_f32)                                                                            \
+      launch_stream<MB, E, true>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, st);           \
+    else                                                                                    \
+      launch_stream<MB, E, false>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, st);          \
+    return;
+  switch (epi) {
+    GAI_SS(EPI_NONE)
+    GAI_SS(EPI_BIAS)
+    GAI_SS(EPI_BIAS_GELU)
+    GAI_SS(EPI_RESIDUAL)
+    GAI_SS(EPI_SWIGLU)
+    GAI_SS(EPI_BIAS_RESIDUAL)
+    GAI_SS(EPI_BIAS_RELU)
+    GAI_SS(EPI_BIAS_QUICKGELU)
+    default:
+      gai_launch_error(__FILE__, __LINE__, "gemm_splitk: unknown epilogue");
+  }
+#undef GAI_SS
+}
+
+}  // namespace
 
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                      int ldc, int epi, int out_f32, float* ws, hipStream_t st) {
@@ -165,10 +390,21 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
   if (M > 64) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: M must be <= 64");
   const int KS = gai_gemm_splitk_ks(M, N, K);
   if (KS == 0) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: K must be a multiple of 512");
-  const int KL = K / KS;
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  const size_t lds = (size_t)16 * MB * KL * 2;
-  dim3 grid((N + 63) / 64, KS);
+  if (!use_legacy(N, K)) {
+    if (KS == 1) {
+      if (MB == 1) dispatch_stream_ks1<1>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+      else if (MB == 2) dispatch_stream_ks1<2>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+      else dispatch_stream_ks1<4>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+      return;
+    }
+    if (MB == 1) launch_stream<1, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
+    else if (MB == 2) launch_stream<2, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
+    else launch_stream<4, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
+  } else {
+    const int KL = K / KS;
+    const size_t lds = (size_t)16 * MB * KL * 2;
+    dim3 grid((N + 63) / 64, KS);
 #define GAI_SK(MBV)                                                                                          \
   case MBV: {                                                                                                \
     static bool once = false;                                                                                \
@@ -181,12 +417,13 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
     GAI_LAUNCH_CHECK();                                                                                      \
     break;                                                                                                   \
   }
-  switch (MB) {
-    GAI_SK(1)
-    GAI_SK(2)
-    GAI_SK(4)
-  }
+    switch (MB) {
+      GAI_SK(1)
+      GAI_SK(2)
+      GAI_SK(4)
+    }
 #undef GAI_SK
+  }
 #define GAI_SKR(E)                                                         \
   case E:                                                                  \
     if (out_f32)                                                           \

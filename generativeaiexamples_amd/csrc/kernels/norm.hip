@@ -20,27 +20,39 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16* __restrict__ x, c
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= T) return;
   const size_t base = (size_t)row * D;
-  float v[NCH][8];
+  // Issue every load of the row (x, residual, gamma) before the first store: residual_out usually
+  // aliases residual_in, so a store inside the load loop would pin each later load behind it and
+  // serialise NCH memory round trips (10+ us for a 64-row decode norm instead of one trip).
+  bf16x8 xa[NCH], ra[NCH], ga[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int idx = (c * 64 + lane) * 8;
+    if (idx < D) {
+      xa[c] = load8(x + base + idx);
+      ra[c] = residual_in ? load8(residual_in + base + idx) : bf16x8{};
+      ga[c] = load8(w + idx);
+    }
+  }
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int idx = (c * 64 + lane) * 8;
     if (idx < D) {
-      bf16x8 a = load8(x + base + idx);
+      bf16x8 a = xa[c];
       if (residual_in) {
-        bf16x8 r = load8(residual_in + base + idx);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = (bf16)((float)a[j] + (float)r[j]);
-        if (residual_out) store8(residual_out + base + idx, a);
+        for (int j = 0; j < 8; ++j) a[j] = (bf16)((float)a[j] + (float)ra[c][j]);
+        xa[c] = a;
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[c][j] = (float)a[j];
-        s += LAYERNORM ? v[c][j] : v[c][j] * v[c][j];
-      }
-    } else {
+      for (int j = 0; j < 8; ++j) s += LAYERNORM ? (float)a[j] : (float)a[j] * (float)a[j];
+    }
+  }
+  if (residual_in && residual_out) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = (c * 64 + lane) * 8;
+      if (idx < D) store8(residual_out + base + idx, xa[c]);
     }
   }
   s = wave_sum(s);
@@ -54,7 +66,7 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16* __restrict__ x, c
       if (idx < D) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float d = v[c][j] - mean;
+          const float d = (float)xa[c][j] - mean;
           q += d * d;
         }
       }
@@ -68,15 +80,15 @@ __global__ __launch_bounds__(256) void norm_kernel(const bf16* __restrict__ x, c
   for (int c = 0; c < NCH; ++c) {
     const int idx = (c * 64 + lane) * 8;
     if (idx < D) {
-      const bf16x8 g = load8(w + idx);
+      const bf16x8 g = ga[c];
       bf16x8 o;
       if (LAYERNORM) {
         const bf16x8 bb = b ? load8(b + idx) : bf16x8{};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (bf16)((v[c][j] - mean) * inv * (float)g[j] + (b ? (float)bb[j] : 0.f));
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)(((float)xa[c][j] - mean) * inv * (float)g[j] + (b ? (float)bb[j] : 0.f));
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[c][j] * inv * (float)g[j]);
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)xa[c][j] * inv * (float)g[j]);
       }
       store8(out + base + idx, o);
     }

@@ -59,3 +59,24 @@ def test_linear_routes_decode_to_splitk(cuda):
         torch.testing.assert_close(y.float().cpu(), r, rtol=2e-2, atol=2e-2)
     finally:
         ops.TUNER.mode = old
+
+
+@pytest.mark.parametrize("M", [5, 16, 40, 64])
+@pytest.mark.parametrize("act", [None, "bias", "gelu", "residual", "swiglu"])
+def test_splitk_wide_single_pass_epilogue(cuda, M, act):
+    """N >= 256 column tiles -> one workgroup pass over K (KS = 1): the epilogue runs inside the GEMM kernel
+    (4-wave in-workgroup K reduction through LDS), including a partial last column tile."""
+    N, K = (16448 if act == "swiglu" else 16400), 1024
+    torch.manual_seed(M + 11)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16) if act in ("bias", "gelu") else None
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if act == "residual" else None
+    assert ops.native().gemm_splitk_ws_floats(M, N, K) == M * N  # KS == 1
+    out_dtype = torch.float32 if act is None else torch.bfloat16
+    y = _run(x, w, bias, res, ops.EPI[act] if act else 0, out_dtype)
+    a = act if act in ("gelu", "swiglu") else None
+    r = ref.linear(x.cpu(), w.cpu(), None if bias is None else bias.cpu(), None if res is None else res.cpu(), a,
+                   torch.float32)
+    tol = 2e-3 if out_dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float().cpu(), r, rtol=tol, atol=tol)
