@@ -367,6 +367,22 @@ void gelu(const Tensor& x, Tensor& y) {
   gai_gelu(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
 }
 
+void gelu_tanh(const Tensor& x, Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  const int I = y.size(-1);
+  TORCH_CHECK(I % 8 == 0 && x.numel() == y.numel(), "gelu_tanh: width must be a multiple of 8");
+  gai_gelu_tanh(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
+}
+
+void geglu_interleaved(const Tensor& x, Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  const int I = y.size(-1);
+  TORCH_CHECK(I % 16 == 0 && x.size(-1) == 2 * I, "geglu_interleaved: bad widths");
+  gai_geglu_interleaved(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -398,6 +414,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool", &pool);
   m.def("silu_mul", &silu_mul);
   m.def("gelu", &gelu);
+  m.def("gelu_tanh", &gelu_tanh);
+  m.def("geglu_interleaved", &geglu_interleaved);
   m.def("silu_mul_interleaved", &silu_mul_interleaved);
   m.attr("ARCH") = "gfx950";
 }

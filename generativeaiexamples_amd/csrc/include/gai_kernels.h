@@ -64,6 +64,8 @@ void gai_embedding(const int* ids, const void* table, void* out, int T, int D, i
 void gai_pool(const void* h, const int* cu, float* out, int B, int D, int mode, int normalize, hipStream_t st);
 void gai_silu_mul(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_gelu(const void* x, void* y, int T, int I, hipStream_t st);
+void gai_gelu_tanh(const void* x, void* y, int T, int I, hipStream_t st);
+void gai_geglu_interleaved(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t st);
 void gai_decode_advance(const int* toks, int* ids, int* pos, int* ctx, int* slots, const int* bt, int max_blocks,
                         const int* n_valid, int B, int block, hipStream_t st);

@@ -53,7 +53,7 @@ __device__ __forceinline__ int k_lds_off(int key, int u) {
 __device__ __forceinline__ int v_lds_off(int d, int u) { return d * 128 + ((u ^ ((d >> 1) & 15)) << 3); }
 
 template <int D, int HPW>
-__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
+__global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
@@ -436,6 +436,9 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   GAI_PF(128, 1)
   GAI_PF(128, 2)
   GAI_PF(128, 4)
+  GAI_PF(256, 1)
+  GAI_PF(256, 2)
+  GAI_PF(256, 4)
 #undef GAI_PF
   gai_launch_error(__FILE__, __LINE__, "attn_prefill: unsupported head_dim");
 }
@@ -470,6 +473,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   }
   GAI_DEC(64)
   GAI_DEC(128)
+  GAI_DEC(256)
 #undef GAI_DEC
   gai_launch_error(__FILE__, __LINE__, "attn_decode: unsupported head_dim");
 }

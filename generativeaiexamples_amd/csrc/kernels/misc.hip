@@ -63,7 +63,9 @@ __global__ __launch_bounds__(256) void pool_kernel(const bf16* __restrict__ h, c
   for (int d = threadIdx.x; d < D; d += 256) out[(size_t)b * D + d] = acc[d] * scale;
 }
 
-// y[t, i] = silu(x[t, i]) * x[t, I + i] (non-interleaved gate|up) or gelu(x)
+// MODE 0: y[t, i] = silu(x[t, i]) * x[t, I + i] (non-interleaved gate|up); 1: gelu_erf(x);
+// 2: SwiGLU on the interleaved-per-16 [gate16|up16] layout; 3: gelu_tanh(x); 4: GeGLU (gelu_tanh(gate) * up,
+// interleaved layout: Gemma).
 template <int MODE>
 __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int T, int I) {
   const int units = I / 8;
@@ -71,12 +73,17 @@ __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf
   if (e >= (long)T * units) return;
   const int t = (int)(e / units), u = (int)(e % units);
   bf16x8 o;
-  if (MODE == 2) {  // gate/up interleaved per 16 columns (the fused-SwiGLU weight layout)
+  if (MODE == 2 || MODE == 4) {  // gate/up interleaved per 16 columns (the fused-GLU weight layout)
     const int c = u * 8, p = c >> 4, c0 = c & 15;
     const bf16x8 g = load8(x + (size_t)t * 2 * I + 32 * p + c0);
     const bf16x8 up = load8(x + (size_t)t * 2 * I + 32 * p + 16 + c0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)(silu((float)g[j]) * (float)up[j]);
+    for (int j = 0; j < 8; ++j)
+      o[j] = (bf16)((MODE == 2 ? silu((float)g[j]) : gelu_tanh((float)g[j])) * (float)up[j]);
+  } else if (MODE == 3) {
+    const bf16x8 a = load8(x + (size_t)t * I + u * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_tanh((float)a[j]);
   } else if (MODE == 0) {
     const bf16x8 g = load8(x + (size_t)t * 2 * I + u * 8);
     const bf16x8 up = load8(x + (size_t)t * 2 * I + I + u * 8);
@@ -143,6 +150,20 @@ void gai_silu_mul_interleaved(const void* x, void* y, int T, int I, hipStream_t 
   if (T == 0) return;
   const long n = (long)T * (I / 8);
   act_kernel<2><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)x, (bf16*)y, T, I);
+  GAI_LAUNCH_CHECK();
+}
+
+void gai_gelu_tanh(const void* x, void* y, int T, int I, hipStream_t st) {
+  if (T == 0) return;
+  const long n = (long)T * (I / 8);
+  act_kernel<3><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)x, (bf16*)y, T, I);
+  GAI_LAUNCH_CHECK();
+}
+
+void gai_geglu_interleaved(const void* x, void* y, int T, int I, hipStream_t st) {
+  if (T == 0) return;
+  const long n = (long)T * (I / 8);
+  act_kernel<4><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)x, (bf16*)y, T, I);
   GAI_LAUNCH_CHECK();
 }
 

@@ -8,6 +8,16 @@ Per layer, 7 launches: RMSNorm -> QKV GEMM -> fused RoPE + paged-KV write -> att
 with the residual add fused in its epilogue -> RMSNorm -> gate/up GEMM with SwiGLU fused in its
 epilogue (interleaved weights) -> down GEMM with fused residual add.
 
+The same decoder serves the other dense families the reference fine-tunes or serves through NIM
+ via architecture flags on :class:`LlamaConfig`:
+  * Gemma / CodeGemma (finetuning/Gemma, finetuning/Codegemma): RMSNorm with (1 + w) weights
+    (folded at load), GeGLU MLP (tanh-GELU gate), embeddings scaled by sqrt(hidden), tied LM head,
+    head_dim 256 (MHA 7B, MQA 2B);
+  * StarCoder2 (finetuning/StarCoder2): LayerNorm with bias, non-gated tanh-GELU MLP (c_fc / c_proj)
+    with biases, biased QKV / O projections, GQA;
+  * Qwen2 / 2.5 (QKV bias) and Qwen3 (per-head q/k RMSNorm before RoPE);
+  * Mistral (no flags).
+
 Tensor parallel: QKV and gate/up are column-parallel (heads / intermediate split),
 O and down are row-parallel followed by one all-reduce each (the residual is added on TP rank 0
 only, so it is counted once), embedding and LM head are vocab-parallel (all-gather of logits).
@@ -44,6 +54,15 @@ class LlamaConfig:
     bos_token_id: int = 128000
     eos_token_ids: tuple = (128001, 128009)
     name: str = "llama"
+    # architecture flags (defaults = Llama)
+    arch: str = "llama"        # llama | mistral | gemma | starcoder2 | qwen2 | qwen3
+    norm: str = "rms"          # rms | layernorm (weight + bias)
+    mlp: str = "swiglu"        # swiglu | geglu (interleaved gate/up) | gelu_tanh (non-gated fc -> down)
+    qkv_bias: bool = False
+    o_bias: bool = False
+    mlp_bias: bool = False
+    embed_scale: bool = False  # h = embed * sqrt(hidden) (Gemma)
+    qk_norm: bool = False      # per-head RMSNorm of q and k before RoPE (Qwen3)
 
     @staticmethod
     def llama3_8b(**kw):
@@ -66,6 +85,52 @@ class LlamaConfig:
                            max_position=32768, bos_token_id=1, eos_token_ids=(2,), **kw)
 
     @staticmethod
+    def gemma_7b(**kw):
+        return LlamaConfig(name="google/gemma-7b", arch="gemma", vocab_size=256000, hidden_size=3072,
+                           intermediate_size=24576, num_layers=28, num_heads=16, num_kv_heads=16, head_dim=256,
+                           rope_theta=10000.0, rms_eps=1e-6, tie_embeddings=True, mlp="geglu", embed_scale=True,
+                           bos_token_id=2, eos_token_ids=(1, 107), **kw)
+
+    @staticmethod
+    def gemma_2b(**kw):
+        return LlamaConfig(name="google/gemma-2b", arch="gemma", vocab_size=256000, hidden_size=2048,
+                           intermediate_size=16384, num_layers=18, num_heads=8, num_kv_heads=1, head_dim=256,
+                           rope_theta=10000.0, rms_eps=1e-6, tie_embeddings=True, mlp="geglu", embed_scale=True,
+                           bos_token_id=2, eos_token_ids=(1, 107), **kw)
+
+    @staticmethod
+    def codegemma_7b(**kw):
+        return LlamaConfig.gemma_7b(**{**dict(name="google/codegemma-7b"), **kw})
+
+    @staticmethod
+    def starcoder2_15b(**kw):
+        return LlamaConfig(name="bigcode/starcoder2-15b", arch="starcoder2", vocab_size=49152, hidden_size=6144,
+                           intermediate_size=24576, num_layers=40, num_heads=48, num_kv_heads=4, head_dim=128,
+                           rope_theta=100000.0, rms_eps=1e-5, max_position=16384, norm="layernorm",
+                           mlp="gelu_tanh", qkv_bias=True, o_bias=True, mlp_bias=True, bos_token_id=0,
+                           eos_token_ids=(0,), **kw)
+
+    @staticmethod
+    def starcoder2_7b(**kw):
+        return LlamaConfig.starcoder2_15b(**{**dict(name="bigcode/starcoder2-7b", hidden_size=4608,
+                                                    intermediate_size=18432, num_layers=32, num_heads=36,
+                                                    num_kv_heads=4, rope_theta=1000000.0), **kw})
+
+    @staticmethod
+    def qwen25_7b(**kw):
+        return LlamaConfig(name="qwen/qwen2.5-7b-instruct", arch="qwen2", vocab_size=152064, hidden_size=3584,
+                           intermediate_size=18944, num_layers=28, num_heads=28, num_kv_heads=4, head_dim=128,
+                           rope_theta=1000000.0, rms_eps=1e-6, max_position=32768, qkv_bias=True,
+                           bos_token_id=151643, eos_token_ids=(151645, 151643), **kw)
+
+    @staticmethod
+    def qwen3_8b(**kw):
+        return LlamaConfig(name="qwen/qwen3-8b", arch="qwen3", vocab_size=151936, hidden_size=4096,
+                           intermediate_size=12288, num_layers=36, num_heads=32, num_kv_heads=8, head_dim=128,
+                           rope_theta=1000000.0, rms_eps=1e-6, max_position=40960, qk_norm=True,
+                           bos_token_id=151643, eos_token_ids=(151645, 151643), **kw)
+
+    @staticmethod
     def tiny(**kw):
         base = dict(vocab_size=512, hidden_size=256, intermediate_size=512, num_layers=2, num_heads=4,
                     num_kv_heads=2, head_dim=64, max_position=2048, bos_token_id=1, eos_token_ids=(2,),
@@ -78,7 +143,22 @@ class LlamaConfig:
         with open(os.path.join(path, "config.json")) as f:
             c = json.load(f)
         eos = c.get("eos_token_id", 2)
-        return LlamaConfig(
+        mt = c.get("model_type", "llama")
+        flags = {}
+        if mt == "gemma":
+            flags = dict(arch="gemma", mlp="geglu", embed_scale=True)
+            c.setdefault("tie_word_embeddings", True)
+        elif mt == "starcoder2":
+            flags = dict(arch="starcoder2", norm="layernorm", mlp="gelu_tanh", qkv_bias=c.get("use_bias", True),
+                         o_bias=c.get("use_bias", True), mlp_bias=c.get("use_bias", True))
+            c.setdefault("rms_norm_eps", c.get("norm_epsilon", 1e-5))
+        elif mt == "qwen2":
+            flags = dict(arch="qwen2", qkv_bias=True)
+        elif mt == "qwen3":
+            flags = dict(arch="qwen3", qk_norm=True, qkv_bias=bool(c.get("attention_bias", False)))
+        elif mt == "mistral":
+            flags = dict(arch="mistral")
+        return LlamaConfig(**flags,
             vocab_size=c["vocab_size"], hidden_size=c["hidden_size"], intermediate_size=c["intermediate_size"],
             num_layers=c["num_hidden_layers"], num_heads=c["num_attention_heads"],
             num_kv_heads=c.get("num_key_value_heads", c["num_attention_heads"]),
@@ -99,6 +179,7 @@ class LlamaModel:
         self.dtype = dtype
         tp = self.ctx.tp_size
         assert cfg.num_heads % tp == 0 and cfg.num_kv_heads % tp == 0 and cfg.intermediate_size % (16 * tp) == 0
+        assert cfg.norm in ("rms", "layernorm") and cfg.mlp in ("swiglu", "geglu", "gelu_tanh"), cfg
         self.hq = cfg.num_heads // tp
         self.hkv = cfg.num_kv_heads // tp
         self.inter = cfg.intermediate_size // tp
@@ -117,6 +198,7 @@ class LlamaModel:
         c, d, dt = self.cfg, self.device, self.dtype
         D, hd = c.hidden_size, c.head_dim
         e = lambda *s: torch.empty(*s, device=d, dtype=dt)  # noqa: E731
+        ln = c.norm == "layernorm"
         self.w["embed"] = e(self.vocab_local, D)
         for i in range(c.num_layers):
             p = f"l{i}."
@@ -124,9 +206,28 @@ class LlamaModel:
             self.w[p + "qkv"] = e((self.hq + 2 * self.hkv) * hd, D)
             self.w[p + "o"] = e(D, self.hq * hd)
             self.w[p + "mlp_norm"] = e(D)
-            self.w[p + "gate_up"] = e(2 * self.inter, D)  # interleaved per 16 rows
+            if c.mlp == "gelu_tanh":
+                self.w[p + "fc"] = e(self.inter, D)
+            else:
+                self.w[p + "gate_up"] = e(2 * self.inter, D)  # interleaved per 16 rows
             self.w[p + "down"] = e(D, self.inter)
+            if ln:
+                self.w[p + "attn_norm_b"] = e(D)
+                self.w[p + "mlp_norm_b"] = e(D)
+            if c.qkv_bias:
+                self.w[p + "qkv_b"] = e((self.hq + 2 * self.hkv) * hd)
+            if c.o_bias:
+                self.w[p + "o_b"] = e(D)
+            if c.mlp_bias:
+                self.w[p + ("fc_b" if c.mlp == "gelu_tanh" else "gate_up_b")] = e(
+                    self.inter if c.mlp == "gelu_tanh" else 2 * self.inter)
+                self.w[p + "down_b"] = e(D)
+            if c.qk_norm:
+                self.w[p + "q_norm"] = e(hd)
+                self.w[p + "k_norm"] = e(hd)
         self.w["norm"] = e(D)
+        if ln:
+            self.w["norm_b"] = e(D)
         self.w["lm_head"] = self.w["embed"] if c.tie_embeddings else e(self.vocab_local, D)
 
     def random_init(self, seed: int = 0):
@@ -136,6 +237,8 @@ class LlamaModel:
         for k, t in self.w.items():
             if k.endswith("norm"):
                 t.fill_(1.0)
+            elif k.endswith("_b"):
+                t.zero_() if k.endswith("norm_b") else randn_like_(t, s, 0.02)
             elif k == "lm_head" and c.tie_embeddings:
                 continue
             else:
@@ -155,6 +258,9 @@ class LlamaModel:
         def put(name, t):
             self.w[name].copy_(t.to(self.dtype))
 
+        def norm_w(t):  # Gemma stores RMSNorm weights as w with y = x_hat * (1 + w): fold the 1 in
+            return t.float() + 1.0 if c.arch == "gemma" else t
+
         emb = sd["model.embed_tokens.weight"]
         pad = self.vocab_local * tp - emb.shape[0]
         if pad:
@@ -162,16 +268,30 @@ class LlamaModel:
         put("embed", shard_rows(emb, emb.shape[0]))
         for i in range(c.num_layers):
             p, h = f"l{i}.", f"model.layers.{i}."
-            put(p + "attn_norm", sd[h + "input_layernorm.weight"])
-            put(p + "mlp_norm", sd[h + "post_attention_layernorm.weight"])
+            put(p + "attn_norm", norm_w(sd[h + "input_layernorm.weight"]))
+            put(p + "mlp_norm", norm_w(sd[h + "post_attention_layernorm.weight"]))
+            if c.norm == "layernorm":
+                put(p + "attn_norm_b", sd[h + "input_layernorm.bias"])
+                put(p + "mlp_norm_b", sd[h + "post_attention_layernorm.bias"])
             q = shard_rows(sd[h + "self_attn.q_proj.weight"], c.num_heads * hd)
             k = shard_rows(sd[h + "self_attn.k_proj.weight"], c.num_kv_heads * hd)
             v = shard_rows(sd[h + "self_attn.v_proj.weight"], c.num_kv_heads * hd)
             put(p + "qkv", torch.cat([q, k, v]))
+            if c.qkv_bias:
+                put(p + "qkv_b", torch.cat([shard_rows(sd[h + "self_attn.q_proj.bias"], c.num_heads * hd),
+                                            shard_rows(sd[h + "self_attn.k_proj.bias"], c.num_kv_heads * hd),
+                                            shard_rows(sd[h + "self_attn.v_proj.bias"], c.num_kv_heads * hd)]))
+            if c.qk_norm:
+                put(p + "q_norm", sd[h + "self_attn.q_norm.weight"])
+                put(p + "k_norm", sd[h + "self_attn.k_norm.weight"])
             o = sd[h + "self_attn.o_proj.weight"]
             put(p + "o", o.reshape(o.shape[0], tp, -1)[:, r] if tp > 1 else o)
+            if c.o_bias:
+                put(p + "o_b", sd[h + "self_attn.o_proj.bias"])
             self._load_mlp(sd, i)
-        put("norm", sd["model.norm.weight"])
+        put("norm", norm_w(sd["model.norm.weight"]))
+        if c.norm == "layernorm":
+            put("norm_b", sd["model.norm.bias"])
         if not c.tie_embeddings:
             lm = sd["lm_head.weight"]
             if pad:
@@ -186,17 +306,30 @@ class LlamaModel:
         def shard_rows(t, n):
             return t.reshape(tp, n // tp, *t.shape[1:])[r] if tp > 1 else t
 
-        g = shard_rows(sd[h + "mlp.gate_proj.weight"], c.intermediate_size)
-        u = shard_rows(sd[h + "mlp.up_proj.weight"], c.intermediate_size)
-        self.w[p + "gate_up"].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
-        dn = sd[h + "mlp.down_proj.weight"]
+        if c.mlp == "gelu_tanh":  # StarCoder2: c_fc -> gelu -> c_proj
+            self.w[p + "fc"].copy_(shard_rows(sd[h + "mlp.c_fc.weight"], c.intermediate_size).to(self.dtype))
+            dn = sd[h + "mlp.c_proj.weight"]
+            if c.mlp_bias:
+                self.w[p + "fc_b"].copy_(shard_rows(sd[h + "mlp.c_fc.bias"], c.intermediate_size).to(self.dtype))
+                self.w[p + "down_b"].copy_(sd[h + "mlp.c_proj.bias"].to(self.dtype))
+        else:
+            g = shard_rows(sd[h + "mlp.gate_proj.weight"], c.intermediate_size)
+            u = shard_rows(sd[h + "mlp.up_proj.weight"], c.intermediate_size)
+            self.w[p + "gate_up"].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
+            dn = sd[h + "mlp.down_proj.weight"]
         self.w[p + "down"].copy_((dn.reshape(dn.shape[0], tp, -1)[:, r] if tp > 1 else dn).to(self.dtype))
 
     def export_hf_state(self) -> Dict[str, torch.Tensor]:
         """Inverse of load_hf_state for a TP=1 model (checkpoint export, TP-reshard tests)."""
         assert self.ctx.tp_size == 1
         c, hd, w = self.cfg, self.cfg.head_dim, self.w
-        sd = {"model.embed_tokens.weight": w["embed"].clone(), "model.norm.weight": w["norm"].clone()}
+
+        def norm_w(t):
+            return (t.float() - 1.0).to(t.dtype) if c.arch == "gemma" else t.clone()
+
+        sd = {"model.embed_tokens.weight": w["embed"].clone(), "model.norm.weight": norm_w(w["norm"])}
+        if c.norm == "layernorm":
+            sd["model.norm.bias"] = w["norm_b"].clone()
         if not c.tie_embeddings:
             sd["lm_head.weight"] = w["lm_head"].clone()
         nq, nk = c.num_heads * hd, c.num_kv_heads * hd
@@ -206,13 +339,33 @@ class LlamaModel:
             sd[h + "self_attn.q_proj.weight"] = qkv[:nq].clone()
             sd[h + "self_attn.k_proj.weight"] = qkv[nq:nq + nk].clone()
             sd[h + "self_attn.v_proj.weight"] = qkv[nq + nk:].clone()
+            if c.qkv_bias:
+                b = w[p + "qkv_b"]
+                sd[h + "self_attn.q_proj.bias"] = b[:nq].clone()
+                sd[h + "self_attn.k_proj.bias"] = b[nq:nq + nk].clone()
+                sd[h + "self_attn.v_proj.bias"] = b[nq + nk:].clone()
+            if c.qk_norm:
+                sd[h + "self_attn.q_norm.weight"] = w[p + "q_norm"].clone()
+                sd[h + "self_attn.k_norm.weight"] = w[p + "k_norm"].clone()
             sd[h + "self_attn.o_proj.weight"] = w[p + "o"].clone()
-            gu = w[p + "gate_up"].reshape(-1, 2, 16, c.hidden_size)
-            sd[h + "mlp.gate_proj.weight"] = gu[:, 0].reshape(-1, c.hidden_size).clone()
-            sd[h + "mlp.up_proj.weight"] = gu[:, 1].reshape(-1, c.hidden_size).clone()
-            sd[h + "mlp.down_proj.weight"] = w[p + "down"].clone()
-            sd[h + "input_layernorm.weight"] = w[p + "attn_norm"].clone()
-            sd[h + "post_attention_layernorm.weight"] = w[p + "mlp_norm"].clone()
+            if c.o_bias:
+                sd[h + "self_attn.o_proj.bias"] = w[p + "o_b"].clone()
+            if c.mlp == "gelu_tanh":
+                sd[h + "mlp.c_fc.weight"] = w[p + "fc"].clone()
+                sd[h + "mlp.c_proj.weight"] = w[p + "down"].clone()
+                if c.mlp_bias:
+                    sd[h + "mlp.c_fc.bias"] = w[p + "fc_b"].clone()
+                    sd[h + "mlp.c_proj.bias"] = w[p + "down_b"].clone()
+            else:
+                gu = w[p + "gate_up"].reshape(-1, 2, 16, c.hidden_size)
+                sd[h + "mlp.gate_proj.weight"] = gu[:, 0].reshape(-1, c.hidden_size).clone()
+                sd[h + "mlp.up_proj.weight"] = gu[:, 1].reshape(-1, c.hidden_size).clone()
+                sd[h + "mlp.down_proj.weight"] = w[p + "down"].clone()
+            sd[h + "input_layernorm.weight"] = norm_w(w[p + "attn_norm"])
+            sd[h + "post_attention_layernorm.weight"] = norm_w(w[p + "mlp_norm"])
+            if c.norm == "layernorm":
+                sd[h + "input_layernorm.bias"] = w[p + "attn_norm_b"].clone()
+                sd[h + "post_attention_layernorm.bias"] = w[p + "mlp_norm_b"].clone()
         return sd
 
     def load_safetensors_dir(self, path: str):
@@ -281,23 +434,48 @@ class LlamaModel:
     def kv_shape(self, num_blocks: int):
         return (num_blocks, self.hkv, ops.BLOCK, self.cfg.head_dim), (num_blocks, self.hkv, self.cfg.head_dim, ops.BLOCK)
 
+    def _norm(self, x, name: str, residual=None):
+        c = self.cfg
+        if c.norm == "layernorm":
+            return ops.layer_norm(x, self.w[name], self.w[name + "_b"], c.rms_eps, residual=residual)
+        return ops.rms_norm(x, self.w[name], c.rms_eps, residual=residual)
+
+    def _row_bias(self, name: str):
+        """Bias of a row-parallel projection: added once (TP rank 0) before the all-reduce."""
+        return self.w.get(name) if self.ctx.tp_rank == 0 else None
+
+    @property
+    def embed_multiplier(self) -> float:
+        # Gemma scales embeddings by sqrt(hidden) rounded to the activation dtype (HF `normalizer`)
+        return float(torch.tensor(self.cfg.hidden_size ** 0.5, dtype=self.dtype))
+
+    def _qk_norm(self, qkv: torch.Tensor, p: str):
+        T, hd, hq, hkv = qkv.shape[0], self.cfg.head_dim, self.hq, self.hkv
+        q3 = qkv.view(T, hq + 2 * hkv, hd)
+        for sl, key in ((slice(0, hq), "q_norm"), (slice(hq, hq + hkv), "k_norm")):
+            part = q3[:, sl].reshape(-1, hd)
+            q3[:, sl] = ops.rms_norm(part, self.w[p + key], self.cfg.rms_eps).view(T, -1, hd)
+
     def forward(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
         """Returns fp32 logits [len(sample_rows), vocab] (gathered over TP)."""
         c, w, ctx = self.cfg, self.w, self.ctx
         T, P = fb.num_tokens, fb.num_prefill_tokens
         hd = c.head_dim
-        # residual stream `res` is updated in place by the fused add+RMSNorm kernel, so the O and down
+        # residual stream `res` is updated in place by the fused add+norm kernel, so the O and down
         # projections are plain GEMMs (row-parallel partial sums all-reduced before the add)
         res = ops.embedding(fb.token_ids, w["embed"], self.vstart, self.vstart + self.vocab_local)
         ctx.tp_all_reduce(res)
+        if c.embed_scale:
+            res.mul_(self.embed_multiplier)
         q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
         attn = torch.empty_like(q)
         h = None
         for i in range(c.num_layers):
             p = f"l{i}."
-            x = ops.rms_norm(res, w[p + "attn_norm"], c.rms_eps) if h is None else \
-                ops.rms_norm(h, w[p + "attn_norm"], c.rms_eps, residual=res)
-            qkv = self._lora(ops.linear(x, w[p + "qkv"]), x, i, "qkv", fb)
+            x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
+            qkv = self._lora(ops.linear(x, w[p + "qkv"], bias=w.get(p + "qkv_b")), x, i, "qkv", fb)
+            if c.qk_norm:
+                self._qk_norm(qkv, p)
             kc, vc = kv.layer(i)
             ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True)
             if P > 0:
@@ -306,16 +484,20 @@ class LlamaModel:
             if T > P:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
                                      max_ctx=fb.max_decode_ctx, out=attn[P:])
-            h = self._lora(ops.linear(attn.view(T, -1), w[p + "o"]), attn.view(T, -1), i, "o", fb)
+            a2 = attn.view(T, -1)
+            h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
             ctx.tp_all_reduce(h)
-            x = ops.rms_norm(h, w[p + "mlp_norm"], c.rms_eps, residual=res)
-            g = ops.linear(x, w[p + "gate_up"], act="swiglu")
-            h = ops.linear(g, w[p + "down"])
+            x = self._norm(h, p + "mlp_norm", residual=res)
+            if c.mlp == "gelu_tanh":
+                g = self._lora(ops.linear(x, w[p + "fc"], bias=w.get(p + "fc_b"), act="gelu_tanh"), x, i, "fc", fb)
+            else:
+                g = ops.linear(x, w[p + "gate_up"], act=c.mlp)
+            h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
             ctx.tp_all_reduce(h)
         if fb.sample_rows is not None:
             h = h.index_select(0, fb.sample_rows)
             res = res.index_select(0, fb.sample_rows)
-        x = ops.rms_norm(h, w["norm"], c.rms_eps, residual=res)
+        x = self._norm(h, "norm", residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
         logits = ctx.tp_all_gather_last(logits)
         return logits[:, : c.vocab_size]
@@ -328,6 +510,8 @@ class LlamaModel:
         T = token_ids.numel()
         hd = c.head_dim
         h = w["embed"][token_ids.long().cpu()]
+        if c.embed_scale:
+            h = h * self.embed_multiplier
         cs = self.cos_sin.cpu()[:T]
         cos, sin = cs[:, None, : hd // 2], cs[:, None, hd // 2:]
 
@@ -338,23 +522,38 @@ class LlamaModel:
         def rms(x, g):
             return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_eps) * g
 
+        def norm(x, name):
+            if c.norm == "layernorm":
+                return torch.nn.functional.layer_norm(x, (x.shape[-1],), w[name], w[name + "_b"], c.rms_eps)
+            return rms(x, w[name])
+
+        def bias(name):
+            return w.get(name, 0.0)
+
         for i in range(c.num_layers):
             p = f"l{i}."
-            x = rms(h, w[p + "attn_norm"])
-            qkv = (x @ w[p + "qkv"].t()).view(T, self.hq + 2 * self.hkv, hd)
+            x = norm(h, p + "attn_norm")
+            qkv = (x @ w[p + "qkv"].t() + bias(p + "qkv_b")).view(T, self.hq + 2 * self.hkv, hd)
             q, k, v = qkv[:, : self.hq], qkv[:, self.hq: self.hq + self.hkv], qkv[:, self.hq + self.hkv:]
+            if c.qk_norm:
+                q, k = rms(q, w[p + "q_norm"]), rms(k, w[p + "k_norm"])
             q, k = rope(q), rope(k)
             rep = self.hq // self.hkv
             k, v = k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1)
             att = torch.einsum("qhd,khd->hqk", q, k) * self.scale
             att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1)[None], float("-inf"))
             o = torch.einsum("hqk,khd->qhd", att.softmax(-1), v).reshape(T, -1)
-            h = h + o @ w[p + "o"].t()
-            x = rms(h, w[p + "mlp_norm"])
-            gu = (x @ w[p + "gate_up"].t()).reshape(T, -1, 2, 16)
-            g = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
-            h = h + g @ w[p + "down"].t()
-        return rms(h, w["norm"]) @ w["lm_head"].t()
+            h = h + o @ w[p + "o"].t() + bias(p + "o_b")
+            x = norm(h, p + "mlp_norm")
+            if c.mlp == "gelu_tanh":
+                g = torch.nn.functional.gelu(x @ w[p + "fc"].t() + bias(p + "fc_b"), approximate="tanh")
+            else:
+                gu = (x @ w[p + "gate_up"].t()).reshape(T, -1, 2, 16)
+                act = torch.nn.functional.silu(gu[:, :, 0]) if c.mlp == "swiglu" else \
+                    torch.nn.functional.gelu(gu[:, :, 0], approximate="tanh")
+                g = (act * gu[:, :, 1]).reshape(T, -1)
+            h = h + g @ w[p + "down"].t() + bias(p + "down_b")
+        return norm(h, "norm") @ w["lm_head"].t()
 
     def config_dict(self):
         return asdict(self.cfg)

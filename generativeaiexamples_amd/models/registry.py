@@ -22,6 +22,14 @@ LLM_PRESETS = {
     "llama3.1-8b": ("meta/llama-3.1-8b-instruct", lambda: LlamaConfig.llama31_8b()),
     "mistral-7b": ("mistralai/mistral-7b-instruct-v0.3", lambda: LlamaConfig.mistral_7b()),
     "tiny-llama": ("tiny-llama", lambda: LlamaConfig.tiny(max_position=4096)),
+    # other dense decoder families of the reference's fine-tuning / NIM notebooks
+    "gemma-7b": ("google/gemma-7b", lambda: LlamaConfig.gemma_7b()),
+    "gemma-2b": ("google/gemma-2b", lambda: LlamaConfig.gemma_2b()),
+    "codegemma-7b": ("google/codegemma-7b", lambda: LlamaConfig.codegemma_7b()),
+    "starcoder2-15b": ("bigcode/starcoder2-15b", lambda: LlamaConfig.starcoder2_15b()),
+    "starcoder2-7b": ("bigcode/starcoder2-7b", lambda: LlamaConfig.starcoder2_7b()),
+    "qwen2.5-7b": ("qwen/qwen2.5-7b-instruct", lambda: LlamaConfig.qwen25_7b()),
+    "qwen3-8b": ("qwen/qwen3-8b", lambda: LlamaConfig.qwen3_8b()),
     "opt-125m": ("facebook/opt-125m", lambda: OPTConfig.opt_125m()),
     "mixtral-8x7b": ("mistralai/mixtral-8x7b-instruct-v0.1", lambda: MixtralConfig.mixtral_8x7b()),
     "tiny-moe": ("tiny-moe", lambda: MixtralConfig.tiny_moe()),
@@ -85,7 +93,7 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
             m.quantize_fp8()
         else:
             from .common import quantize_linear_weights_fp8
-            quantize_linear_weights_fp8(m.w, [k for k in m.w if k.split(".")[-1] in ("qkv", "o", "gate_up", "down")])
+            quantize_linear_weights_fp8(m.w, [k for k in m.w if k.split(".")[-1] in ("qkv", "o", "gate_up", "fc", "down")])
         name += "-fp8"
     tok = llama3_byte_tokenizer(vocab) if vocab >= 128256 else small_byte_tokenizer(vocab) \
         if vocab <= 4096 else _generic_tok(m.cfg)

@@ -90,6 +90,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     act: None | 'gelu' | 'relu' | 'quick_gelu' | 'swiglu' (w interleaved per 16 rows, see interleave_gate_up).
     An :class:`Fp8Weight` ``w`` routes to the fp8 MFMA GEMM (``linear_fp8``).
     """
+    if act in ("geglu", "gelu_tanh"):
+        # tanh-GELU family (Gemma GeGLU, StarCoder2 MLP): GEMM (+ bias) then one elementwise kernel
+        assert residual is None and out is None
+        y = linear(x, w, bias, out_dtype=None)
+        y = geglu_interleaved(y) if act == "geglu" else gelu_tanh(y)
+        return y if out_dtype in (None, y.dtype) else y.to(out_dtype)
     if isinstance(w, Fp8Weight):
         return linear_fp8(x, w, bias, residual, act, out_dtype, out)
     if not x.is_cuda:
@@ -521,6 +527,24 @@ def gelu(x):
         return ref.gelu(x)
     y = torch.empty_like(x)
     native().gelu(x, y)
+    return y
+
+
+def gelu_tanh(x):
+    """tanh-approximated GELU (HF ``gelu_pytorch_tanh``: StarCoder2, Gemma)."""
+    if not x.is_cuda:
+        return ref.gelu_tanh(x)
+    y = torch.empty_like(x)
+    native().gelu_tanh(x, y)
+    return y
+
+
+def geglu_interleaved(x):
+    """gelu_tanh(gate) * up on the interleaved-per-16 [gate16|up16] layout -> width / 2 (Gemma MLP)."""
+    if not x.is_cuda:
+        return ref.geglu_interleaved(x)
+    y = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
+    native().geglu_interleaved(x, y)
     return y
 
 

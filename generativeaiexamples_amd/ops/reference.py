@@ -52,10 +52,13 @@ def linear(x, w, bias=None, residual=None, act=None, out_dtype=None):
         y = F.relu(y)
     elif act == "quick_gelu":
         y = y * torch.sigmoid(1.702 * y)
-    elif act == "swiglu":
+    elif act == "gelu_tanh":
+        y = F.gelu(y, approximate="tanh")
+    elif act in ("swiglu", "geglu"):
         n = y.shape[-1]
         y4 = y.reshape(*y.shape[:-1], n // 32, 2, 16)
-        y = (F.silu(y4[..., 0, :]) * y4[..., 1, :]).reshape(*y.shape[:-1], n // 2)
+        g = F.silu(y4[..., 0, :]) if act == "swiglu" else F.gelu(y4[..., 0, :], approximate="tanh")
+        y = (g * y4[..., 1, :]).reshape(*y.shape[:-1], n // 2)
     if residual is not None:
         y = y + residual.float()
     return y.to(out_dtype or x.dtype)
@@ -295,6 +298,16 @@ def silu_mul(x):
 
 def gelu(x):
     return F.gelu(x.float()).to(x.dtype)
+
+
+def gelu_tanh(x):
+    return F.gelu(x.float(), approximate="tanh").to(x.dtype)
+
+
+def geglu_interleaved(x):
+    n = x.shape[-1]
+    x4 = x.float().reshape(*x.shape[:-1], n // 32, 2, 16)
+    return (F.gelu(x4[..., 0, :], approximate="tanh") * x4[..., 1, :]).reshape(*x.shape[:-1], n // 2).to(x.dtype)
 
 
 # ---------------------------------------------------------------------------------------------- fp8

@@ -20,8 +20,17 @@ def _rms(x, g, eps):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * g.float()).to(x.dtype)
 
 
-def _lin(x, w, lora: LoRAAdapter | None, layer: int, target: str):
+def _norm(model, x, name):
+    c, w = model.cfg, model.w
+    if c.norm == "layernorm":
+        return F.layer_norm(x.float(), (x.shape[-1],), w[name].float(), w[name + "_b"].float(), c.rms_eps).to(x.dtype)
+    return _rms(x, w[name], c.rms_eps)
+
+
+def _lin(x, w, lora: LoRAAdapter | None, layer: int, target: str, bias=None):
     y = x @ w.t()
+    if bias is not None:
+        y = y + bias
     if lora is not None:
         a = lora.params.get(f"l{layer}.{target}.A")
         if a is not None:
@@ -44,7 +53,10 @@ def lm_loss(model, lora: LoRAAdapter | None, ids: torch.Tensor, labels: torch.Te
     inside = (local >= 0) & (local < model.vocab_local)
     x = F.embedding(local.clamp(0, model.vocab_local - 1), w["embed"]) * inside[..., None].to(w["embed"].dtype)
     x = reduce_from_tp(x, ctx)
+    if c.embed_scale:
+        x = x * model.embed_multiplier
     cs = model.cos_sin[:S].to(x.device)
+    rank0 = ctx.tp_rank == 0
     cos, sin = cs[:, : hd // 2], cs[:, hd // 2:]
 
     def rope(t):  # [B, S, h, hd]
@@ -54,27 +66,35 @@ def lm_loss(model, lora: LoRAAdapter | None, ids: torch.Tensor, labels: torch.Te
 
     def block(x, i):
         p = f"l{i}."
-        h = copy_to_tp(_rms(x, w[p + "attn_norm"], c.rms_eps), ctx)
-        qkv = _lin(h, w[p + "qkv"], lora, i, "qkv")
+        h = copy_to_tp(_norm(model, x, p + "attn_norm"), ctx)
+        qkv = _lin(h, w[p + "qkv"], lora, i, "qkv", w.get(p + "qkv_b"))
         q, k, v = qkv.split([hq * hd, hkv * hd, hkv * hd], -1)
-        q, k = rope(q.view(B, S, hq, hd)), rope(k.view(B, S, hkv, hd))
+        q, k = q.view(B, S, hq, hd), k.view(B, S, hkv, hd)
+        if c.qk_norm:
+            q, k = _rms(q, w[p + "q_norm"], c.rms_eps), _rms(k, w[p + "k_norm"], c.rms_eps)
+        q, k = rope(q), rope(k)
         v = v.view(B, S, hkv, hd)
         a = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                            is_causal=True, enable_gqa=hq != hkv)
-        o = _lin(a.transpose(1, 2).reshape(B, S, hq * hd), w[p + "o"], lora, i, "o")
+        o = _lin(a.transpose(1, 2).reshape(B, S, hq * hd), w[p + "o"], lora, i, "o",
+                 w.get(p + "o_b") if rank0 else None)
         x = x + reduce_from_tp(o, ctx)
-        h = copy_to_tp(_rms(x, w[p + "mlp_norm"], c.rms_eps), ctx)
-        gu = _lin(h, w[p + "gate_up"], lora, i, "gate_up")
-        gu = gu.view(B, S, -1, 2, 16)
-        m = (F.silu(gu[..., 0, :].float()) * gu[..., 1, :].float()).to(x.dtype).reshape(B, S, -1)
-        return x + reduce_from_tp(_lin(m, w[p + "down"], lora, i, "down"), ctx)
+        h = copy_to_tp(_norm(model, x, p + "mlp_norm"), ctx)
+        if c.mlp == "gelu_tanh":
+            m = F.gelu(_lin(h, w[p + "fc"], lora, i, "fc", w.get(p + "fc_b")).float(), approximate="tanh").to(x.dtype)
+        else:
+            gu = _lin(h, w[p + "gate_up"], lora, i, "gate_up")
+            gu = gu.view(B, S, -1, 2, 16)
+            g = F.silu(gu[..., 0, :].float()) if c.mlp == "swiglu" else F.gelu(gu[..., 0, :].float(), approximate="tanh")
+            m = (g * gu[..., 1, :].float()).to(x.dtype).reshape(B, S, -1)
+        return x + reduce_from_tp(_lin(m, w[p + "down"], lora, i, "down", w.get(p + "down_b") if rank0 else None), ctx)
 
     for i in range(c.num_layers):
         if checkpoint:
             x = torch.utils.checkpoint.checkpoint(block, x, i, use_reentrant=False)
         else:
             x = block(x, i)
-    h = copy_to_tp(_rms(x, w["norm"], c.rms_eps), ctx)
+    h = copy_to_tp(_norm(model, x, "norm"), ctx)
     logits = gather_last(h @ w["lm_head"].t(), ctx)[..., : c.vocab_size].float()
     if not bool((labels[:, 1:] != -100).any()):  # nothing to learn in this micro-batch
         return logits.sum() * 0.0

@@ -14,7 +14,7 @@ DEFAULT_TARGETS = ("qkv", "o")
 class LoRAConfig:
     r: int = 16
     alpha: float = 32.0
-    targets: Tuple[str, ...] = DEFAULT_TARGETS  # subset of qkv, o, gate_up, down
+    targets: Tuple[str, ...] = DEFAULT_TARGETS  # subset of qkv, o, gate_up (or fc: non-gated MLP), down
     dropout: float = 0.0
 
     @property
@@ -53,7 +53,7 @@ class LoRAAdapter:
         out = []
         for k, v in self.params.items():
             t = k.split(".")[1]
-            if (k.endswith(".A") and t in ("qkv", "gate_up")) or (k.endswith(".B") and t in ("o", "down")):
+            if (k.endswith(".A") and t in ("qkv", "gate_up", "fc")) or (k.endswith(".B") and t in ("o", "down")):
                 out.append(v)
         return out
 
