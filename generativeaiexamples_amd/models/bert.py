@@ -194,6 +194,40 @@ class BertModel:
             self.w["cls_out_b"][: w.shape[0]].copy_(sd["classifier.bias"].to(self.dtype))
         return self
 
+    def _unpad_heads(self, t: torch.Tensor, rows: bool) -> torch.Tensor:
+        c = self.cfg
+        hd, hp, H = c.head_dim, c.head_dim_padded, c.num_heads
+        if hp == hd:
+            return t
+        if rows:
+            return t.reshape(3, H, hp, *t.shape[1:])[:, :, :hd].reshape(3 * H * hd, *t.shape[1:])
+        return t.reshape(t.shape[0], H, hp)[:, :, :hd].reshape(t.shape[0], H * hd)
+
+    def export_hf_state(self) -> Dict[str, torch.Tensor]:
+        """Inverse of :meth:`load_hf_state` (HF ``BertModel`` names, padded head dims removed)."""
+        c, w = self.cfg, self.w
+        sd = {"embeddings.word_embeddings.weight": w["word"], "embeddings.position_embeddings.weight": w["pos"],
+              "embeddings.token_type_embeddings.weight": w["type"], "embeddings.LayerNorm.weight": w["emb_ln_w"],
+              "embeddings.LayerNorm.bias": w["emb_ln_b"]}
+        D = c.hidden_size
+        for i in range(c.num_layers):
+            p, h = f"l{i}.", f"encoder.layer.{i}."
+            qkv, qkv_b = self._unpad_heads(w[p + "qkv"], True), self._unpad_heads(w[p + "qkv_b"], True)
+            for j, n in enumerate(("query", "key", "value")):
+                sd[h + f"attention.self.{n}.weight"] = qkv[j * D:(j + 1) * D]
+                sd[h + f"attention.self.{n}.bias"] = qkv_b[j * D:(j + 1) * D]
+            sd[h + "attention.output.dense.weight"] = self._unpad_heads(w[p + "o"], False)
+            sd[h + "attention.output.dense.bias"] = w[p + "o_b"]
+            sd[h + "attention.output.LayerNorm.weight"] = w[p + "ln1_w"]
+            sd[h + "attention.output.LayerNorm.bias"] = w[p + "ln1_b"]
+            sd[h + "intermediate.dense.weight"] = w[p + "up"]
+            sd[h + "intermediate.dense.bias"] = w[p + "up_b"]
+            sd[h + "output.dense.weight"] = w[p + "down"]
+            sd[h + "output.dense.bias"] = w[p + "down_b"]
+            sd[h + "output.LayerNorm.weight"] = w[p + "ln2_w"]
+            sd[h + "output.LayerNorm.bias"] = w[p + "ln2_b"]
+        return {k: v.detach().clone() for k, v in sd.items()}
+
     # ---------------------------------------------------------------------------- forward
     def encode_hidden(self, ids: torch.Tensor, cu_seqlens: torch.Tensor, seq_lens: List[int],
                       type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -192,3 +192,23 @@ def lora_dp_worker(rank, world, port, out_dir):
                 "launched": tr.bucketer.launched}, os.path.join(out_dir, f"lora_dp_{rank}.pt"))
     dist.barrier()
     os._exit(0)
+
+
+def embed_ft_dp_worker(rank, world, port, out_dir):
+    """DP=2 contrastive fine-tuning of a tiny encoder (gloo): replicas stay identical, loss falls."""
+    _init(rank, world, port, 1)
+    torch.manual_seed(0)
+    from generativeaiexamples_amd.engine.embedder import Embedder
+    from generativeaiexamples_amd.engine.tokenizer import bert_byte_tokenizer
+    from generativeaiexamples_amd.models.bert import BertConfig, BertModel
+    from generativeaiexamples_amd.training.embed_ft import EmbedFineTuner, EmbedFTConfig, synthetic_pairs
+
+    enc = BertModel(BertConfig.tiny(num_layers=1), device="cpu").random_init(rank)  # rank 0's weights broadcast
+    emb = Embedder(enc, bert_byte_tokenizer(2048))
+    cfg = EmbedFTConfig(global_batch=16, micro_batch=4, lr=2e-4, max_steps=6, gather_negatives=True, tau=0.05)
+    ft = EmbedFineTuner(emb, cfg, synthetic_pairs(64))
+    hist = ft.fit()
+    torch.save({"hist": torch.tensor(hist), "w": ft.w["l0.qkv"].detach().clone()},
+               os.path.join(out_dir, f"eft_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -20,3 +20,27 @@ def test_lora_sft_gpu_loss_falls(cuda):
     h = tr.train()
     assert all(x == x for x in h) and h[-1] < 0.5 * h[0]
     assert tr.lora.params["l0.qkv.A"].device.type == "cuda"
+
+
+def test_embed_finetune_on_gpu(cuda):
+    """Contrastive full-weight fine-tuning on the GPU (bf16 autocast), then the tuned weights serve through
+    the HIP encoder kernels and agree with the training forward."""
+    from generativeaiexamples_amd.engine.embedder import Embedder
+    from generativeaiexamples_amd.engine.tokenizer import bert_byte_tokenizer
+    from generativeaiexamples_amd.models.bert import BertConfig, BertModel
+    from generativeaiexamples_amd.training import embed_ft as E
+
+    torch.manual_seed(0)
+    enc = BertModel(BertConfig.tiny(num_layers=2), device=cuda).random_init(3)
+    emb = Embedder(enc, bert_byte_tokenizer(2048))
+    rows = E.synthetic_pairs(64)
+    before = E.recall_at_k(emb, rows[:32])
+    ft = E.EmbedFineTuner(emb, E.EmbedFTConfig(global_batch=16, micro_batch=8, lr=3e-4, max_steps=20, tau=0.05), rows)
+    hist = ft.fit()
+    assert sum(hist[-4:]) < sum(hist[:4])
+    assert E.recall_at_k(emb, rows[:32]) >= before
+    texts = ["query: w1 w2 w3", "passage: some passage text"]
+    with torch.no_grad():
+        train_side = ft._encode(texts, "passage").float()
+    serve_side = emb.embed(texts, "passage").float()
+    torch.testing.assert_close(train_side, serve_side, rtol=0, atol=5e-2)
