@@ -421,6 +421,8 @@ class LlamaModel:
         slots = getattr(fb, "lora_slots", None)
         if not self.lora_names or slots is None:
             return y
+        if slots.shape[0] < x.shape[0]:  # sequence-parallel padding rows use the base model
+            slots = torch.cat([slots, slots.new_zeros(x.shape[0] - slots.shape[0])])
         for s in range(1, len(self.lora_names) + 1):
             ab = self.lora_w.get((s, layer, target))
             if ab is None:
@@ -458,6 +460,8 @@ class LlamaModel:
 
     def forward(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
         """Returns fp32 logits [len(sample_rows), vocab] (gathered over TP)."""
+        if self.ctx.tp_size > 1 and self.ctx.sequence_parallel and fb.num_prefill_tokens > 0:
+            return self._forward_sp(fb, kv, decode_ws)
         c, w, ctx = self.cfg, self.w, self.ctx
         T, P = fb.num_tokens, fb.num_prefill_tokens
         hd = c.head_dim
@@ -500,6 +504,54 @@ class LlamaModel:
         x = self._norm(h, "norm", residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
         logits = ctx.tp_all_gather_last(logits)
+        return logits[:, : c.vocab_size]
+
+    def _forward_sp(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
+        """Tensor + sequence parallel forward for prefill / mixed steps: the residual stream
+        and the norms live on T/tp token rows per rank; every row-parallel output is reduce-scattered
+        and every column-parallel input all-gathered (tokens padded to a multiple of tp)."""
+        c, w, ctx = self.cfg, self.w, self.ctx
+        tp = ctx.tp_size
+        T, P = fb.num_tokens, fb.num_prefill_tokens
+        Tp = -(-T // tp) * tp
+        hd = c.head_dim
+        ids = fb.token_ids
+        if Tp > T:
+            ids = torch.cat([ids, ids.new_zeros(Tp - T)])
+        res = ctx.tp_reduce_scatter_rows(ops.embedding(ids, w["embed"], self.vstart, self.vstart + self.vocab_local))
+        if c.embed_scale:
+            res.mul_(self.embed_multiplier)
+        q = torch.empty(Tp, self.hq, hd, device=res.device, dtype=self.dtype)
+        attn = torch.zeros_like(q)
+        h = None
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
+            x = ctx.tp_all_gather_rows(x)
+            qkv = self._lora(ops.linear(x, w[p + "qkv"], bias=w.get(p + "qkv_b")), x, i, "qkv", fb)
+            if c.qk_norm:
+                self._qk_norm(qkv, p)
+            kc, vc = kv.layer(i)
+            ops.rope_kv_write(qkv[:T], fb.positions, self.cos_sin, fb.slots, q[:T], kc, vc, self.hq, self.hkv, hd,
+                              True)
+            ops.attention_prefill(q[:P], kc, vc, fb.prefill_block_tables, fb.cu_q, fb.prefill_ctx, self.scale,
+                                  True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P])
+            if T > P:
+                ops.attention_decode(q[P:T], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
+                                     max_ctx=fb.max_decode_ctx, out=attn[P:T])
+            a2 = attn.view(Tp, -1)
+            h = ctx.tp_reduce_scatter_rows(
+                self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb))
+            x = ctx.tp_all_gather_rows(self._norm(h, p + "mlp_norm", residual=res))
+            if c.mlp == "gelu_tanh":
+                g = self._lora(ops.linear(x, w[p + "fc"], bias=w.get(p + "fc_b"), act="gelu_tanh"), x, i, "fc", fb)
+            else:
+                g = ops.linear(x, w[p + "gate_up"], act=c.mlp)
+            h = ctx.tp_reduce_scatter_rows(ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b")))
+        x = ctx.tp_all_gather_rows(self._norm(h, "norm", residual=res))[:T]
+        if fb.sample_rows is not None:
+            x = x.index_select(0, fb.sample_rows)
+        logits = ctx.tp_all_gather_last(ops.linear(x, w["lm_head"], out_dtype=torch.float32))
         return logits[:, : c.vocab_size]
 
     # ------------------------------------------------------------------ reference

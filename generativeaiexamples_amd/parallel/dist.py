@@ -33,6 +33,11 @@ class DistContext:
     tp_group: Optional[object] = None
     dp_group: Optional[object] = None
     world_group: Optional[object] = None
+    # Megatron-style sequence parallelism inside the TP group: between the row-parallel and
+    # the next column-parallel GEMM the activations stay sharded along tokens, each all-reduce becomes a
+    # reduce-scatter + all-gather pair (same bytes on the xGMI ring) and the residual adds / norms run on
+    # T / tp rows per rank.
+    sequence_parallel: bool = False
 
     @property
     def tp_rank(self) -> int:
@@ -67,6 +72,33 @@ class DistContext:
             dist.all_gather(parts, t.contiguous(), group=self.tp_group)
         return torch.cat(parts, dim=-1)
 
+    def tp_reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Partial sums [T, D] (T divisible by tp) -> this rank's summed rows [T / tp, D]."""
+        if self.tp_size == 1:
+            return t
+        n = t.shape[0] // self.tp_size
+        with guard("tp_reduce_scatter", self.rank):
+            if t.is_cuda:
+                out = torch.empty(n, *t.shape[1:], dtype=t.dtype, device=t.device)
+                dist.reduce_scatter_tensor(out, t.contiguous(), group=self.tp_group)
+                return out
+            f = t.float()  # gloo has no reduce-scatter: all-reduce + keep the local slice
+            dist.all_reduce(f, group=self.tp_group)
+            return f[self.tp_rank * n:(self.tp_rank + 1) * n].to(t.dtype).contiguous()
+
+    def tp_all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Row shards [T / tp, D] -> [T, D] in TP-rank order."""
+        if self.tp_size == 1:
+            return t
+        with guard("tp_all_gather_rows", self.rank):
+            if t.is_cuda:
+                out = torch.empty(t.shape[0] * self.tp_size, *t.shape[1:], dtype=t.dtype, device=t.device)
+                dist.all_gather_into_tensor(out, t.contiguous(), group=self.tp_group)
+                return out
+            parts = [torch.empty_like(t) for _ in range(self.tp_size)]
+            dist.all_gather(parts, t.contiguous(), group=self.tp_group)
+            return torch.cat(parts)
+
     def all_gather_obj(self, obj, group=None):
         if not self.is_distributed:
             return [obj]
@@ -96,7 +128,8 @@ def get_context() -> DistContext:
     return _CTX
 
 
-def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int | None = None) -> DistContext:
+def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: int | None = None,
+                     sequence_parallel: bool | None = None) -> DistContext:
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 
     Falls back to a single-process context when WORLD_SIZE is unset or 1.
@@ -112,6 +145,9 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
     if backend is None:
         backend = os.environ.get("GAI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend if world > 1 else "none")
+    if sequence_parallel is None:
+        sequence_parallel = os.environ.get("GAI_SEQUENCE_PARALLEL") == "1"
+    ctx.sequence_parallel = bool(sequence_parallel)
     if use_gpu:
         # GAI_SINGLE_DEVICE=1: every rank on cuda:0 (gloo rehearsal of a multi-rank run on one GPU)
         dev_idx = 0 if os.environ.get("GAI_SINGLE_DEVICE") == "1" else local

@@ -212,3 +212,40 @@ def embed_ft_dp_worker(rank, world, port, out_dir):
                os.path.join(out_dir, f"eft_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def tp_sp_worker(rank, world, port, out_dir):
+    """TP=2 with sequence parallelism (reduce-scatter / all-gather) == TP=2 all-reduce == TP=1, on a mixed
+    prefill + decode batch whose token count is not a multiple of tp."""
+    ctx = _init(rank, world, port, world)
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+
+    outs = {}
+    for name, kw in (("llama", {}), ("starcoder2", dict(arch="starcoder2", norm="layernorm", mlp="gelu_tanh",
+                                                        qkv_bias=True, o_bias=True, mlp_bias=True))):
+        cfg = LlamaConfig.tiny(num_heads=4, num_kv_heads=2, vocab_size=512, **kw)
+        ref = LlamaModel(cfg, device="cpu", dist_ctx=DistContext()).random_init(9)
+        sd = ref.export_hf_state()
+        m = LlamaModel(cfg, device="cpu", dist_ctx=ctx).load_hf_state(sd)
+        tok = small_byte_tokenizer(512)
+        res = {}
+        for mode in ("ref", "tp", "sp"):
+            model = ref if mode == "ref" else m
+            ctx.sequence_parallel = mode == "sp"
+            eng = LLMEngine(model, tok, EngineConfig(num_blocks=64, max_model_len=256, use_graphs=False,
+                                                     decode_steps=1))
+            first = eng.add_request(list(range(5, 16)), SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+            eng.step()  # prefill of the first request
+            eng.add_request(list(range(7, 7 + 26)), SamplingParams(temperature=0.0, max_tokens=1))
+            b = eng.sched.schedule()  # 1 decode token + 26 prefill tokens = 27 (odd)
+            fb, _ = eng._make_batch(b)
+            res[mode] = model.forward(fb, eng.kv).float()
+            del first
+        ctx.sequence_parallel = False
+        outs[name] = res
+    torch.save(outs, os.path.join(out_dir, f"sp_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
