@@ -1,7 +1,7 @@
 """In-tree build of the native extensions (gfx950 only).
 
 Produces, next to this file:
-  * ``_C.so``  - HIP kernels (``csrc/kernels/*.hip``, hipcc --offload-arch=gfx950)
+  * ``_C.so``  - HIP kernels (``csrc/kernels/*.hip``, ``csrc/comm/*.hip``, hipcc --offload-arch=gfx950)
                  + PyTorch bindings (``csrc/bindings/*.cpp``).
   * ``_rt.so`` - the host runtime (``csrc/runtime/*.cpp``): paged-KV block
                  manager, continuous-batching scheduler core, BPE/byte tokenizer
@@ -100,7 +100,7 @@ def build_c(jobs: int = 8, force: bool = False, verbose: bool = False) -> Path:
                  "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations",
                  *[f"-I{p}" for p in inc]]
     todo, objs = [], []
-    for s in sorted((CSRC / "kernels").glob("*.hip")):
+    for s in sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "comm").glob("*.hip")):
         o = BUILD / (s.stem + ".hip.o")
         objs.append(o)
         if force or _needs(o, s, hdr):

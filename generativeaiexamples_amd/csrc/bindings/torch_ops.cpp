@@ -383,6 +383,29 @@ void geglu_interleaved(const Tensor& x, Tensor& y) {
   gai_geglu_interleaved(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
 }
 
+void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
+                      const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
+                      int64_t slot_bytes) {
+  check_dev(inp, "inp");
+  check_dev(out, "out");
+  TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.numel() == out.numel(), "custom_allreduce: in/out mismatch");
+  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "custom_allreduce: bf16 or fp32");
+  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= GAI_AR_MAX_BLOCKS, "custom_allreduce: counters");
+  check_i32(err, "err");
+  const int world = (int)data_ptrs.size();
+  TORCH_CHECK(world >= 2 && world <= GAI_AR_MAX_WORLD && (int)sig_ptrs.size() == world, "custom_allreduce: world");
+  TORCH_CHECK(rank >= 0 && rank < world, "custom_allreduce: rank");
+  void* d[GAI_AR_MAX_WORLD];
+  uint32_t* s[GAI_AR_MAX_WORLD];
+  for (int q = 0; q < world; ++q) {
+    d[q] = reinterpret_cast<void*>(data_ptrs[q]);
+    s[q] = reinterpret_cast<uint32_t*>(sig_ptrs[q]);
+  }
+  gai_custom_allreduce(inp.data_ptr(), out.data_ptr(), inp.numel() * inp.element_size(),
+                       inp.scalar_type() == at::kFloat, d, s, reinterpret_cast<uint32_t*>(counters.data_ptr()),
+                       (int)rank, world, slot_bytes, err.data_ptr<int>(), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -417,5 +440,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_tanh", &gelu_tanh);
   m.def("geglu_interleaved", &geglu_interleaved);
   m.def("silu_mul_interleaved", &silu_mul_interleaved);
+  m.def("custom_allreduce", &custom_allreduce);
+  m.def("ipc_malloc", [](int64_t bytes) { return reinterpret_cast<int64_t>(gai_ipc_malloc(bytes)); });
+  m.def("ipc_free", [](int64_t p) { gai_ipc_free(reinterpret_cast<void*>(p)); });
+  m.def("ipc_get_handle", [](int64_t p) {
+    char h[64] = {0};
+    gai_ipc_get_handle(reinterpret_cast<void*>(p), h);
+    return pybind11::bytes(h, 64);
+  });
+  m.def("ipc_open", [](pybind11::bytes h) {
+    std::string b = h;
+    TORCH_CHECK(b.size() == 64, "ipc_open: handle must be 64 bytes");
+    return reinterpret_cast<int64_t>(gai_ipc_open(b.data()));
+  });
+  m.def("ipc_close", [](int64_t p) { gai_ipc_close(reinterpret_cast<void*>(p)); });
+  m.attr("AR_CHUNK") = GAI_AR_CHUNK;
+  m.attr("AR_MAX_BLOCKS") = GAI_AR_MAX_BLOCKS;
   m.attr("ARCH") = "gfx950";
 }

@@ -1,0 +1,187 @@
+// One-shot peer-memory all-reduce over xGMI (SURVEY §2.4 D1 / P1, §5.8 "small messages").
+//
+// Decode-time TP all-reduces are latency bound (Llama-3-70B TP8, batch 64: 1 MiB, 160 per token).
+// A ring all-reduce crosses N-1 hops in sequence; on a fully connected xGMI mesh every rank can
+// instead push its whole input to all N-1 peers at once (one link each, concurrently) and reduce
+// locally: one hop of latency.
+//
+// Memory (per rank, allocated uncached so no L2 of any GPU holds a stale copy, IPC-exported):
+//   data  [2 parity][W src][slot_bytes]   peers write their contribution into slot `src`
+//   sig   [kArMaxBlocks][8] uint32         peer `src` stores the epoch of block b into sig[b][src]
+// plus a local, never shared, uint32 counter per block that carries the epoch between launches, so
+// the launch has no per-call scalar argument and replays correctly from a captured HIP graph.
+//
+// Block b owns the fixed byte range [b * kArChunk, (b + 1) * kArChunk) of every call. Per call:
+//   1. e = ++counter[b]; parity p = e & 1
+//   2. push own chunk to data_q[p][rank] of every peer q (16-B stores, remote for q != rank)
+//   3. s_waitcnt vmcnt(0) in every wave, barrier, then lane q stores sig_q[b][rank] = e (system scope)
+//   4. lanes 0..W-1 poll the local sig[b][q] until it equals e (bounded: a timeout sets *err and the
+//      block proceeds, so a broken peer can never hang the GPU), barrier
+//   5. out chunk = sum_q data_local[p][q] (fp32 accumulate in peer order 0..W-1: every rank computes
+//      bit-identical results)
+// Reuse of parity p at call e+2 is safe without a closing barrier: a peer's block b can only reach
+// e+2 after seeing our signal for e+1, which we send after finishing our reads of call e (same
+// stream, kernels serialised). Flags only ever hold e-1 or e while we wait for e (a peer cannot run
+// ahead of our own signal), so the equality test is wrap-safe.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gai_common.h"
+#include "gai_kernels.h"
+
+namespace {
+
+constexpr int kArThreads = 256;
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void acc_bf16x8(float (&a)[8], const uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[2 * i] += __uint_as_float(w[i] << 16);
+    a[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  // round-to-nearest-even, NaN kept quiet
+  auto rn = [](float f) -> uint32_t {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+  };
+  return rn(lo) | (rn(hi) << 16);
+}
+
+struct ArPtrs {
+  char* data[GAI_AR_MAX_WORLD];
+  uint32_t* sig[GAI_AR_MAX_WORLD];
+};
+
+template <int W, bool F32>
+__global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in, uint4* out,
+                                                                ArPtrs p, uint32_t* __restrict__ counters, int rank,
+                                                                int64_t n16, int64_t slot_bytes, int* err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t e_sh;
+  if (tid == 0) e_sh = counters[b] + 1u;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int par = (int)(e & 1u);
+  constexpr int64_t kVec = GAI_AR_CHUNK / 16;
+  const int64_t v0 = (int64_t)b * kVec, v1 = min(v0 + kVec, n16);
+  const int64_t my_off = ((int64_t)par * W + rank) * slot_bytes;
+
+  // 2. push
+  for (int64_t v = v0 + tid; v < v1; v += kArThreads) {
+    const uint4 x = in[v];
+#pragma unroll
+    for (int q = 0; q < W; ++q) reinterpret_cast<uint4*>(p.data[q] + my_off)[v] = x;
+  }
+  // 3. drain this wave's stores, join the workgroup, signal every peer
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (tid < W) __hip_atomic_store(p.sig[tid] + b * GAI_AR_MAX_WORLD + rank, e, __ATOMIC_RELEASE,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+  // 4. wait for every peer's chunk
+  if (tid < W) {
+    uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {  // ~seconds: a peer died or diverged; never hang the GPU
+        atomicOr(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // 5. reduce the W local slots in rank order
+  const char* base = p.data[rank] + (int64_t)par * W * slot_bytes;
+  for (int64_t v = v0 + tid; v < v1; v += kArThreads) {
+    if (F32) {
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const uint4 x = reinterpret_cast<const uint4*>(base + q * slot_bytes)[v];
+        s += f32x4_t{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+      }
+      out[v] = uint4{__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
+    } else {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) acc_bf16x8(a, reinterpret_cast<const uint4*>(base + q * slot_bytes)[v]);
+      out[v] = uint4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]),
+                     pack_bf16x2(a[6], a[7])};
+    }
+  }
+  if (tid == 0) counters[b] = e;
+}
+
+}  // namespace
+
+void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
+                          uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
+                          int* err, hipStream_t st) {
+  if (bytes == 0) return;
+  if (bytes % 16 || bytes > slot_bytes) gai_launch_error(__FILE__, __LINE__, "custom_allreduce: bad message size");
+  const int64_t nblk = (bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
+  if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "custom_allreduce: message too large");
+  ArPtrs p{};
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = static_cast<char*>(peer_data[q]);
+    p.sig[q] = peer_sig[q];
+  }
+  const int64_t n16 = bytes / 16;
+#define GAI_AR(WW)                                                                                            \
+  if (world == WW) {                                                                                          \
+    if (f32)                                                                                                  \
+      ar_oneshot_kernel<WW, true><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p, counters, \
+                                                                    rank, n16, slot_bytes, err);              \
+    else                                                                                                      \
+      ar_oneshot_kernel<WW, false><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p,          \
+                                                                     counters, rank, n16, slot_bytes, err);   \
+    GAI_LAUNCH_CHECK();                                                                                       \
+    return;                                                                                                   \
+  }
+  GAI_AR(2)
+  GAI_AR(4)
+  GAI_AR(8)
+  GAI_AR(3)
+  GAI_AR(5)
+  GAI_AR(6)
+  GAI_AR(7)
+#undef GAI_AR
+  gai_launch_error(__FILE__, __LINE__, "custom_allreduce: world size must be 2..8");
+}
+
+// --- IPC buffer management (host) ---------------------------------------------------------------
+void* gai_ipc_malloc(int64_t bytes) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess)
+    gai_launch_error(__FILE__, __LINE__, "ipc_malloc: hipExtMallocWithFlags(uncached) failed");
+  if (hipMemset(p, 0, bytes) != hipSuccess) gai_launch_error(__FILE__, __LINE__, "ipc_malloc: memset failed");
+  if (hipDeviceSynchronize() != hipSuccess) gai_launch_error(__FILE__, __LINE__, "ipc_malloc: sync failed");
+  return p;
+}
+
+void gai_ipc_free(void* p) { (void)hipFree(p); }
+
+void gai_ipc_get_handle(void* p, char* handle64) {
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, p) != hipSuccess) gai_launch_error(__FILE__, __LINE__, "hipIpcGetMemHandle failed");
+  static_assert(sizeof(h) <= 64, "ipc handle size");
+  for (size_t i = 0; i < sizeof(h); ++i) handle64[i] = reinterpret_cast<const char*>(&h)[i];
+}
+
+void* gai_ipc_open(const char* handle64) {
+  hipIpcMemHandle_t h;
+  for (size_t i = 0; i < sizeof(h); ++i) reinterpret_cast<char*>(&h)[i] = handle64[i];
+  void* p = nullptr;
+  if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+    gai_launch_error(__FILE__, __LINE__, "hipIpcOpenMemHandle failed");
+  return p;
+}
+
+void gai_ipc_close(void* p) { (void)hipIpcCloseMemHandle(p); }

@@ -75,3 +75,16 @@ void gai_patchify(const float* img, int B, int C, int H, int W, int P, int Kp, c
                   const float* inv_std, void* out, hipStream_t st);
 void gai_vit_embed(const void* patches, const void* cls, const void* pos, void* out, int B, int NP, int D,
                    hipStream_t st);
+
+// comm/custom_ar.hip (one-shot peer-memory all-reduce; buffers from gai_ipc_malloc, uncached)
+#define GAI_AR_MAX_WORLD 8
+#define GAI_AR_CHUNK 16384
+#define GAI_AR_MAX_BLOCKS 512
+void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
+                          uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
+                          int* err, hipStream_t st);
+void* gai_ipc_malloc(int64_t bytes);
+void gai_ipc_free(void* p);
+void gai_ipc_get_handle(void* p, char* handle64);
+void* gai_ipc_open(const char* handle64);
+void gai_ipc_close(void* p);

@@ -1,0 +1,107 @@
+"""One-shot peer-memory all-reduce for latency-bound TP messages.
+
+RCCL's ring all-reduce crosses ``world - 1`` hops one after another. On the fully connected xGMI
+mesh of an MI355X node every rank can push its whole input to all peers concurrently (one link
+each) and reduce locally, so a decode-size message (Llama-3-70B TP8, batch 64: 1 MiB per
+all-reduce, 160 per token) costs one hop. The kernel is ``csrc/comm/custom_ar.hip``; this module
+owns the IPC buffers:
+
+* every rank allocates (uncached, so no GPU's L2 keeps a stale line) a data area of
+  ``2 parity x world x max_bytes`` and a signal area, exports both with ``hipIpcGetMemHandle``;
+* handles are exchanged with one ``all_gather_object`` on the TP group (works over RCCL or gloo);
+* every rank maps its peers' areas (``hipIpcOpenMemHandle``).
+
+The launch takes no per-call scalar (epochs live in a device counter per workgroup), so it is
+captured into the decode HIP graph like any other kernel. Messages larger than ``max_bytes`` or not
+a multiple of 16 bytes go to RCCL. A peer that never arrives makes the kernel give up after a
+bounded spin and set an error word (checked by :meth:`check`), never hang the GPU.
+
+Reference parity: the reference has no in-repo collective (NCCL is implicit inside TRT-LLM,
+SURVEY §2.4 P1); this is the "custom one-shot xGMI all-reduce for <= 1 MiB" of its MI355X design.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _native():
+    from .. import ops
+
+    return ops.native()
+
+
+class CustomAllReduce:
+    """Peer-memory all-reduce over one process group. All ranks must construct it together."""
+
+    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 8 << 20):
+        C = _native()
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if not 2 <= self.world <= 8:
+            raise ValueError("CustomAllReduce supports 2..8 ranks")
+        max_bytes = min(int(max_bytes), C.AR_CHUNK * C.AR_MAX_BLOCKS)
+        self.max_bytes = max_bytes - max_bytes % C.AR_CHUNK
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(self.device):
+            self._data = C.ipc_malloc(2 * self.world * self.max_bytes)
+            self._sig = C.ipc_malloc(C.AR_MAX_BLOCKS * 8 * 4)
+            handles = (C.ipc_get_handle(self._data), C.ipc_get_handle(self._sig))
+            allh: List = [None] * self.world
+            dist.all_gather_object(allh, handles, group=group)
+            self._opened: List[int] = []
+            self.data_ptrs, self.sig_ptrs = [], []
+            for q, (hd, hs) in enumerate(allh):
+                if q == self.rank:
+                    self.data_ptrs.append(self._data)
+                    self.sig_ptrs.append(self._sig)
+                else:
+                    pd, ps = C.ipc_open(hd), C.ipc_open(hs)
+                    self._opened += [pd, ps]
+                    self.data_ptrs.append(pd)
+                    self.sig_ptrs.append(ps)
+            self.counters = torch.zeros(C.AR_MAX_BLOCKS, dtype=torch.int32, device=self.device)
+            self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)  # every peer has mapped every buffer before the first launch
+        self._closed = False
+
+    def eligible(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return (not self._closed and t.is_cuda and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32)
+                and 0 < nbytes <= self.max_bytes and nbytes % 16 == 0)
+
+    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Sum ``t`` over the group (in place unless ``out`` is given). Graph-capturable."""
+        out = t if out is None else out
+        _native().custom_allreduce(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
+                                   self.max_bytes)
+        return out
+
+    def check(self) -> None:
+        """Raise if a launch timed out waiting for a peer (host sync)."""
+        if int(self.err.item()):
+            raise RuntimeError("custom all-reduce: a peer did not arrive (timed out); results are invalid")
+
+    def close(self) -> None:
+        if self._closed:
+            return
+        C = _native()
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            C.ipc_close(p)
+        C.ipc_free(self._data)
+        C.ipc_free(self._sig)
+        self._closed = True
+
+
+def maybe_create(group, world: int, device: torch.device) -> Optional[CustomAllReduce]:
+    """The TP group's custom all-reduce, or None (CPU, one rank, GAI_CUSTOM_AR=0, or setup failure)."""
+    if world < 2 or world > 8 or device.type != "cuda" or os.environ.get("GAI_CUSTOM_AR", "1") == "0":
+        return None
+    mb = int(os.environ.get("GAI_CUSTOM_AR_MAX_MB", "8"))
+    return CustomAllReduce(group, device, max_bytes=mb << 20)

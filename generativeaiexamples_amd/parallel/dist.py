@@ -38,6 +38,8 @@ class DistContext:
     # reduce-scatter + all-gather pair (same bytes on the xGMI ring) and the residual adds / norms run on
     # T / tp rows per rank.
     sequence_parallel: bool = False
+    # one-shot peer-memory all-reduce for TP messages <= GAI_CUSTOM_AR_MAX_MB (parallel/custom_ar.py)
+    custom_ar: Optional[object] = None
 
     @property
     def tp_rank(self) -> int:
@@ -54,6 +56,9 @@ class DistContext:
     # ---------------- collectives (no-ops when the group has one member) ----------------
     def tp_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
+            car = self.custom_ar
+            if car is not None and car.eligible(t):  # latency-bound sizes: one-shot xGMI push
+                return car.all_reduce(t)
             with guard("tp_all_reduce", self.rank):
                 if t.is_cuda or t.dtype in (torch.float32, torch.float64):
                     dist.all_reduce(t, group=self.tp_group)
@@ -174,12 +179,20 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
             g = dist.new_group(ranks) if ctx.dp_size > 1 else None
             if rank in ranks:
                 ctx.dp_group = g
+        want_car = os.environ.get("GAI_CUSTOM_AR", "1" if backend == "nccl" else "0") == "1"
+        if tp_size > 1 and use_gpu and want_car:
+            from .custom_ar import maybe_create
+
+            ctx.custom_ar = maybe_create(ctx.tp_group, tp_size, ctx.device)
     _CTX = ctx
     return ctx
 
 
 def shutdown():
     global _CTX
+    if _CTX is not None and _CTX.custom_ar is not None:
+        _CTX.custom_ar.close()
+        _CTX.custom_ar = None
     if dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

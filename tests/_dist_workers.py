@@ -249,3 +249,86 @@ def tp_sp_worker(rank, world, port, out_dir):
     torch.save(outs, os.path.join(out_dir, f"sp_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def custom_ar_worker(rank, world, port, out_dir):
+    """Every rank on cuda:0 (one-GPU box), gloo for the handle exchange: the one-shot peer-memory
+    all-reduce must equal the fp32 sum of every rank's input, eagerly (bf16 + fp32, in/out of
+    place, sizes across chunk boundaries, repeated calls over both parities) and from a captured
+    HIP graph replayed with new inputs. Writes one status line per rank."""
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from generativeaiexamples_amd.parallel.custom_ar import CustomAllReduce
+
+    car = CustomAllReduce(None, dev, max_bytes=4 << 20)
+    errs = []
+
+    def inputs(n, dtype, seed):
+        g = torch.Generator().manual_seed(seed)
+        xs = [torch.randn(n, generator=g).to(dtype) for _ in range(world)]
+        ref = torch.stack([x.float() for x in xs]).sum(0)
+        return xs[rank].to(dev), ref
+
+    sizes = [8, 64, 2048, 8192, 8200, 65536 + 8, 524288, (4 << 20) // 2]  # elements (bf16)
+    for it, n in enumerate(sizes * 2):  # twice: both buffer parities per block
+        for dtype in (torch.bfloat16, torch.float32):
+            if n * (2 if dtype == torch.bfloat16 else 4) > car.max_bytes:
+                continue
+            x, ref = inputs(n, dtype, 100 * it + (dtype == torch.float32))
+            if it % 2:
+                y = car.all_reduce(x)  # in place
+            else:
+                y = torch.empty_like(x)
+                car.all_reduce(x, y)
+            torch.cuda.synchronize()
+            tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+            e = (y.float().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+            if not e < tol:
+                errs.append(f"n={n} {dtype} rel err {e}")
+    # graph capture: three chained all-reduces on static buffers, replayed with new inputs
+    n = 64 * 4096
+    static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        car.all_reduce(static)  # warm (also advances the epoch counters identically on every rank)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        car.all_reduce(static)
+        static.mul_(0.5)
+        car.all_reduce(static)
+    for rep in range(4):
+        x, ref = inputs(n, torch.bfloat16, 7000 + rep)
+        static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        want = ref * 0.5 * world
+        e = (static.float().cpu() - want).abs().max().item() / (want.abs().max().item() + 1e-6)
+        if not e < 3e-2:
+            errs.append(f"graph replay {rep} rel err {e}")
+    car.check()
+    # rough latency (on a shared single GPU: all ranks time-slice one device)
+    t = torch.zeros(64 * 8192, dtype=torch.bfloat16, device=dev)
+    for _ in range(5):
+        car.all_reduce(t)
+    torch.cuda.synchronize()
+    dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(50):
+        car.all_reduce(t)
+    ev1.record()
+    torch.cuda.synchronize()
+    us = ev0.elapsed_time(ev1) * 1000 / 50
+    car.check()
+    dist.barrier()
+    car.close()
+    with open(os.path.join(out_dir, f"car_{rank}.json"), "w") as f:
+        json.dump({"errors": errs, "us_1MiB": us}, f)
+    dist.destroy_process_group()

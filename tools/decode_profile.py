@@ -53,8 +53,8 @@ def main():
     def sample(*args, **kw):
         t = time.perf_counter(); r = orig_sample(*args, **kw); acc["sample"] += time.perf_counter() - t; return r  # noqa: E702
 
-    def process(*args):
-        t = time.perf_counter(); r = orig_process(*args); acc["process"] += time.perf_counter() - t; return r  # noqa: E702
+    def process(*args, **kw):
+        t = time.perf_counter(); r = orig_process(*args, **kw); acc["process"] += time.perf_counter() - t; return r  # noqa: E702
 
     class S:  # proxy scheduler
         def __getattr__(self, k):
