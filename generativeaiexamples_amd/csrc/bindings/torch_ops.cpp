@@ -107,7 +107,7 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                   const Tensor& tiles, const Tensor& cu_q, const Tensor& ctx_lens, Tensor& out, int64_t Hq,
-                  int64_t Hkv, double scale, bool causal) {
+                  int64_t Hkv, double scale, bool causal, const optional<Tensor>& lse) {
   check_bf16(q, "q");
   check_bf16(k_cache, "k_cache");
   check_bf16(v_cache, "v_cache");
@@ -117,9 +117,16 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   check_i32(ctx_lens, "ctx_lens");
   check_bf16(out, "out");
   const int D = q.size(-1);
+  float* lse_p = nullptr;
+  if (lse) {
+    check_f32(*lse, "lse");
+    TORCH_CHECK(lse->numel() == q.numel() / D, "attn_prefill: lse must be [T, Hq]");
+    lse_p = lse->data_ptr<float>();
+  }
   gai_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                    block_tables.size(1), tiles.data_ptr<int>(), tiles.numel() / 2, cu_q.data_ptr<int>(),
-                   ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, cur_stream());
+                   ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, lse_p,
+                   cur_stream());
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,

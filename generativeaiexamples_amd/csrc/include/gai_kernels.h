@@ -35,7 +35,7 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
-                      int Hq, int Hkv, int D, float scale, int causal, hipStream_t st);
+                      int Hq, int Hkv, int D, float scale, int causal, float* lse, hipStream_t st);
 int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,

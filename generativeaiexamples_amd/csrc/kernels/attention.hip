@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
-    float scale, int causal) {
+    float scale, int causal, float* __restrict__ lse) {
   using Cfg = PrefillCfg<D>;
   constexpr int RPW = 4 / HPW;  // row groups per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -211,13 +211,16 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc_o[dt][4 * c + r] * inv);
         *reinterpret_cast<bf16x4_t*>(op + 32 * dt + 8 * c + 4 * h) = o;
       }
+    // natural-log softmax normaliser per (row, head): merges partial results (ring attention)
+    if (lse != nullptr && h == 0)
+      lse[(size_t)(qbeg + qrow) * Hq + head] = l_run > 0.f ? (m_run + __log2f(l_run)) * 0.69314718055994531f : kNeg;
   }
 }
 
 // ----------------------------------------------------------------------------------------------
 // Decode
 // ----------------------------------------------------------------------------------------------
-template <int D, bool PIPE>
+template <int D, bool PIPE, int H, bool V16>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
@@ -250,66 +253,92 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   float m_run = kNeg, l_run = 0.f;
   const float sl2 = scale * kLog2e;
 
-  // K/V of one 32-key chunk (2 pages) per wave: K rows for the QK^T MFMA (lane: key lane&15, 16 B of
-  // dims 32t + 8gq) and the V^T columns for the PV MFMA. Software-pipelined one chunk ahead with a
-  // register double buffer: the next chunk's loads are in flight while this chunk's MFMAs / softmax run.
+  // A wave step covers H halves of 32 keys (2 pages each). Per half: K rows for the QK^T MFMA (lane:
+  // key row lane&15, 16 B of dims 32t + 8gq) and V^T columns for the PV MFMA.
+  //  * V16 = false: S row m of MFMA i is key 16i + m; P^T's k order is then {4gq..4gq+3, 16+4gq..+3}
+  //    and V^T is read as two 8-B pieces (one per page).
+  //  * V16 = true: row m of MFMA i is key 8(m>>2) + 4i + (m&3), so lane group gq ends up holding the
+  //    8 CONSECUTIVE keys 8gq..8gq+7 of P^T, and its V^T operand is one 16-B load (page gq>>1, keys
+  //    8(gq&1)..+7): half the V load instructions.
   // Addresses of a chunk past the split are clamped to its last page (unconditional loads: a
-  // data-dependent branch around them would force vmcnt(0) waits), and such a chunk is never computed.
+  // data-dependent branch around them would force vmcnt(0) waits), and such keys are masked.
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
   struct Chunk {
-    bf16x8 k[2][D / 32];
-    bf16x4_t vlo[D / 16], vhi[D / 16];
+    bf16x8 k[H][2][D / 32];
+    bf16x4_t vlo[H][V16 ? 1 : D / 16], vhi[H][V16 ? 1 : D / 16];
+    bf16x8 v8[H][V16 ? D / 16 : 1];
   };
   const int last_page = (kend - 1) / kBS;
   auto load_chunk = [&](int kb, Chunk& c) {
-    const int p0 = min(kb / kBS, last_page);
-    const int blk0 = bt[p0];
-    const int blk1 = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : blk0;
-    const size_t pb0 = ((size_t)blk0 * Hkv + g) * kBS * D, pb1 = ((size_t)blk1 * Hkv + g) * kBS * D;
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      c.k[0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
-      c.k[1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
-    }
+    for (int h = 0; h < H; ++h) {
+      const int p0 = min(kb / kBS + 2 * h, last_page);
+      const int blk0 = bt[p0];
+      const int blk1 = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : blk0;
+      const size_t pb0 = ((size_t)blk0 * Hkv + g) * kBS * D, pb1 = ((size_t)blk1 * Hkv + g) * kBS * D;
+      if (V16) {
+        const int m = lane & 15;
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      const size_t off = (size_t)(16 * dt + (lane & 15)) * kBS + 4 * gq;
-      c.vlo[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
-      c.vhi[dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
+        for (int i = 0; i < 2; ++i) {
+          const int key = 8 * (m >> 2) + 4 * i + (m & 3);  // 0..31 inside the half
+          const size_t pb = key < 16 ? pb0 : pb1;
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t) c.k[h][i][t] = load8(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
+        }
+        const size_t pbv = gq < 2 ? pb0 : pb1;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt)
+          c.v8[h][dt] = load8(vc + pbv + (size_t)(16 * dt + (lane & 15)) * kBS + 8 * (gq & 1));
+      } else {
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          c.k[h][0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+          c.k[h][1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+        }
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt) {
+          const size_t off = (size_t)(16 * dt + (lane & 15)) * kBS + 4 * gq;
+          c.vlo[h][dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
+          c.vhi[h][dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
+        }
+      }
     }
   };
   auto compute_chunk = [&](int kb, const Chunk& c) {
-    f32x4 s[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      s[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) s[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[i][t], qf[t], s[i], 0, 0, 0);
-    }
+    f32x4 s[H][2];
     float mt = kNeg;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb + 16 * i + 4 * gq + r;
-        const float x = key < kend ? s[i][r] * sl2 : kNeg;
-        s[i][r] = x;
-        mt = fmaxf(mt, x);
+      for (int i = 0; i < 2; ++i) {
+        s[h][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t)
+          s[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[h][i][t], qf[t], s[h][i], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb + 32 * h + (V16 ? 8 * gq + 4 * i + r : 16 * i + 4 * gq + r);
+          const float x = key < kend ? s[h][i][r] * sl2 : kNeg;
+          s[h][i][r] = x;
+          mt = fmaxf(mt, x);
+        }
       }
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = exp2f(m_run - m_new);
     float rs = 0.f;
-    bf16x8 pf;
+    bf16x8 pf[H];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(s[i][r] - m_new);
-        rs += pv;
-        pf[4 * i + r] = (bf16)pv;
-      }
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(s[h][i][r] - m_new);
+          rs += pv;
+          pf[h][4 * i + r] = (bf16)pv;
+        }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
@@ -317,30 +346,39 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       acc_o[dt] *= alpha;
-      const bf16x8 vf = {c.vlo[dt][0], c.vlo[dt][1], c.vlo[dt][2], c.vlo[dt][3],
-                         c.vhi[dt][0], c.vhi[dt][1], c.vhi[dt][2], c.vhi[dt][3]};
-      acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, acc_o[dt], 0, 0, 0);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        bf16x8 vf;
+        if (V16) {
+          vf = c.v8[h][dt];
+        } else {
+          vf = bf16x8{c.vlo[h][dt][0], c.vlo[h][dt][1], c.vlo[h][dt][2], c.vlo[h][dt][3],
+                      c.vhi[h][dt][0], c.vhi[h][dt][1], c.vhi[h][dt][2], c.vhi[h][dt][3]};
+        }
+        acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[h], acc_o[dt], 0, 0, 0);
+      }
     }
   };
 
-  int kb = kstart + 32 * wid;
+  constexpr int kStep = 128 * H;
+  int kb = kstart + 32 * H * wid;
   if (PIPE) {
     if (kb < kend) {
       Chunk ca, cb;
       load_chunk(kb, ca);
       for (;;) {
-        load_chunk(kb + 128, cb);
+        load_chunk(kb + kStep, cb);
         compute_chunk(kb, ca);
-        kb += 128;
+        kb += kStep;
         if (kb >= kend) break;
-        load_chunk(kb + 128, ca);
+        load_chunk(kb + kStep, ca);
         compute_chunk(kb, cb);
-        kb += 128;
+        kb += kStep;
         if (kb >= kend) break;
       }
     }
   } else {
-    for (; kb < kend; kb += 128) {
+    for (; kb < kend; kb += kStep) {
       Chunk c;
       load_chunk(kb, c);
       compute_chunk(kb, c);
@@ -415,7 +453,7 @@ void set_max_lds(F* f, int bytes) {
 
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
-                      int Hq, int Hkv, int D, float scale, int causal, hipStream_t st) {
+                      int Hq, int Hkv, int D, float scale, int causal, float* lse, hipStream_t st) {
   if (ntiles == 0) return;
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
@@ -426,7 +464,7 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
     set_max_lds(kern, lds);                                                                                    \
     kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,  \
                                                   block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq, \
-                                                  Hkv, scale, causal);                                         \
+                                                  Hkv, scale, causal, lse);                                    \
     GAI_LAUNCH_CHECK();                                                                                        \
     return;                                                                                                    \
   }
@@ -456,10 +494,15 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
   if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
   const dim3 grid(max_splits, Hkv, B);
-  static const bool pipe = getenv("GAI_DECODE_PIPE") && atoi(getenv("GAI_DECODE_PIPE")) != 0;
+  // GAI_DECODE_VARIANT: 0 = 8-B V^T pieces, 1 = 16-B V^T loads (default), 2 = 16-B + 64 keys per wave step,
+  // 3 = 16-B + register double buffer (software pipelined)
+  static const int variant = getenv("GAI_DECODE_VARIANT") ? atoi(getenv("GAI_DECODE_VARIANT")) : 1;
 #define GAI_DEC(DD)                                                                                             \
   if (D == DD) {                                                                                                \
-    auto kern = pipe ? attn_decode_kernel<DD, true> : attn_decode_kernel<DD, false>;                           \
+    auto kern = variant == 0   ? attn_decode_kernel<DD, false, 1, false>                                       \
+                : variant == 2 ? attn_decode_kernel<DD, false, 2, true>                                        \
+                : variant == 3 ? attn_decode_kernel<DD, true, 1, true>                                         \
+                               : attn_decode_kernel<DD, false, 1, true>;                                       \
     kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,    \
                                                  block_tables, max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, \
                                                  Hq, Hkv, scale, split_keys, max_splits);                       \

@@ -331,9 +331,14 @@ def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device) -> tor
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, tiles=None,
-                      q_lens: Sequence[int] | None = None, out=None):
+                      q_lens: Sequence[int] | None = None, out=None, lse=None):
+    """Varlen paged flash attention. ``lse`` (optional fp32 [T, Hq]) receives each row's natural-log
+    softmax normaliser, used to merge partial attentions (parallel/context_parallel.py)."""
     if not q.is_cuda:
-        return _into(out, ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal))
+        o, l = ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal, return_lse=True)
+        if lse is not None:
+            lse.copy_(l)
+        return _into(out, o)
     Hq, Hkv = q.shape[1], k_cache.shape[1]
     if tiles is None:
         if q_lens is None:
@@ -341,7 +346,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
             q_lens = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
         tiles = build_prefill_tiles(q_lens, Hq, Hkv, q.device)
     out = torch.empty_like(q) if out is None else out
-    native().attn_prefill(q, k_cache, v_cache, block_tables, tiles, cu_q, ctx_lens, out, Hq, Hkv, scale, causal)
+    native().attn_prefill(q, k_cache, v_cache, block_tables, tiles, cu_q, ctx_lens, out, Hq, Hkv, scale, causal, lse)
     return out
 
 
@@ -363,11 +368,13 @@ class DecodeWorkspace:
         return self.fixed_split or self.choose_split(self.max_ctx)
 
     @staticmethod
-    def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int = 2048) -> int:
-        """Split length (multiple of 128) giving ~target_wgs workgroups of (split, kv-head, sequence):
-        measured on MI355X (B=64, 8 KV heads, ctx 2.6k) 4.5 TB/s at 256-key splits vs 5.1 TB/s at 1024 -
-        long per-wave streams amortise the per-workgroup prologue/combine, while small batches still
-        need many splits to fill 256 CUs."""
+    def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int = 1536) -> int:
+        """Split length (multiple of 128) giving ~target_wgs workgroups of (split, kv-head, sequence).
+        The head_dim-128 kernel runs 3 workgroups per CU (VGPR-bound), i.e. 768 resident on 256 CUs,
+        so 1536 = exactly two waves of workgroups. Measured on MI355X (B=64, 8 KV heads, ctx
+        2.3-2.6k, profiles/r1/decode_attn_split_sweep_v2.jsonl): 896-key splits (1536 WGs) 5.34 TB/s vs
+        768-key splits (2048 WGs = 2.67 waves, a 1/3-empty last wave) 5.04 TB/s; 256-key splits
+        4.5 TB/s (per-workgroup prologue / combine not amortised)."""
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128

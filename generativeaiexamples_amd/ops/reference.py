@@ -126,9 +126,11 @@ def gather_kv(k_cache, v_cache, block_table, n):
     return k, v
 
 
-def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True):
-    """q [Tq, Hq, D]; per sequence b the queries are the last q_len positions of ctx_lens[b] keys."""
+def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, return_lse=False):
+    """q [Tq, Hq, D]; per sequence b the queries are the last q_len positions of ctx_lens[b] keys.
+    return_lse: also return the fp32 [Tq, Hq] natural-log softmax normalisers (-1e30 for empty rows)."""
     out = torch.empty_like(q)
+    lse = torch.full(q.shape[:2], -1e30, dtype=torch.float32, device=q.device)
     Hq = q.shape[1]
     Hkv = k_cache.shape[1]
     cu = cu_q.tolist()
@@ -148,7 +150,8 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
             att = att.masked_fill(mask[None], float("-inf"))
         p = att.softmax(-1)
         out[s:e] = torch.einsum("hqk,khd->qhd", p, v).to(q.dtype)
-    return out
+        lse[s:e] = torch.logsumexp(att, -1).transpose(0, 1)
+    return (out, lse) if return_lse else out
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale):

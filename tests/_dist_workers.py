@@ -332,3 +332,34 @@ def custom_ar_worker(rank, world, port, out_dir):
     with open(os.path.join(out_dir, f"car_{rank}.json"), "w") as f:
         json.dump({"errors": errs, "us_1MiB": us}, f)
     dist.destroy_process_group()
+
+
+def cp_ring_worker(rank, world, port, out_dir, causal, device="cpu"):
+    """Ring attention over `world` gloo ranks: each rank's zigzag output must match the same rows of
+    full (unsharded) attention. device='cuda': every rank on cuda:0, pairs on the HIP kernel."""
+    import json
+    import math
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from generativeaiexamples_amd.ops import reference as ref
+    from generativeaiexamples_amd.parallel import context_parallel as cp
+
+    S, Hq, Hkv, D = 2 * world * 24, 4, 2, 64
+    g = torch.Generator().manual_seed(5)
+    q = torch.randn(S, Hq, D, generator=g).to(torch.bfloat16)
+    k = torch.randn(S, Hkv, D, generator=g).to(torch.bfloat16)
+    v = torch.randn(S, Hkv, D, generator=g).to(torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    cu = torch.tensor([0, S], dtype=torch.int32)
+    full = ref.attention_dense(q, k, v, cu, scale, bool(causal)).float()
+    dev = torch.device(device if device == "cpu" else "cuda:0")
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
+    mine = cp.ring_attention(*(cp.zigzag_shard(t, rank, world).to(dev) for t in (q, k, v)), scale=scale,
+                             causal=bool(causal)).float().cpu()
+    want = cp.zigzag_shard(full, rank, world)
+    err = (mine - want).abs().max().item()
+    with open(os.path.join(out_dir, f"cp_{rank}.json"), "w") as f:
+        json.dump({"err": err}, f)
+    dist.destroy_process_group()
