@@ -231,7 +231,7 @@ void vit_embed(const Tensor& patches, const Tensor& cls, const Tensor& pos, Tens
 }
 
 void gemm_splitk(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
-                 int64_t epi, Tensor& ws) {
+                 int64_t epi, Tensor& ws, bool psw) {
   check_bf16(A, "A");
   check_bf16(B, "B");
   check_dev(C, "C");
@@ -253,7 +253,7 @@ void gemm_splitk(const Tensor& A, const Tensor& B, Tensor& C, const optional<Ten
     TORCH_CHECK(R->numel() == (int64_t)M * N, "gemm_splitk: residual has wrong size");
   }
   gai_gemm_splitk(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr(bias), opt_ptr(R), M, N, K, ldc, (int)epi,
-                  f32 ? 1 : 0, ws.data_ptr<float>(), cur_stream());
+                  f32 ? 1 : 0, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream());
 }
 
 void quant_rows_fp8(const Tensor& x, Tensor& q, Tensor& scale) {
@@ -413,6 +413,26 @@ void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>
                        (int)rank, world, slot_bytes, err.data_ptr<int>(), cur_stream());
 }
 
+void gemm_splitk_add_rmsnorm(const Tensor& A, const Tensor& B, const optional<Tensor>& bias, Tensor& res,
+                             const Tensor& g, Tensor& out, double eps, Tensor& ws, bool psw) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_bf16(res, "res");
+  check_bf16(g, "g");
+  check_bf16(out, "out");
+  const int K = A.size(-1);
+  const int M = A.numel() / K;
+  const int N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && res.numel() == (int64_t)M * N && out.numel() == (int64_t)M * N && g.numel() == N,
+              "gemm_splitk_add_rmsnorm: shape mismatch");
+  TORCH_CHECK(gai_gemm_splitk_fusable_norm(M, N, K), "gemm_splitk_add_rmsnorm: shape not fusable");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
+              "gemm_splitk_add_rmsnorm: workspace too small");
+  if (bias) check_bf16(*bias, "bias");
+  gai_gemm_splitk_add_rmsnorm(A.data_ptr(), B.data_ptr(), opt_ptr(bias), res.data_ptr(), g.data_ptr(),
+                              out.data_ptr(), M, N, K, (float)eps, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -422,7 +442,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_write", &rope_kv_write);
   m.def("gemm", &gemm);
   m.def("gemm_fp8", &gemm_fp8);
-  m.def("gemm_splitk", &gemm_splitk);
+  m.def("gemm_splitk", &gemm_splitk, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
+        pybind11::arg("R"), pybind11::arg("epi"), pybind11::arg("ws"), pybind11::arg("psw") = false);
   m.def("gemm_splitk_ws_floats", [](int64_t M, int64_t N, int64_t K) {
     return (int64_t)(gai_gemm_splitk_ws_bytes(M, N, K) / 4);
   });
@@ -447,6 +468,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_tanh", &gelu_tanh);
   m.def("geglu_interleaved", &geglu_interleaved);
   m.def("silu_mul_interleaved", &silu_mul_interleaved);
+  m.def("gemm_splitk_add_rmsnorm", &gemm_splitk_add_rmsnorm);
+  m.def("gemm_splitk_fusable_norm", [](int64_t M, int64_t N, int64_t K) { return gai_gemm_splitk_fusable_norm(M, N, K) != 0; });
   m.def("custom_allreduce", &custom_allreduce);
   m.def("ipc_malloc", [](int64_t bytes) { return reinterpret_cast<int64_t>(gai_ipc_malloc(bytes)); });
   m.def("ipc_free", [](int64_t p) { gai_ipc_free(reinterpret_cast<void*>(p)); });

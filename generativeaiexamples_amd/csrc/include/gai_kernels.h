@@ -26,11 +26,12 @@ void gai_gemm_fp8(const void* A, const void* B, const float* sa, const float* sb
                   const void* R, int M, int N, int K, int ldc, int epi, int out_f32, int force, hipStream_t st);
 void gai_quant_rows_fp8(const void* x, int M, int K, long ldx, void* q, float* scale, hipStream_t st);
 
-// gemm_splitk.hip (decode M <= 64: weight-streaming split-K; ws = fp32 [KS, M, N] partials)
+// gemm_splitk.hip (decode M <= 64: weight-streaming split-K; ws = fp32 [KS, M, N] partials;
+//                  psw: B pre-shuffled into MFMA fragments [N/16][K/32][64][8], see ops.preshuffle_weight)
 int gai_gemm_splitk_ks(int M, int N, int K);
 size_t gai_gemm_splitk_ws_bytes(int M, int N, int K);
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                     int ldc, int epi, int out_f32, float* ws, hipStream_t st);
+                     int ldc, int epi, int out_f32, float* ws, int psw, hipStream_t st);
 
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -88,3 +89,8 @@ void gai_ipc_free(void* p);
 void gai_ipc_get_handle(void* p, char* handle64);
 void* gai_ipc_open(const char* handle64);
 void gai_ipc_close(void* p);
+
+// gemm_splitk.hip fused decode tail (TP = 1): res = bf16(bf16(A.W^T + bias) + res); out = rmsnorm(res) * g
+int gai_gemm_splitk_fusable_norm(int M, int N, int K);
+void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias, void* res, const void* g, void* out,
+                                 int M, int N, int K, float eps, float* ws, int psw, hipStream_t st);

@@ -24,7 +24,13 @@ namespace {
 constexpr int kRing = 16;            // k-steps (of 32) of weight fragments in flight per wave
 constexpr int kKAlign = kRing * 32;  // K-slice granularity
 
-template <int MB>
+// Pre-shuffled weight layout [N/16][K/32][64 lanes][8]: fragment (nt, kt) holds, for lane l,
+// W[16 nt + (l & 15)][32 kt + 8 (l >> 4) .. +7] - exactly the B operand of v_mfma_f32_16x16x32_bf16.
+__device__ __forceinline__ size_t psw_offset(int nt, int kt, int K, int lane) {
+  return (((size_t)nt * (K / 32) + kt) * 64 + lane) * 8;
+}
+
+template <int MB, bool PSW>
 __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                           float* __restrict__ part, int M, int N, int K, int KL) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // A slice [16*MB][KL] bf16, swizzled chunks
@@ -46,12 +52,16 @@ __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict
   }
 
   // ---- weight stream of this wave: rows n0 + 16*wid + (lane & 15)
+  // PSW: W is pre-shuffled into MFMA fragments (psw_offset): one k32 step of a 16-row tile is 1 KiB
+  // contiguous, so a wave load is 8 whole 128-B lines instead of 16 half lines of 16 rows.
   const int n = min(n0 + 16 * wid + (lane & 15), N - 1);
-  const bf16* wp = W + (size_t)n * K + k0 + 8 * (lane >> 4);
+  const bf16* wp = PSW ? W + psw_offset(min(n0 / 16 + wid, N / 16 - 1), k0 / 32, K, lane)
+                       : W + (size_t)n * K + k0 + 8 * (lane >> 4);
+  constexpr int kStepW = PSW ? 512 : 32;  // elements between consecutive k32 steps of one lane
   const int nsteps = KL / 32;  // multiple of kRing
   bf16x8 ring[kRing];
 #pragma unroll
-  for (int u = 0; u < kRing; ++u) ring[u] = load8(wp + u * 32);
+  for (int u = 0; u < kRing; ++u) ring[u] = load8(wp + u * kStepW);
 
   f32x4 acc[MB];
 #pragma unroll
@@ -80,7 +90,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict
 #pragma unroll
     for (int u = 0; u < kRing; ++u) {
       const bf16x8 b = ring[u];
-      ring[u] = load8(wp + (s + kRing + u) * 32);
+      ring[u] = load8(wp + (s + kRing + u) * kStepW);
       step(s + u, b);
     }
   }
@@ -120,7 +130,7 @@ constexpr int kLdsRow = 68;  // fp32 row stride of the reduction tiles
 template <int MB>
 constexpr int dec_lds_bytes() { return 4 * 16 * MB * kLdsRow * 4; }
 
-template <int MB, int EPI, bool OUTF32>
+template <int MB, int EPI, bool OUTF32, bool PSW>
 __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                           float* __restrict__ part, void* __restrict__ C,
                                                           const bf16* __restrict__ bias, const bf16* R, int M, int N,
@@ -140,12 +150,15 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
   for (int i = 0; i < MB; ++i) ap[i] = A + (size_t)min(16 * i + (lane & 15), M - 1) * K + kbeg + kq;
   const bf16* wp[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) wp[j] = W + (size_t)min(n0 + 16 * j + (lane & 15), N - 1) * K + kbeg + kq;
+  for (int j = 0; j < 4; ++j)
+    wp[j] = PSW ? W + psw_offset(min(n0 / 16 + j, N / 16 - 1), kbeg / 32, K, lane)
+                : W + (size_t)min(n0 + 16 * j + (lane & 15), N - 1) * K + kbeg + kq;
+  constexpr int kStepW = PSW ? 512 : 32;
 
   bf16x8 ra[kDepth][MB], rw[kDepth][4];
   auto load = [&](int s, bf16x8 (&a)[MB], bf16x8 (&w)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = load8(wp[j] + 32 * s);
+    for (int j = 0; j < 4; ++j) w[j] = load8(wp[j] + kStepW * s);
 #pragma unroll
     for (int i = 0; i < MB; ++i) a[i] = load8(ap[i] + 32 * s);
   };
@@ -343,13 +356,13 @@ namespace {
 
 template <int MB, int EPI, bool OUTF32>
 void launch_stream(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                   int ldc, int KS, float* ws, hipStream_t st) {
-  auto kern = gemm_dec_kernel<MB, EPI, OUTF32>;
-  static bool once = false;
-  if (!once) {
+                   int ldc, int KS, float* ws, bool psw, hipStream_t st) {
+  auto kern = psw ? gemm_dec_kernel<MB, EPI, OUTF32, true> : gemm_dec_kernel<MB, EPI, OUTF32, false>;
+  static bool once[2] = {false, false};
+  if (!once[psw]) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                         dec_lds_bytes<MB>());
-    once = true;
+    once[psw] = true;
   }
   dim3 grid((N + 63) / 64, KS);
   kern<<<grid, 256, dec_lds_bytes<MB>(), st>>>((const bf16*)A, (const bf16*)B, ws, C, (const bf16*)bias,
@@ -359,13 +372,13 @@ void launch_stream(const void* A, const void* B, void* C, const void* bias, cons
 
 template <int MB>
 void dispatch_stream_ks1(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                         int ldc, int epi, int out_f32, hipStream_t st) {
+                         int ldc, int epi, int out_f32, bool psw, hipStream_t st) {
 #define GAI_SS(E)                                                                           \
   case E:                                                                                   \
     if (out_f32)                                                                            \
-      launch_stream<MB, E, true>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, st);           \
+      launch_stream<MB, E, true>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, psw, st);      \
     else                                                                                    \
-      launch_stream<MB, E, false>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, st);          \
+      launch_stream<MB, E, false>(A, B, C, bias, R, M, N, K, ldc, 1, nullptr, psw, st);     \
     return;
   switch (epi) {
     GAI_SS(EPI_NONE)
@@ -384,46 +397,146 @@ void dispatch_stream_ks1(const void* A, const void* B, void* C, const void* bias
 
 }  // namespace
 
+namespace {
+
+// fp32 partials [KS, M, N] of A . W^T into ws (KS > 1), either kernel variant.
+void launch_partials(const void* A, const void* B, int M, int N, int K, int KS, float* ws, int psw, hipStream_t st) {
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  if (!use_legacy(N, K)) {
+    if (MB == 1) launch_stream<1, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, psw, st);
+    else if (MB == 2) launch_stream<2, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, psw, st);
+    else launch_stream<4, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, psw, st);
+    return;
+  }
+  const int KL = K / KS;
+  const size_t lds = (size_t)16 * MB * KL * 2;
+  dim3 grid((N + 63) / 64, KS);
+#define GAI_SK(MBV)                                                                                          \
+  case MBV: {                                                                                                \
+    static bool once = false;                                                                                \
+    if (!once) {                                                                                             \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, false>),                     \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true>),                      \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
+      once = true;                                                                                           \
+    }                                                                                                        \
+    if (psw)                                                                                                 \
+      gemm_splitk_kernel<MBV, true><<<grid, 256, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, KL); \
+    else                                                                                                     \
+      gemm_splitk_kernel<MBV, false><<<grid, 256, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, KL);\
+    GAI_LAUNCH_CHECK();                                                                                      \
+    break;                                                                                                   \
+  }
+  switch (MB) {
+    GAI_SK(1)
+    GAI_SK(2)
+    GAI_SK(4)
+  }
+#undef GAI_SK
+}
+
+// Fused decode tail for TP = 1: h = sum_k partials (+ bias) rounded to bf16, r = bf16(h + res) written
+// back to res, out = rmsnorm(r) * g. One 256-thread workgroup per row (16 columns per thread at
+// N = 4096, NCH chunks of 8): replaces the split-K reduce launch AND the norm launch (whose 64-row
+// grid is 16 workgroups) with one 64-workgroup kernel that issues every load of the row up front.
+template <int NCH>
+__global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(const float* __restrict__ part, int KS, int M, int N,
+                                                                 const bf16* __restrict__ bias, bf16* res,
+                                                                 const bf16* __restrict__ g, float eps,
+                                                                 bf16* __restrict__ out) {
+  __shared__ float scratch[16];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  float v[NCH][8];
+  bf16x8 rr[NCH], gg[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < N) {
+      rr[c] = load8(res + (size_t)m * N + idx);
+      gg[c] = load8(g + idx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      for (int k = 0; k < KS; ++k) {
+        const float4* p = reinterpret_cast<const float4*>(part + ((size_t)k * M + m) * N + idx);
+        const float4 a = p[0], b = p[1];
+        v[c][0] += a.x; v[c][1] += a.y; v[c][2] += a.z; v[c][3] += a.w;  // NOLINT
+        v[c][4] += b.x; v[c][5] += b.y; v[c][6] += b.z; v[c][7] += b.w;  // NOLINT
+      }
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < N) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float h = v[c][j];
+        if (bias) h += (float)bias[idx + j];
+        r[j] = (bf16)((float)(bf16)h + (float)rr[c][j]);
+        v[c][j] = (float)r[j];
+        ss += v[c][j] * v[c][j];
+      }
+      store8(res + (size_t)m * N + idx, r);
+    }
+  }
+  const float inv = rsqrtf(block_sum(ss, scratch) / N + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int idx = (c * 256 + tid) * 8;
+    if (idx < N) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[c][j] * inv * (float)gg[c][j]);
+      store8(out + (size_t)m * N + idx, o);
+    }
+  }
+}
+
+}  // namespace
+
+int gai_gemm_splitk_fusable_norm(int M, int N, int K) {
+  return M >= 1 && M <= 64 && N % 8 == 0 && N <= 256 * 8 * 4 && gai_gemm_splitk_ks(M, N, K) > 1;
+}
+
+void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias, void* res, const void* g, void* out,
+                                 int M, int N, int K, float eps, float* ws, int psw, hipStream_t st) {
+  if (M == 0) return;
+  if (!gai_gemm_splitk_fusable_norm(M, N, K)) gai_launch_error(__FILE__, __LINE__, "gemm_splitk_add_rmsnorm: shape");
+  const int KS = gai_gemm_splitk_ks(M, N, K);
+  launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  const int nch = (N + 2047) / 2048;
+#define GAI_FN(NC)                                                                                          \
+  if (nch == NC) {                                                                                          \
+    splitk_add_rmsnorm_kernel<NC><<<M, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, (bf16*)res,           \
+                                                     (const bf16*)g, eps, (bf16*)out);                       \
+    GAI_LAUNCH_CHECK();                                                                                     \
+    return;                                                                                                 \
+  }
+  GAI_FN(1)
+  GAI_FN(2)
+  GAI_FN(3)
+  GAI_FN(4)
+#undef GAI_FN
+}
+
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                     int ldc, int epi, int out_f32, float* ws, hipStream_t st) {
+                     int ldc, int epi, int out_f32, float* ws, int psw, hipStream_t st) {
+  if (psw && N % 16) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: pre-shuffled weights need N % 16 == 0");
   if (M == 0 || N == 0) return;
   if (M > 64) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: M must be <= 64");
   const int KS = gai_gemm_splitk_ks(M, N, K);
   if (KS == 0) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: K must be a multiple of 512");
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  if (!use_legacy(N, K)) {
-    if (KS == 1) {
-      if (MB == 1) dispatch_stream_ks1<1>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-      else if (MB == 2) dispatch_stream_ks1<2>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-      else dispatch_stream_ks1<4>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-      return;
-    }
-    if (MB == 1) launch_stream<1, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
-    else if (MB == 2) launch_stream<2, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
-    else launch_stream<4, EPI_NONE, true>(A, B, nullptr, nullptr, nullptr, M, N, K, 0, KS, ws, st);
-  } else {
-    const int KL = K / KS;
-    const size_t lds = (size_t)16 * MB * KL * 2;
-    dim3 grid((N + 63) / 64, KS);
-#define GAI_SK(MBV)                                                                                          \
-  case MBV: {                                                                                                \
-    static bool once = false;                                                                                \
-    if (!once) {                                                                                             \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV>),                            \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
-      once = true;                                                                                           \
-    }                                                                                                        \
-    gemm_splitk_kernel<MBV><<<grid, 256, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, KL);        \
-    GAI_LAUNCH_CHECK();                                                                                      \
-    break;                                                                                                   \
+  if (!use_legacy(N, K) && KS == 1) {
+    if (MB == 1) dispatch_stream_ks1<1>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, psw, st);
+    else if (MB == 2) dispatch_stream_ks1<2>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, psw, st);
+    else dispatch_stream_ks1<4>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, psw, st);
+    return;
   }
-    switch (MB) {
-      GAI_SK(1)
-      GAI_SK(2)
-      GAI_SK(4)
-    }
-#undef GAI_SK
-  }
+  launch_partials(A, B, M, N, K, KS, ws, psw, st);
 #define GAI_SKR(E)                                                         \
   case E:                                                                  \
     if (out_f32)                                                           \

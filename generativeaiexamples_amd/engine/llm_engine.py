@@ -57,6 +57,9 @@ class EngineConfig:
     kv_memory_bytes: Optional[int] = None
     prefix_cache: bool = True
     use_graphs: bool = True
+    # keep an MFMA-fragment-shuffled copy of the decode projection weights (ops.preshuffle_weight):
+    # +1x projection weights in HBM for 1.2x faster gate_up / down streaming at decode batch sizes
+    decode_preshuffle: bool = True
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     # multi-step decode: when every running sequence is decoding (nothing waiting), run this many
     # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)
@@ -107,6 +110,9 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
+        if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
+                and hasattr(model, "preshuffle_decode_weights")):
+            model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
         nb = cfg.num_blocks or self._blocks_from_memory()
         # one extra block, never handed out, is the scratch page of padded graph rows
         # models with non-KV layers (cross-attention) report how many layers own a paged KV cache

@@ -230,6 +230,21 @@ class LlamaModel:
             self.w["norm_b"] = e(D)
         self.w["lm_head"] = self.w["embed"] if c.tie_embeddings else e(self.vocab_local, D)
 
+    # gate_up stays on the plain layout: at N = 28672 hipBLASLt streams it at 4.9 TB/s (47.6 us, B = 64)
+    # vs 62.7 us for the 448-workgroup fragment-stream kernel (1.75 workgroups per CU: the second
+    # round runs a quarter empty) - profiles/r1/decode_forward_kernel_stats_v3.csv
+    DECODE_PROJECTIONS = ("qkv", "o", "down", "proj")
+
+    def preshuffle_decode_weights(self) -> int:
+        """Attach fragment-shuffled copies of the per-layer projection weights for the decode GEMM
+        (ops.preshuffle_weight); returns the bytes added. Call after the weights are final."""
+        added = 0
+        for k, v in self.w.items():
+            if k.rsplit(".", 1)[-1] in self.DECODE_PROJECTIONS and isinstance(v, torch.Tensor) \
+                    and getattr(v, "_gai_psw", None) is None and ops.preshuffle_weight(v):
+                added += v.numel() * v.element_size()
+        return added
+
     def random_init(self, seed: int = 0):
         """Random-init weights of the real architecture (benchmarks have no checkpoints offline)."""
         c = self.cfg
@@ -474,9 +489,17 @@ class LlamaModel:
         q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
         attn = torch.empty_like(q)
         h = None
+        # TP = 1 decode: fold each row-parallel projection's split-K reduce, the residual add and the next
+        # RMSNorm into one kernel (ops.linear_add_rmsnorm); xn carries the normalised input forward
+        fuse = (res.is_cuda and ctx.tp_size == 1 and c.norm != "layernorm" and not self.lora_names and T <= 64
+                and os.environ.get("GAI_FUSE_NORM", "1") == "1")
+        xn = None
         for i in range(c.num_layers):
             p = f"l{i}."
-            x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
+            if xn is not None:
+                x, xn = xn, None
+            else:
+                x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
             qkv = self._lora(ops.linear(x, w[p + "qkv"], bias=w.get(p + "qkv_b")), x, i, "qkv", fb)
             if c.qk_norm:
                 self._qk_norm(qkv, p)
@@ -489,15 +512,27 @@ class LlamaModel:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
                                      max_ctx=fb.max_decode_ctx, out=attn[P:])
             a2 = attn.view(T, -1)
-            h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
-            ctx.tp_all_reduce(h)
-            x = self._norm(h, p + "mlp_norm", residual=res)
+            if fuse:
+                x = ops.linear_add_rmsnorm(a2, w[p + "o"], res, w[p + "mlp_norm"], c.rms_eps, bias=w.get(p + "o_b"))
+            else:
+                h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
+                ctx.tp_all_reduce(h)
+                x = self._norm(h, p + "mlp_norm", residual=res)
             if c.mlp == "gelu_tanh":
                 g = self._lora(ops.linear(x, w[p + "fc"], bias=w.get(p + "fc_b"), act="gelu_tanh"), x, i, "fc", fb)
             else:
                 g = ops.linear(x, w[p + "gate_up"], act=c.mlp)
-            h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
-            ctx.tp_all_reduce(h)
+            last = i + 1 == c.num_layers
+            if fuse and not (last and fb.sample_rows is not None):
+                nxt = "norm" if last else f"l{i + 1}.attn_norm"
+                xn = ops.linear_add_rmsnorm(g, w[p + "down"], res, w[nxt], c.rms_eps, bias=w.get(p + "down_b"))
+                h = None
+            else:
+                h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
+                ctx.tp_all_reduce(h)
+        if xn is not None:  # the final norm already ran inside the last layer's down projection
+            logits = ops.linear(xn, w["lm_head"], out_dtype=torch.float32)
+            return ctx.tp_all_gather_last(logits)[:, : c.vocab_size]
         if fb.sample_rows is not None:
             h = h.index_select(0, fb.sample_rows)
             res = res.index_select(0, fb.sample_rows)

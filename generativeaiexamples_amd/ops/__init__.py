@@ -124,6 +124,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     x2 = x.reshape(M, K)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
+    psw = getattr(w, "_gai_psw", None)
+    if psw is not None and M <= 64:  # decode: weight stream from the fragment-shuffled copy
+        if out is None:
+            out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
+        nat = native()
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x2.device)
+        nat.gemm_splitk(x2, psw, out, bias, residual, epi, ws, True)
+        return out
     if residual is None and out is None and TUNER.pick(M, N, K, act, bias is not None, out_dtype, x2, w) == "blas":
         return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
     if out is None:
@@ -133,6 +141,48 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 _SPLITK = os.environ.get("GAI_SPLITK", "1") == "1"
+
+
+def linear_add_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                       bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode tail of a row-parallel projection at TP = 1: ``residual += x @ w^T (+ bias)`` (bf16 rounding
+    as the unfused pair) and return ``rmsnorm(residual) * norm_w``. For decode-sized M the split-K
+    partials are reduced, added and normalised in ONE kernel (no separate reduce / norm launches);
+    otherwise ``linear`` + ``rms_norm``."""
+    K = x.shape[-1]
+    M, N = x.numel() // K, w.shape[0]
+    if (x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and M <= 64
+            and native().gemm_splitk_fusable_norm(M, N, K)):
+        nat = native()
+        psw = getattr(w, "_gai_psw", None)
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x.device)
+        out = torch.empty_like(residual)
+        nat.gemm_splitk_add_rmsnorm(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, residual,
+                                    norm_w, out, eps, ws, psw is not None)
+        return out
+    return rms_norm(linear(x, w, bias), norm_w, eps, residual=residual)
+
+
+def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> the same [N, K]-shaped storage in MFMA B-fragment order [N/16][K/32][64 lanes][8]:
+    lane l of fragment (nt, kt) holds w[16 nt + (l & 15), 32 kt + 8 (l >> 4) : +8]. A decode GEMM wave
+    then streams 1 KiB contiguous per k32 step (8 full 128-B lines) instead of 16 half lines."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0
+    return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+def preshuffle_weight(w: torch.Tensor) -> bool:
+    """Attach a fragment-shuffled copy of a bf16 weight for the decode GEMM (M <= 64). Costs one extra
+    copy of the weight in HBM (16 GB for Llama-3-8B: 288 GB per MI355X buys decode bandwidth).
+    Returns False when the shape does not qualify (N % 16, K % 512)."""
+    if not (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return False
+    N, K = w.shape
+    if N % 16 or K % 512 or N < 64:
+        return False
+    w._gai_psw = shuffle_fragments(w)
+    return True
 
 
 def _native_gemm(x2, w, out, bias, residual, epi):

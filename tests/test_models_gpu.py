@@ -125,3 +125,51 @@ def test_multi_step_graph_decode_equals_single_step(cuda):
     reqs = eng.generate(prompts, SamplingParams(temperature=0.8, top_p=0.9, max_tokens=24, ignore_eos=True))
     for r in reqs:
         assert len(r.output_ids) == 24 and all(0 <= t < g.cfg.vocab_size for t in r.output_ids)
+
+
+
+FUSABLE = dict(hidden_size=1024, intermediate_size=2048, num_heads=8, num_kv_heads=2, head_dim=128)
+
+
+def test_fused_add_rmsnorm_decode_matches(cuda, monkeypatch):
+    """TP=1 decode folds split-K reduce + residual add + RMSNorm into one kernel: the logits of a small
+    prefill step (T <= 64, sampled rows) match the unfused path and the CPU fp32 reference, and those of
+    a pure decode step (every row sampled: the final norm is fused too) match the unfused path."""
+    g, c = _pair_llama(cuda, **FUSABLE)
+    assert g.preshuffle_decode_weights() > 0  # fused path on fragment-shuffled weights too
+    tok = small_byte_tokenizer(512)
+    prompts = [list(range(3, 3 + n)) for n in (9, 20, 30)]
+    eng = LLMEngine(g, tok, EngineConfig(num_blocks=64, max_model_len=512, use_graphs=False))
+    ceng = LLMEngine(c, tok, EngineConfig(num_blocks=64, max_model_len=512, use_graphs=False))
+    for e in (eng, ceng):
+        for p in prompts:
+            e.add_request(p, SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+
+    def both(fb):
+        outs = {}
+        for flag in ("1", "0"):
+            monkeypatch.setenv("GAI_FUSE_NORM", flag)
+            outs[flag] = g.forward(fb, eng.kv, eng.decode_ws).float().cpu()
+        return outs
+
+    fb, _ = eng._make_batch(eng.sched.schedule())
+    outs = both(fb)
+    cfb, _ = ceng._make_batch(ceng.sched.schedule())
+    ref_logits = c.forward(cfb, ceng.kv, ceng.decode_ws).float()
+    scale = ref_logits.abs().max().item()
+    assert (outs["1"] - outs["0"]).abs().max().item() < 0.02 * scale + 0.02
+    assert (outs["1"] - ref_logits).abs().max().item() < 0.05 * scale + 0.05
+    # fresh engine state: one full step (prefill + sample), then a pure decode batch
+    eng2 = LLMEngine(g, tok, EngineConfig(num_blocks=64, max_model_len=512, use_graphs=False))
+    for p in prompts:
+        eng2.add_request(p, SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+    eng2.step()
+    b = eng2.sched.schedule()
+    assert b.num_prefill_tokens == 0 if hasattr(b, "num_prefill_tokens") else True
+    fb, _ = eng2._make_batch(b)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GAI_FUSE_NORM", flag)
+        outs[flag] = g.forward(fb, eng2.kv, eng2.decode_ws).float().cpu()
+    assert outs["1"].shape[0] == len(prompts)
+    assert (outs["1"] - outs["0"]).abs().max().item() < 0.02 * outs["0"].abs().max().item() + 0.02

@@ -80,3 +80,32 @@ def test_splitk_wide_single_pass_epilogue(cuda, M, act):
                    torch.float32)
     tol = 2e-3 if out_dtype == torch.float32 else 2e-2
     torch.testing.assert_close(y.float().cpu(), r, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("act", [None, "swiglu", "residual", "bias"])
+@pytest.mark.parametrize("N,K", [(4096, 14336), (6144, 4096), (2048, 1024)])
+def test_preshuffled_weights_match(cuda, M, act, N, K):
+    """Decode GEMM on fragment-shuffled weights (both split-K kernel variants) == plain layout."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.02).bfloat16()
+    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if act == "bias" else None
+    r = torch.randn(M, N, device=cuda).bfloat16() if act == "residual" else None
+    a = act if act == "swiglu" else None
+    want = ops.linear(x, w, bias=b, residual=r, act=a).float()
+    w2 = w.clone()
+    assert ops.preshuffle_weight(w2)
+    # the fragment copy is a permutation of the weight
+    assert torch.equal(ops.shuffle_fragments(w2).view(-1).sort().values, w2.view(-1).sort().values)
+    got = ops.linear(x, w2, bias=b, residual=r, act=a).float()
+    assert (got - want).abs().max() <= 2e-2 * (want.abs().max() + 1)
+
+
+def test_engine_preshuffles_projections(cuda):
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.tiny(), device=cuda).random_init(0)
+    added = m.preshuffle_decode_weights()
+    assert added > 0 and getattr(m.w["l0.down"], "_gai_psw", None) is not None  # K=512 qualifies
+    assert getattr(m.w["l0.attn_norm"], "_gai_psw", None) is None

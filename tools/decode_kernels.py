@@ -20,11 +20,14 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--ctx", type=int, default=2600)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-psw", action="store_true", help="plain-layout decode weights (no fragment copies)")
     ap.add_argument("--policy", default=None, help="GEMM policy override: tune|native|hipblaslt")
     a = ap.parse_args()
     if a.policy:
         ops.TUNER.mode = a.policy
     m, tok, name = build_llm(a.model, device="cuda")
+    if not a.no_psw:
+        m.preshuffle_decode_weights()  # what LLMEngine does (EngineConfig.decode_preshuffle)
     c = m.cfg
     nbps = (a.ctx + 16) // 16 + 1
     kv = KVCache(getattr(m, "num_kv_layers", c.num_layers), a.batch * nbps + 1, m.hkv, c.head_dim, m.device, m.dtype)

@@ -62,6 +62,35 @@ def bench_decode_gemm(rows, shapes):
                          speedup_vs_blas=t_bl / t_sk))
 
 
+def bench_psw(rows, shapes):
+    """Decode GEMM: plain split-K kernel vs the same on fragment-shuffled weights vs hipBLASLt."""
+    for M, N, K, name in shapes:
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        # a pool of weights larger than the 256 MB Infinity Cache, cycled, so every call streams from HBM
+        ncopy = max(2, -(-(640 << 20) // (N * K * 2)))
+        ws_ = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(ncopy)]
+        sh_ = [ops.shuffle_fragments(w) for w in ws_]
+        w = ws_[0]
+        nat = ops.native()
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device="cuda")
+        y0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        y1 = torch.empty_like(y0)
+        it = [0]
+
+        def nxt(pool):
+            it[0] = (it[0] + 1) % ncopy
+            return pool[it[0]]
+        t0 = timeit(lambda: nat.gemm_splitk(x, nxt(ws_), y0, None, None, 0, ws, False), iters=50)
+        t1 = timeit(lambda: nat.gemm_splitk(x, nxt(sh_), y1, None, None, 0, ws, True), iters=50)
+        tb = timeit(lambda: torch.mm(x, nxt(ws_).t()), iters=50)
+        nat.gemm_splitk(x, sh_[0], y1, None, None, 0, ws, True)
+        err = (y1.float() - (x.float() @ w.float().t())).abs().max().item()
+        by = N * K * 2
+        rows.append(dict(op="decode_gemm_psw", name=name, M=M, N=N, K=K, plain_us=t0 * 1e3, psw_us=t1 * 1e3,
+                         blas_us=tb * 1e3, psw_tbps=by / t1 / 1e9, plain_tbps=by / t0 / 1e9, max_err=err))
+        del ws_, sh_
+
+
 def bench_fp8(rows, shapes):
     """fp8 GEMM (block-scaled MFMA) alone and with the fused per-token quantiser, vs bf16 hipBLASLt and
     (when this torch build has it) hipBLASLt fp8 via torch._scaled_mm."""
@@ -169,6 +198,12 @@ def main():
                    (M, 4096, 14336, f"down b{M}")]
         sh += [(64, 128256, 4096, "lm_head b64")]
         bench_decode_gemm(rows, sh)
+    if "psw" in only:
+        sh = []
+        for M in (1, 16, 64):
+            sh += [(M, 6144, 4096, f"qkv b{M}"), (M, 4096, 4096, f"o b{M}"), (M, 28672, 4096, f"gate_up b{M}"),
+                   (M, 4096, 14336, f"down b{M}")]
+        bench_psw(rows, sh)
     if "fp8" in only:
         bench_fp8(rows, [(4096, 6144, 4096, "qkv prefill"), (4096, 28672, 4096, "gate_up prefill"),
                          (4096, 4096, 14336, "down prefill"), (8192, 8192, 8192, "square 8k"),
