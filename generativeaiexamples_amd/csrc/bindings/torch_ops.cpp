@@ -433,6 +433,27 @@ void gemm_splitk_add_rmsnorm(const Tensor& A, const Tensor& B, const optional<Te
                               out.data_ptr(), M, N, K, (float)eps, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream());
 }
 
+void gdn_decode(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& g, const Tensor& beta, Tensor& state,
+                const Tensor& slots, Tensor& out) {
+  check_f32(q, "q");
+  check_f32(k, "k");
+  check_f32(v, "v");
+  check_f32(g, "g");
+  check_f32(beta, "beta");
+  check_f32(state, "state");
+  check_f32(out, "out");
+  check_i32(slots, "slots");
+  TORCH_CHECK(q.dim() == 3 && k.sizes() == q.sizes() && v.dim() == 3 && state.dim() == 4, "gdn_decode: shapes");
+  const int B = q.size(0), Hv = q.size(1), DK = q.size(2), DV = v.size(2);
+  TORCH_CHECK(v.size(0) == B && v.size(1) == Hv && g.numel() == (int64_t)B * Hv && beta.numel() == (int64_t)B * Hv,
+              "gdn_decode: v / g / beta shapes");
+  TORCH_CHECK(state.size(1) == Hv && state.size(2) == DK && state.size(3) == DV && slots.numel() == B &&
+                  out.numel() == (int64_t)B * Hv * DV, "gdn_decode: state / slots / out shapes");
+  gai_gdn_decode(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(),
+                 beta.data_ptr<float>(), state.data_ptr<float>(), slots.data_ptr<int>(), out.data_ptr<float>(), B, Hv,
+                 DK, DV, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -470,6 +491,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("silu_mul_interleaved", &silu_mul_interleaved);
   m.def("gemm_splitk_add_rmsnorm", &gemm_splitk_add_rmsnorm);
   m.def("gemm_splitk_fusable_norm", [](int64_t M, int64_t N, int64_t K) { return gai_gemm_splitk_fusable_norm(M, N, K) != 0; });
+  m.def("gdn_decode", &gdn_decode);
   m.def("custom_allreduce", &custom_allreduce);
   m.def("ipc_malloc", [](int64_t bytes) { return reinterpret_cast<int64_t>(gai_ipc_malloc(bytes)); });
   m.def("ipc_free", [](int64_t p) { gai_ipc_free(reinterpret_cast<void*>(p)); });

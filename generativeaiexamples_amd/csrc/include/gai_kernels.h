@@ -94,3 +94,7 @@ void gai_ipc_close(void* p);
 int gai_gemm_splitk_fusable_norm(int M, int N, int K);
 void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias, void* res, const void* g, void* out,
                                  int M, int N, int K, float eps, float* ws, int psw, hipStream_t st);
+
+// gdn.hip (Qwen3-Next gated DeltaNet decode step; state pool [slots, Hv, DK, DV] fp32, updated in place)
+void gai_gdn_decode(const float* q, const float* k, const float* v, const float* g, const float* beta, float* state,
+                    const int* slots, float* out, int B, int Hv, int DK, int DV, hipStream_t st);

@@ -243,6 +243,7 @@ class LLMEngine:
         if P > 0:
             fb.cu_q, fb.prefill_ctx, fb.prefill_block_tables = dev[3], dev[4], dev[5]
             fb.prefill_qlen = list(b.prefill_qlen)
+            fb.prefill_ctx_host = list(b.prefill_ctx)
             fb.prefill_tiles = dev[9].reshape(-1)
         if len(b.decode_seq_ids):
             fb.decode_ctx, fb.decode_block_tables = dev[6], dev[7]

@@ -24,6 +24,7 @@ class ForwardBatch:
     prefill_block_tables: Optional[torch.Tensor] = None  # [P, maxb] int32
     prefill_tiles: Optional[torch.Tensor] = None   # attention tiles (host-built)
     prefill_qlen: List[int] = field(default_factory=list)
+    prefill_ctx_host: List[int] = field(default_factory=list)  # host copy of prefill_ctx (state-slot models)
     # decode part
     decode_ctx: Optional[torch.Tensor] = None      # [Dn] int32
     decode_block_tables: Optional[torch.Tensor] = None  # [Dn, maxb] int32

@@ -15,6 +15,7 @@ from .llama import LlamaConfig, LlamaModel
 from .mixtral import MixtralConfig, MixtralModel
 from .mllama import MllamaConfig, MllamaModel
 from .opt import OPTConfig, OPTModel
+from .qwen3_next import Qwen3NextConfig, Qwen3NextModel
 
 LLM_PRESETS = {
     "llama3-8b": ("meta/llama3-8b-instruct", lambda: LlamaConfig.llama3_8b()),
@@ -30,6 +31,11 @@ LLM_PRESETS = {
     "starcoder2-7b": ("bigcode/starcoder2-7b", lambda: LlamaConfig.starcoder2_7b()),
     "qwen2.5-7b": ("qwen/qwen2.5-7b-instruct", lambda: LlamaConfig.qwen25_7b()),
     "qwen3-8b": ("qwen/qwen3-8b", lambda: LlamaConfig.qwen3_8b()),
+    # hybrid Gated-DeltaNet / gated-attention MoE (the reference's Qwen3-Next agent notebook)
+    "qwen3-next-80b-a3b": ("qwen/qwen3-next-80b-a3b-instruct", lambda: Qwen3NextConfig.qwen3_next_80b_a3b()),
+    "qwen3-next-80b-a3b-thinking": ("qwen/qwen3-next-80b-a3b-thinking",
+                                    lambda: Qwen3NextConfig.qwen3_next_80b_a3b(name="qwen/qwen3-next-80b-a3b-thinking")),
+    "tiny-qwen3-next": ("tiny-qwen3-next", lambda: Qwen3NextConfig.tiny()),
     "opt-125m": ("facebook/opt-125m", lambda: OPTConfig.opt_125m()),
     "mixtral-8x7b": ("mistralai/mixtral-8x7b-instruct-v0.1", lambda: MixtralConfig.mixtral_8x7b()),
     "tiny-moe": ("tiny-moe", lambda: MixtralConfig.tiny_moe()),
@@ -67,6 +73,8 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
         arch = json.load(open(os.path.join(weights, "config.json"))).get("model_type", "llama")
         if arch == "opt":
             m = OPTModel(OPTConfig.from_hf(weights), device=device)
+        elif arch == "qwen3_next":
+            m = Qwen3NextModel(Qwen3NextConfig.from_hf(weights), device=device)
         else:
             m = LlamaModel(LlamaConfig.from_hf(weights), device=device)
         m.load_safetensors_dir(weights) if hasattr(m, "load_safetensors_dir") else _load_st(m, weights)
@@ -84,6 +92,9 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
         vocab = cfg.text.vocab_size
     elif isinstance(cfg, MixtralConfig):
         m = MixtralModel(cfg, device=device).random_init(seed)
+        vocab = cfg.vocab_size
+    elif isinstance(cfg, Qwen3NextConfig):
+        m = Qwen3NextModel(cfg, device=device).random_init(seed)
         vocab = cfg.vocab_size
     else:
         m = LlamaModel(cfg, device=device).random_init(seed)
