@@ -110,6 +110,8 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
+        if self.device.type == "cuda":
+            ops.enable_tuned_blas()
         if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident

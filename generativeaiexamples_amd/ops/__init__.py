@@ -290,6 +290,33 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias=None, residual=None, act=None
     return out
 
 
+_TUNED_BLAS = False
+
+
+def enable_tuned_blas() -> bool:
+    """Load the hipBLASLt solutions measured on MI355X for the prefill GEMM shapes (PyTorch TunableOp,
+    lookup only - no tuning at run time). profiles/r1/tunableop_prefill_gemms.jsonl: Llama-3-8B QKV
+    (M = 16384) 1265 -> 1615 TF/s, O 1459 -> 1627 TF/s; gate_up / down keep the default solution.
+    Shapes not in the table use hipBLASLt's heuristic. GAI_TUNABLEOP=0 disables."""
+    global _TUNED_BLAS
+    if _TUNED_BLAS or os.environ.get("GAI_TUNABLEOP", "1") == "0" or not torch.cuda.is_available():
+        return _TUNED_BLAS
+    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "data", "tunableop_mi355x.csv")
+    if not os.path.exists(path):
+        return False
+    import tempfile
+
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    # results are written back to the *current* filename at exit: point it at a scratch file
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"gai_tunableop_{os.getpid()}.csv"))
+    _TUNED_BLAS = bool(tunable.read_file(path))
+    return _TUNED_BLAS
+
+
 class GemmTuner:
     """Per-shape choice between the hand-written MFMA GEMM (fused epilogue) and hipBLASLt + an
     elementwise epilogue kernel, decided by timing both on the first call of each (M-bucket, N, K,

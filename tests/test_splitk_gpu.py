@@ -109,3 +109,15 @@ def test_engine_preshuffles_projections(cuda):
     added = m.preshuffle_decode_weights()
     assert added > 0 and getattr(m.w["l0.down"], "_gai_psw", None) is not None  # K=512 qualifies
     assert getattr(m.w["l0.attn_norm"], "_gai_psw", None) is None
+
+
+def test_tuned_blas_table_loads_and_is_exact(cuda):
+    """The shipped hipBLASLt solution table (TunableOp, lookup only) loads on this image and the tuned
+    QKV prefill GEMM matches the fp32 product."""
+    assert ops.enable_tuned_blas()
+    torch.manual_seed(0)
+    x = torch.randn(16384, 4096, device=cuda).bfloat16()
+    w = (torch.randn(6144, 4096, device=cuda) * 0.02).bfloat16()
+    y = torch.mm(x, w.t())
+    ref_rows = (x[:64].float() @ w.float().t())
+    assert (y[:64].float() - ref_rows).abs().max() < 0.05
