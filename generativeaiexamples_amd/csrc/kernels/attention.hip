@@ -29,6 +29,11 @@ constexpr int kBS = 16;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNeg = -1e30f;
 
+// Raw v_exp_f32 (2^x). exp2f wraps it in a denormal range fix-up (cmp, 2x cndmask, add, ldexp: 6 VALU
+// ops per element); softmax arguments are <= 0, and results below 2^-126 are irrelevant next to the
+// row maximum's 1.0, so the bare instruction is exact enough and 6x cheaper on the VALU.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // ----------------------------------------------------------------------------------------------
 // Prefill
 // ----------------------------------------------------------------------------------------------
@@ -147,35 +152,53 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], s[sub], 0, 0, 0);
       }
     }
-    // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves
+    // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves.
+    // Interior tiles (every key < ctx and, causal, <= the wave's first query position) skip the
+    // per-element mask: wave-uniform test, so only the diagonal / tail tiles pay for it.
     float mt = kNeg;
+    const int kend = kt * 64 + 63;
+    if (kend < ctx && (!causal || kend <= ctx - qlen + r0)) {
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+      for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool ok = key < ctx && (!causal || key <= qpos);
-        const float x = ok ? s[sub][r] * sl2 : kNeg;
-        s[sub][r] = x;
-        mt = fmaxf(mt, x);
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float x = s[sub][r] * sl2;
+          s[sub][r] = x;
+          mt = fmaxf(mt, x);
+        }
+    } else {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const bool ok = key < ctx && (!causal || key <= qpos);
+          const float x = ok ? s[sub][r] * sl2 : kNeg;
+          s[sub][r] = x;
+          mt = fmaxf(mt, x);
+        }
+    }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = fexp2(m_run - m_new);
     float rs = 0.f;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[sub][r] - m_new);
+        const float p = fexp2(s[sub][r] - m_new);
         s[sub][r] = p;
         rs += p;
       }
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
     m_run = m_new;
+    // lazy rescale: once the running maxima settle (most tiles after the first few) alpha == 1 in
+    // every lane and the D/32 x 16 accumulator multiplies are skipped (bit-identical result)
+    if (__any(alpha != 1.f)) {
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i) acc_o[i] *= alpha;
+      for (int i = 0; i < D / 32; ++i) acc_o[i] *= alpha;
+    }
 
     // O^T[d][q] += V^T[d][key] . P^T[key][q]
 #pragma unroll
@@ -326,7 +349,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = fexp2(m_run - m_new);
     float rs = 0.f;
     bf16x8 pf[H];
 #pragma unroll
@@ -335,7 +358,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(s[h][i][r] - m_new);
+          const float pv = fexp2(s[h][i][r] - m_new);
           rs += pv;
           pf[h][4 * i + r] = (bf16)pv;
         }
@@ -403,7 +426,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     float L = 0.f, O = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const float f = exp2f(red_m[w][qq] - M);
+      const float f = fexp2(red_m[w][qq] - M);
       L += red_l[w][qq] * f;
       O += red_o[w][d][qq] * f;
     }
@@ -433,7 +456,7 @@ __global__ void attn_decode_reduce_kernel(const float* __restrict__ ws_o, const 
   float L = 0.f, O = 0.f;
   for (int s = 0; s < ns; ++s) {
     const size_t i = ((size_t)s * B + seq) * Hq + hq;
-    const float f = exp2f(ws_ml[i * 2] - M);
+    const float f = fexp2(ws_ml[i * 2] - M);
     L += ws_ml[i * 2 + 1] * f;
     O += ws_o[i * D + d] * f;
   }
