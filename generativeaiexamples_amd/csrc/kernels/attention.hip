@@ -161,11 +161,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float x = s[sub][r] * sl2;
-          s[sub][r] = x;
-          mt = fmaxf(mt, x);
-        }
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[sub][r]);
     } else {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -173,12 +169,13 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         for (int r = 0; r < 16; ++r) {
           const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
           const bool ok = key < ctx && (!causal || key <= qpos);
-          const float x = ok ? s[sub][r] * sl2 : kNeg;
+          const float x = ok ? s[sub][r] : kNeg;
           s[sub][r] = x;
           mt = fmaxf(mt, x);
         }
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    // scores stay unscaled; the scale folds into the max (scale > 0) and into one fma per exp
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
     const float m_new = fmaxf(m_run, mt);
     const float alpha = fexp2(m_run - m_new);
     float rs = 0.f;
@@ -186,7 +183,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(s[sub][r] - m_new);
+        const float p = fexp2(fmaf(s[sub][r], sl2, -m_new));
         s[sub][r] = p;
         rs += p;
       }
