@@ -7,6 +7,7 @@
 
 #include "block_manager.h"
 #include "scheduler.h"
+#include "shm_channel.h"
 
 namespace py = pybind11;
 using namespace gai;
@@ -94,4 +95,40 @@ PYBIND11_MODULE(_rt, m) {
       .def("has_work", &Scheduler::has_work)
       .def("num_tokens", &Scheduler::num_tokens)
       .def("num_generated", &Scheduler::num_generated);
+
+  py::class_<ShmChannel>(m, "ShmChannel")
+      .def_static("create", &ShmChannel::create, py::arg("name"), py::arg("num_readers"),
+                  py::arg("slot_bytes") = 8 << 20, py::arg("num_slots") = 4, py::return_value_policy::take_ownership)
+      .def_static("open", &ShmChannel::open, py::arg("name"), py::arg("reader"), py::arg("timeout_s") = 60.0,
+                  py::call_guard<py::gil_scoped_release>(), py::return_value_policy::take_ownership)
+      .def("send",
+           [](ShmChannel& c, py::bytes msg, double timeout_s) {
+             char* buf = nullptr;
+             Py_ssize_t len = 0;
+             if (PyBytes_AsStringAndSize(msg.ptr(), &buf, &len) != 0) throw py::error_already_set();
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = c.send(buf, (uint64_t)len, timeout_s);
+             }
+             return ok;
+           },
+           py::arg("msg"), py::arg("timeout_s") = -1.0,
+           "publish one message to every reader; False if a reader did not free a slot within timeout_s")
+      .def("recv",
+           [](ShmChannel& c, double timeout_s) -> py::object {
+             std::vector<char> out;
+             int rc;
+             {
+               py::gil_scoped_release nogil;
+               rc = c.recv(out, timeout_s);
+             }
+             if (rc == 1) return py::none();
+             if (rc == 2) throw std::runtime_error("ShmChannel: the writer process is gone");
+             return py::bytes(out.data(), out.size());
+           },
+           py::arg("timeout_s") = -1.0, "next message (bytes), or None on timeout")
+      .def_property_readonly("slot_bytes", &ShmChannel::slot_bytes)
+      .def_property_readonly("num_readers", &ShmChannel::num_readers)
+      .def_property_readonly("sent", &ShmChannel::sent);
 }

@@ -115,7 +115,19 @@ class LLMEngine:
         if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
+        # tensor parallel: rank 0 of the TP group plans every step, the other members execute its plans
+        ctx = getattr(model, "ctx", None)
+        self.tp_size = ctx.tp_size if ctx is not None else 1
+        self.leader = self.tp_size == 1 or ctx.tp_rank == 0
+        if self.tp_size > 1 and hasattr(model, "register_request"):
+            raise NotImplementedError(f"{mc.name}: per-request model state is not replicated to TP followers")
         nb = cfg.num_blocks or self._blocks_from_memory()
+        if self.tp_size > 1:  # every rank's cache must hold the leader's block ids: agree on the minimum
+            import torch.distributed as dist
+            t = torch.tensor([nb], dtype=torch.int64,
+                             device=self.device if ctx.backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.tp_group)
+            nb = int(t.item())
         # one extra block, never handed out, is the scratch page of padded graph rows
         # models with non-KV layers (cross-attention) report how many layers own a paged KV cache
         self.kv = KVCache(self._kv_layers(), nb + 1, model.hkv, mc.head_dim, self.device, model.dtype)
@@ -141,6 +153,10 @@ class LLMEngine:
         self.lock = threading.RLock()
         self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0, multi_step_runs=0)
         self.eos = set(mc.eos_token_ids) | set(getattr(tokenizer, "eos_ids", ()) or ())
+        self.chan = None
+        if self.tp_size > 1:
+            from ..parallel.step_channel import StepChannel
+            self.chan = StepChannel(ctx)
 
     # ------------------------------------------------------------------ memory
     def _kv_layers(self) -> int:
@@ -205,6 +221,10 @@ class LLMEngine:
         """Register a LoRA adapter (object or directory) for per-request selection. Captured decode graphs
         are dropped and re-captured lazily so they include the new adapter's deltas."""
         with self.lock:
+            if self.chan is not None and self.leader:
+                if not isinstance(adapter, str):
+                    raise ValueError("tensor-parallel engines load LoRA adapters by path (every rank loads it)")
+                self.chan.send({"op": "call", "fn": "add_lora", "args": [name, adapter]})
             slot = self.model.add_lora(name, adapter)
             self.graphs.clear()
             return slot
@@ -218,47 +238,82 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ batch construction
     def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
-        return self.stager.stage([np.asarray(a, dtype=np.int32) if np.asarray(a).dtype != np.int32 else a
-                                  for a in arrays])
+        """Stage index / parameter arrays. int32, float32 and int64 keep their dtype (sampling temperature,
+        top_p and 64-bit seeds must not be truncated); any other integer dtype is narrowed to int32."""
+        out = []
+        for a in arrays:
+            a = np.asarray(a)
+            if a.dtype not in (np.int32, np.float32, np.int64):
+                a = a.astype(np.float32 if a.dtype.kind == "f" else np.int32)
+            out.append(a)
+        return self.stager.stage(out)
 
-    def _make_batch(self, b) -> tuple:
+    # ------------------------------------------------------------------ step plans
+    # A step is planned on the TP leader (scheduler decisions, sampling parameters, KV pages) and executed
+    # from the plan on every rank: the plan is a dict of numpy arrays and plain values, published unchanged
+    # to the follower ranks (parallel/step_channel.py) when the model is tensor-parallel.
+    def _plan_eager(self, b) -> dict:
         P = b.num_prefill_tokens
         samples = b.prefill_samples
         cu = b.cu_q
-        rows, seq_order = [], []
+        rows = []
         for i, sid in enumerate(b.prefill_seq_ids):
             if samples[i]:
                 rows.append(int(cu[i + 1]) - 1)
-                seq_order.append(sid)
-        for j, sid in enumerate(b.decode_seq_ids):
-            rows.append(P + j)
-            seq_order.append(sid)
+        nd = len(b.decode_seq_ids)
+        rows += range(P, P + nd)
         arrs = [b.token_ids, b.positions, b.slots, cu, b.prefill_ctx, b.prefill_block_tables, b.decode_ctx,
                 b.decode_block_tables, np.asarray(rows, dtype=np.int32)]
         if P > 0:
-            q_lens = b.prefill_qlen
             rpt = ops.prefill_rows_per_tile(self.model.hq, self.model.hkv)
-            tiles = np.asarray([(i, s) for i, n in enumerate(q_lens) for s in range(0, n, rpt)], dtype=np.int32)
-            arrs.append(tiles)
-        dev = self._to_device(arrs)
+            arrs.append(np.asarray([(i, s) for i, n in enumerate(b.prefill_qlen) for s in range(0, n, rpt)],
+                                   dtype=np.int32).reshape(-1, 2))
+        plan = dict(op="eager", P=int(P), arr=arrs, qlen=[int(x) for x in b.prefill_qlen],
+                    pctx=[int(x) for x in b.prefill_ctx], max_dctx=int(b.decode_ctx.max()) if nd else 0,
+                    seq_ids=[int(x) for x in b.prefill_seq_ids] + [int(x) for x in b.decode_seq_ids],
+                    pseq=[int(x) for x, smp in zip(b.prefill_seq_ids, samples) if smp])
+        if getattr(self.model, "lora_names", None):
+            per_seq = [self._slot(s) for s in plan["seq_ids"]]
+            qlen = list(b.prefill_qlen) + [1] * nd
+            plan["lora"] = np.repeat(np.asarray(per_seq, np.int32), qlen)
+        return plan
+
+    def _batch_from_plan(self, plan: dict) -> ForwardBatch:
+        P = plan["P"]
+        dev = self._to_device(plan["arr"] + ([plan["lora"]] if plan.get("lora") is not None else []))
         fb = ForwardBatch(token_ids=dev[0], positions=dev[1], slots=dev[2], num_prefill_tokens=P)
         if P > 0:
             fb.cu_q, fb.prefill_ctx, fb.prefill_block_tables = dev[3], dev[4], dev[5]
-            fb.prefill_qlen = list(b.prefill_qlen)
-            fb.prefill_ctx_host = list(b.prefill_ctx)
+            fb.prefill_qlen = list(plan["qlen"])
+            fb.prefill_ctx_host = list(plan["pctx"])
             fb.prefill_tiles = dev[9].reshape(-1)
-        if len(b.decode_seq_ids):
+        if plan["max_dctx"]:
             fb.decode_ctx, fb.decode_block_tables = dev[6], dev[7]
-            fb.max_decode_ctx = int(b.decode_ctx.max())
+            fb.max_decode_ctx = plan["max_dctx"]
         fb.sample_rows = dev[8].long()
-        fb.seq_ids = list(b.prefill_seq_ids) + list(b.decode_seq_ids)
-        if getattr(self.model, "lora_names", None):
-            per_seq = [self._slot(s) for s in fb.seq_ids]
-            qlen = list(b.prefill_qlen) + [1] * len(b.decode_seq_ids)
-            fb.lora_slots = self._to_device([np.repeat(np.asarray(per_seq, np.int32), qlen)])[0]
+        fb.seq_ids = list(plan["seq_ids"])
+        if plan.get("lora") is not None:
+            fb.lora_slots = dev[-1]
         if hasattr(self.model, "prepare_batch"):
             self.model.prepare_batch(fb)
-        return fb, seq_order
+        return fb
+
+    def _make_batch(self, b) -> tuple:
+        """(ForwardBatch, sampled sequence ids) of a StepBatch, built through the eager plan (tests, tools)."""
+        plan = self._plan_eager(b)
+        return self._batch_from_plan(plan), plan["pseq"] + [int(x) for x in b.decode_seq_ids]
+
+    def _publish(self, plan: dict) -> None:
+        if self.chan is not None:
+            self.chan.send(plan)
+
+    def _step_done(self) -> None:
+        """End of a step on every rank: (followers) wait for the step's GPU work so the staging buffers can
+        be reused, then poll the custom all-reduce's error word (RankFailure on a missed peer)."""
+        if self.tp_size > 1:
+            if not self.leader and self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+            self.model.ctx.check_comm()
 
     # ------------------------------------------------------------------ HIP graphs (decode)
     def _slot(self, sid: int) -> int:
@@ -272,7 +327,6 @@ class LLMEngine:
         return None
 
     def _capture(self, bs: int):
-        mc = self.model.cfg
         d = self.device
         ids = torch.zeros(bs, dtype=torch.int32, device=d)
         pos = torch.zeros(bs, dtype=torch.int32, device=d)
@@ -295,9 +349,10 @@ class LLMEngine:
         with torch.cuda.graph(g, stream=s):
             logits = self.model.forward(fb, self.kv, self.decode_ws)
         self.graphs[bs] = (g, fb, logits)
-        del mc
 
     def capture_graphs(self, max_bs: Optional[int] = None):
+        """Capture the decode graphs of every batch bucket <= max_bs. With TP, every rank calls this at the
+        same point (the captures contain the collectives)."""
         if self.device.type != "cuda" or not self.cfg.use_graphs:
             return
         for bs in self.cfg.graph_batch_sizes:
@@ -357,23 +412,19 @@ class LLMEngine:
             return 1
         lim = self.cfg.max_model_len
         for r in reqs:
-            if r is None or r.finished or r.params.has_penalty:
+            if r is None or r.finished or r.params.has_penalty or r.params.guided is not None:
                 return 1
             n = len(r.output_ids)
             if r.params.max_tokens - n < K or len(r.prompt_ids) + n + K > lim:
                 return 1
         return K
 
-    def _run_multi(self, b, reqs, K: int) -> Optional[List[RequestOutput]]:
+    def _plan_multi(self, b, reqs, K: int) -> Optional[dict]:
         ids_list = list(b.decode_seq_ids)
         n = len(ids_list)
         bt_np = self.sched.reserve_decode(ids_list, K)
         if bt_np is None:
             return None
-        bs = self._graph_bucket(n)
-        if bs not in self.multi_graphs:
-            self._capture_multi(bs)
-        g, run, fb, samp, n_valid, toks = self.multi_graphs[bs]
         params = [r.params for r in reqs]
         temp = np.fromiter((0.0 if p.top_k == 1 else p.temperature for p in params), np.float32, n)
         top_p = np.fromiter((p.top_p for p in params), np.float32, n)
@@ -381,13 +432,22 @@ class LLMEngine:
         # per-run seed stream: the graph bakes the in-run step index, the host mixes in the engine step
         seeds = (np.asarray([r.seed for r in reqs], np.int64) * np.int64(0x9E3779B1)
                  + np.int64(self.step_count) * np.int64(0x632BE5AB)) & np.int64(0x7FFFFFFFFFFFFFFF)
-        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx, bt_np, temp, top_p, top_k, seeds,
-                               np.asarray([n], np.int32)])
+        return dict(op="multi", K=int(K), n=n, arr=[b.token_ids, b.positions, b.slots, b.decode_ctx, bt_np, temp,
+                                                     top_p, top_k, seeds, np.asarray([n], np.int32)])
+
+    def _exec_multi(self, plan: dict) -> Optional[np.ndarray]:
+        """Run a K-step decode graph from a plan; the leader gets the sampled tokens [K, n] back."""
+        n, K = plan["n"], plan["K"]
+        bs = self._graph_bucket(n)
+        if bs not in self.multi_graphs:
+            self._capture_multi(bs)
+        g, run, fb, samp, n_valid, toks = self.multi_graphs[bs]
+        src = self._to_device(plan["arr"])
         fb.token_ids[:n].copy_(src[0])
         fb.positions[:n].copy_(src[1])
         fb.slots[:n].copy_(src[2])
         fb.decode_ctx[:n].copy_(src[3])
-        mb = bt_np.shape[1]
+        mb = plan["arr"][4].shape[1]
         fb.decode_block_tables[:n, :mb].copy_(src[4])
         if n < bs:
             fb.token_ids[n:].zero_()
@@ -406,9 +466,15 @@ class LLMEngine:
         else:
             run()  # eager (CPU / graphs off): same device-side feedback, no host round trip per token
         self.stats["multi_step_runs"] += 1
+        host = toks[:, :n].cpu().numpy() if self.leader else None  # [K, n]
+        self._step_done()
+        return host
+
+    def _finish_multi(self, b, reqs, K: int, host: np.ndarray) -> List[RequestOutput]:
+        ids_list = list(b.decode_seq_ids)
+        n = len(ids_list)
         self.step_count += K - 1
         self.stats["decode_tokens"] += n * (K - 1)
-        host = toks[:, :n].cpu().numpy()  # [K, n]
         self._mark("forward")
         outs: List[RequestOutput] = []
         alive = list(range(n))
@@ -423,27 +489,70 @@ class LLMEngine:
         self._mark("process")
         return outs
 
-    def _run_graph(self, b, n: int):
+    def _plan_single(self, b) -> tuple:
+        """(plan, seq_order) of a one-token step: a captured decode graph when the batch is pure decode and
+        fits a bucket, otherwise an eager (prefill / mixed) forward. Sampling parameters ride along."""
+        P, nd = b.num_prefill_tokens, len(b.decode_seq_ids)
+        if P == 0 and self.device.type == "cuda" and self.cfg.use_graphs and self._graph_bucket(nd) is not None:
+            seq_order = [int(x) for x in b.decode_seq_ids]
+            plan = dict(op="graph", n=nd, arr=[b.token_ids, b.positions, b.slots, b.decode_ctx,
+                                                b.decode_block_tables], seq_ids=seq_order)
+            if getattr(self.model, "lora_names", None):
+                plan["lora"] = np.asarray([self._slot(s) for s in seq_order], np.int32)
+        else:
+            plan = self._plan_eager(b)
+            seq_order = plan["pseq"] + [int(x) for x in b.decode_seq_ids]
+        reqs = [self.requests.get(s) for s in seq_order]
+        params = [r.params if r else SamplingParams() for r in reqs]
+        plan["samp"] = SamplingBatch.arrays(params, [r.seed if r else 0 for r in reqs])
+        plan["step"] = self.step_count
+        return plan, seq_order, reqs
+
+    def _exec_single(self, plan: dict, reqs=None) -> Optional[List[int]]:
+        """Forward of a one-token step on this rank; the leader also samples (followers need no tokens:
+        the next plan carries them)."""
+        if plan["op"] == "graph":
+            logits = self._run_graph(plan)
+        else:
+            fb = self._batch_from_plan(plan)
+            logits = self.model.forward(fb, self.kv, self.decode_ws)
+            if fb.sample_rows.numel() == 0:
+                logits = None
+        self._mark("forward")
+        toks = None
+        if self.leader and logits is not None:
+            self._penalize(logits, reqs)
+            temp, top_p, top_k, seeds = self._to_device(plan["samp"])
+            self._mark("penalize_pack")
+            t = ops.sample(logits, temp, top_p, top_k, seeds, plan["step"])
+            self._mark("sample")
+            toks = t.cpu().tolist()
+        self._step_done()
+        return toks
+
+    def _run_graph(self, plan: dict):
+        n = plan["n"]
         bs = self._graph_bucket(n)
         if bs not in self.graphs:
             self._capture(bs)
         g, fb, logits = self.graphs[bs]
-        src = self._to_device([b.token_ids, b.positions, b.slots, b.decode_ctx, b.decode_block_tables])
+        arr = plan["arr"]
+        src = self._to_device(arr)
         fb.token_ids[:n].copy_(src[0])
         fb.positions[:n].copy_(src[1])
         fb.slots[:n].copy_(src[2])
         fb.decode_ctx[:n].copy_(src[3])
-        mb = b.max_blocks
+        mb = arr[4].shape[1]
         fb.decode_block_tables[:n, :mb].copy_(src[4])
         if n < bs:  # padded rows: scratch page, ctx 1
             fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
             fb.decode_ctx[n:].fill_(1)
             fb.decode_block_tables[n:, 0].fill_(self.pad_block)
         if fb.extra is not None:
-            self.model.fill_graph_inputs(fb.extra, list(b.decode_seq_ids), n)
+            self.model.fill_graph_inputs(fb.extra, list(plan["seq_ids"]), n)
         if fb.lora_slots is not None:
             fb.lora_slots.zero_()
-            fb.lora_slots[:n].copy_(self._to_device([np.asarray([self._slot(s) for s in b.decode_seq_ids], np.int32)])[0])
+            fb.lora_slots[:n].copy_(self._to_device([plan["lora"]])[0])
         g.replay()
         self.stats["graph_steps"] += 1
         return logits[:n]
@@ -451,6 +560,8 @@ class LLMEngine:
     # ------------------------------------------------------------------ step
     @torch.inference_mode()
     def step(self) -> List[RequestOutput]:
+        if not self.leader:
+            raise RuntimeError("LLMEngine.step() runs on the TP leader; followers call follow()")
         with self.lock:
             if self._timing:
                 self._t_mark = time.perf_counter()
@@ -470,33 +581,50 @@ class LLMEngine:
                 dreqs = [self.requests.get(s) for s in b.decode_seq_ids]
                 K = self._multi_steps_for(b, dreqs)
                 if K > 1:
-                    with roctx_range("decode_multi"):
-                        outs = self._run_multi(b, dreqs, K)
-                    if outs is not None:
-                        return outs
+                    plan = self._plan_multi(b, dreqs, K)
+                    if plan is not None:
+                        self._publish(plan)
+                        with roctx_range("decode_multi"):
+                            host = self._exec_multi(plan)
+                        return self._finish_multi(b, dreqs, K, host)
+            plan, seq_order, reqs = self._plan_single(b)
+            self._publish(plan)
             with roctx_range("prefill" if P else "decode"):
-                if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
-                        and self._graph_bucket(nd) is not None):
-                    seq_order = list(b.decode_seq_ids)
-                    logits = self._run_graph(b, nd)
-                else:
-                    fb, seq_order = self._make_batch(b)
-                    if not seq_order:
-                        self.model.forward(fb, self.kv, self.decode_ws)
-                        return []
-                    logits = self.model.forward(fb, self.kv, self.decode_ws)
-            self._mark("forward")
-            reqs = [self.requests.get(s) for s in seq_order]
-            params = [r.params if r else SamplingParams() for r in reqs]
-            self._penalize(logits, reqs)
-            sb = SamplingBatch(params, [r.seed if r else 0 for r in reqs], self.device, self.stager)
-            self._mark("penalize_pack")
-            toks = ops.sample(logits, sb.temperature, sb.top_p, sb.top_k, sb.seeds, self.step_count)
-            self._mark("sample")
-            toks = toks.cpu().tolist()
+                toks = self._exec_single(plan, reqs)
+            if toks is None:
+                return []
             out = self._process(seq_order, reqs, toks)
             self._mark("process")
             return out
+
+    # ------------------------------------------------------------------ tensor-parallel followers
+    @torch.inference_mode()
+    def follow(self) -> str:
+        """Follower ranks of a TP engine: execute rank 0's step plans until it yields ('yield': the caller's
+        SPMD code continues, e.g. the next retrieval phase of a benchmark step) or stops ('stop')."""
+        if self.leader or self.chan is None:
+            raise RuntimeError("follow() runs on TP follower ranks")
+        while True:
+            plan = self.chan.recv()
+            op = plan["op"]
+            if op in ("yield", "stop"):
+                return op
+            self.stager.reset()
+            if op == "multi":
+                self._exec_multi(plan)
+            elif op in ("graph", "eager"):
+                self._exec_single(plan)
+            elif op == "call" and plan["fn"] in self._REPLICATED:
+                getattr(self, plan["fn"])(*plan["args"])
+            else:
+                raise RuntimeError(f"step channel: unknown plan op {op!r}")
+
+    _REPLICATED = ("add_lora",)
+
+    def release_followers(self, stop: bool = False) -> None:
+        """Leader: hand control back to the followers' callers ('yield') or end their loops ('stop')."""
+        if self.chan is not None and self.leader:
+            self.chan.send({"op": "stop" if stop else "yield"})
 
     def _mark(self, phase: str):
         """GAI_STEP_TIMING=1: synchronise and accumulate wall time per step phase in ``self.phase_ms``."""

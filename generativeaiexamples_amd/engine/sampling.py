@@ -22,6 +22,8 @@ class SamplingParams:
     repetition_penalty: float = 1.0
     min_tokens: int = 0
     logprobs: bool = False
+    # constrained decoding (engine/guided.py): a compiled grammar / JSON-schema matcher, or None
+    guided: Optional[object] = None
 
     @property
     def greedy(self) -> bool:
@@ -35,12 +37,17 @@ class SamplingParams:
 class SamplingBatch:
     """Packs the per-row sampling parameters of one step into device tensors (one staged H2D copy)."""
 
-    def __init__(self, params: List[SamplingParams], seeds: List[int], device, stager=None):
+    @staticmethod
+    def arrays(params: List[SamplingParams], seeds: List[int]):
+        """Host arrays (temperature fp32, top_p fp32, top_k int32, seeds int64) of one step's rows."""
         import numpy as np
         temp = np.fromiter((0.0 if p.top_k == 1 else p.temperature for p in params), np.float32, len(params))
         top_p = np.fromiter((p.top_p for p in params), np.float32, len(params))
         top_k = np.fromiter((p.top_k for p in params), np.int32, len(params))
-        sd = np.asarray(seeds, dtype=np.int64)
+        return [temp, top_p, top_k, np.asarray(seeds, dtype=np.int64)]
+
+    def __init__(self, params: List[SamplingParams], seeds: List[int], device, stager=None):
+        temp, top_p, top_k, sd = self.arrays(params, seeds)
         if stager is None:
             from .staging import HostStager
             stager = HostStager(device, 1024)

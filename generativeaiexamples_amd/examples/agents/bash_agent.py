@@ -4,8 +4,9 @@ plus W12's "detailed thinking on/off" system-prompt switch).
 
 The model is offered one tool, ``exec_bash_command(cmd)``. Each turn: POST the conversation + tool
 schema to /v1/chat/completions; when the reply carries ``tool_calls`` the command is checked against
-the allow-list (first word), optionally confirmed by the user, run in the jailed working directory
-with a timeout, and its stdout/stderr returned as a ``tool`` message; a reply without tool calls
+the allow-list (first word), its flags (no ``find -exec/-delete/...``) and its path arguments (each must
+resolve inside the working directory), optionally confirmed by the user, run in that directory with a
+timeout, and its stdout/stderr returned as a ``tool`` message; a reply without tool calls
 ends the loop.
 
     python -m generativeaiexamples_amd.examples.agents.bash_agent --base-url http://localhost:8000 \\
@@ -21,6 +22,13 @@ import subprocess
 from typing import Callable, List, Optional
 
 ALLOWED = ("ls", "cat", "head", "tail", "wc", "grep", "find", "pwd", "echo", "sort", "uniq", "du", "df", "date")
+# options that execute, delete or write files (find), or follow arbitrary paths outside the sandbox
+_BANNED_FLAGS = {"find": {"-exec", "-execdir", "-ok", "-okdir", "-delete", "-fprint", "-fprint0", "-fprintf", "-fls",
+                          "-L", "-follow"},
+                 "grep": {"-r", "-R", "--dereference-recursive"},
+                 "sort": {"-o", "--output", "-T", "--temporary-directory", "--compress-program"}}
+_BANNED_FLAG_PREFIXES = {"sort": ("--output=", "--temporary-directory=", "--compress-program="),
+                         "grep": ("--dereference",)}
 TOOL = {"type": "function", "function": {
     "name": "exec_bash_command", "description": "Execute an allow-listed bash command and return its output.",
     "parameters": {"type": "object", "properties": {"cmd": {"type": "string", "description": "the command"}},
@@ -29,7 +37,13 @@ TOOL = {"type": "function", "function": {
 
 class BashTool:
     def __init__(self, cwd: str, allowed=ALLOWED, timeout: float = 10.0, confirm: Optional[Callable[[str], bool]] = None):
-        self.cwd, self.allowed, self.timeout, self.confirm = os.path.abspath(cwd), set(allowed), timeout, confirm
+        self.cwd, self.allowed, self.timeout, self.confirm = os.path.realpath(cwd), set(allowed), timeout, confirm
+
+    def _inside(self, arg: str) -> bool:
+        """True when ``arg``, read as a path relative to the working directory (``~`` expanded, symlinks
+        resolved), stays inside it. Non-path arguments (patterns, numbers) resolve inside trivially."""
+        p = os.path.realpath(os.path.join(self.cwd, os.path.expanduser(arg)))
+        return p == self.cwd or p.startswith(self.cwd + os.sep)
 
     def __call__(self, cmd: str) -> str:
         try:
@@ -38,8 +52,18 @@ class BashTool:
             return f"error: cannot parse command ({e})"
         if not argv or argv[0] not in self.allowed:
             return f"error: '{argv[0] if argv else ''}' is not allowed; allowed: {', '.join(sorted(self.allowed))}"
-        if any(tok in cmd for tok in (";", "&&", "||", "|", "`", "$(", ">", "<")):
+        if any(tok in cmd for tok in (";", "&&", "||", "|", "`", "$(", ">", "<", "\n")):
             return "error: command chaining, pipes and redirection are not allowed"
+        bad = [a for a in argv[1:] if a in _BANNED_FLAGS.get(argv[0], ()) or
+               any(a.startswith(p) for p in _BANNED_FLAG_PREFIXES.get(argv[0], ()))]
+        if bad:
+            return f"error: option {bad[0]} is not allowed for {argv[0]}"
+        for a in argv[1:]:
+            if a.startswith("-") and "=" not in a:
+                continue
+            path = a.split("=", 1)[1] if a.startswith("-") else a
+            if not self._inside(path):
+                return f"error: path {path!r} is outside the working directory"
         if self.confirm is not None and not self.confirm(cmd):
             return "error: the user declined to run this command"
         try:

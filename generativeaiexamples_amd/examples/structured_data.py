@@ -34,9 +34,39 @@ _ALLOWED_NODES = (ast.Expression, ast.Call, ast.Attribute, ast.Name, ast.Load, a
                   ast.In, ast.NotIn, ast.IfExp, ast.FloorDiv, ast.Pow)
 _SAFE_BUILTINS = {"len": len, "round": round, "min": min, "max": max, "sum": sum, "abs": abs, "sorted": sorted,
                   "list": list, "str": str, "int": int, "float": float}
+# Allow-list of attributes an expression may touch (DataFrame / Series / GroupBy / .str / .dt accessors).
+# Everything else - readers (read_pickle / read_csv: arbitrary files or URLs), writers (to_json, to_hdf,
+# to_markdown(buf=...)), eval/query/apply/pipe (code execution) - is rejected at parse time.
+_ALLOWED_ATTRS = frozenset("""
+    loc iloc at iat shape columns index dtypes size ndim empty T values
+    head tail nlargest nsmallest sort_values sort_index sort groupby agg aggregate
+    mean median sum count min max std var mode nunique unique value_counts describe quantile prod cumsum
+    cummax cummin idxmax idxmin abs round clip corr cov rank pct_change diff
+    isna isnull notna notnull fillna dropna drop_duplicates duplicated isin between where mask
+    reset_index set_index rename astype copy get first last nth size filter
+    str dt contains startswith endswith lower upper strip len split replace year month day
+    to_list tolist to_dict item any all eq ne lt le gt ge add sub mul div truediv floordiv mod pow
+    merge join concat DataFrame Series to_datetime to_numeric cut
+""".split())
+# a subset of ``pd`` functions, reachable only as pd.<name>
+_PD_FUNCS = frozenset({"concat", "to_datetime", "to_numeric", "cut", "DataFrame", "Series", "isna", "notna"})
+# keyword arguments that name a file, buffer, URL or callable
+_BANNED_KWARGS = frozenset({"path", "path_or_buf", "buf", "filepath_or_buffer", "func", "engine", "storage_options",
+                            "io", "con", "excel_writer"})
+
+
+class _SafePd:
+    """The only view of pandas an expression gets: the allow-listed functions, nothing else."""
+
+    def __init__(self):
+        for n in _PD_FUNCS:
+            setattr(self, n, getattr(pd, n))
 
 
 def safe_pandas_eval(expr: str, df: pd.DataFrame) -> Any:
+    """Evaluate one LLM-written pandas expression over ``df`` under an AST allow-list: allowed node types,
+    allow-listed attribute names only (no readers / writers / eval / apply), no keyword argument that can
+    name a path, buffer, URL or callable, and no string argument that looks like a path or URL."""
     expr = expr.strip().strip("`")
     if expr.startswith("python"):
         expr = expr[6:].strip()
@@ -44,14 +74,20 @@ def safe_pandas_eval(expr: str, df: pd.DataFrame) -> Any:
     for node in ast.walk(tree):
         if not isinstance(node, _ALLOWED_NODES):
             raise ValueError(f"disallowed syntax: {type(node).__name__}")
-        if isinstance(node, ast.Attribute) and node.attr.startswith("_"):
-            raise ValueError("private attributes are not allowed")
+        if isinstance(node, ast.Attribute):
+            if node.attr.startswith("_") or node.attr not in _ALLOWED_ATTRS:
+                raise ValueError(f"attribute {node.attr!r} is not allowed")
+            if isinstance(node.value, ast.Name) and node.value.id == "pd" and node.attr not in _PD_FUNCS:
+                raise ValueError(f"pd.{node.attr} is not allowed")
         if isinstance(node, ast.Name) and node.id not in ("df", "pd", *_SAFE_BUILTINS):
             raise ValueError(f"unknown name {node.id}")
-        if isinstance(node, ast.Attribute) and node.attr in ("to_csv", "to_pickle", "to_parquet", "eval", "query",
-                                                             "to_sql", "to_excel", "pipe", "apply", "applymap"):
-            raise ValueError(f"method {node.attr} is not allowed")
-    return eval(compile(tree, "<pandas-expr>", "eval"), {"__builtins__": _SAFE_BUILTINS}, {"df": df, "pd": pd})
+        if isinstance(node, ast.keyword) and (node.arg is None or node.arg in _BANNED_KWARGS):
+            raise ValueError(f"keyword argument {node.arg!r} is not allowed")
+        if isinstance(node, ast.Constant) and isinstance(node.value, str) and (
+                node.value.startswith(("/", "~")) or ".." in node.value or "\\" in node.value
+                or "://" in node.value):
+            raise ValueError("path-like string arguments are not allowed")
+    return eval(compile(tree, "<pandas-expr>", "eval"), {"__builtins__": _SAFE_BUILTINS}, {"df": df, "pd": _SafePd()})
 
 
 class StructuredDataRAG(BaseExample):

@@ -83,9 +83,13 @@ class CustomAllReduce:
         return out
 
     def check(self) -> None:
-        """Raise if a launch timed out waiting for a peer (host sync)."""
+        """Raise :class:`RankFailure` if a launch timed out waiting for a peer (host sync). The error word
+        stays set, and the caller (``DistContext.check_comm``) retires this all-reduce: its per-block epochs
+        are out of step with the peers' after a timeout, so later calls could not be trusted either."""
         if int(self.err.item()):
-            raise RuntimeError("custom all-reduce: a peer did not arrive (timed out); results are invalid")
+            from .fault import RankFailure
+            raise RankFailure(f"custom all-reduce on rank {self.rank}: a peer did not arrive within the bounded "
+                              "spin; the reduced activations of that step are invalid")
 
     def close(self) -> None:
         if self._closed:

@@ -58,7 +58,8 @@ class DistContext:
         if self.tp_size > 1:
             car = self.custom_ar
             if car is not None and car.eligible(t):  # latency-bound sizes: one-shot xGMI push
-                return car.all_reduce(t)
+                with guard("tp_custom_all_reduce", self.rank):  # fault injection + error mapping
+                    return car.all_reduce(t)
             with guard("tp_all_reduce", self.rank):
                 if t.is_cuda or t.dtype in (torch.float32, torch.float64):
                     dist.all_reduce(t, group=self.tp_group)
@@ -67,6 +68,20 @@ class DistContext:
                     dist.all_reduce(f, group=self.tp_group)
                     t.copy_(f)
         return t
+
+    def check_comm(self) -> None:
+        """Poll the device-side error word of the custom all-reduce; call at a point that has already
+        synchronised with the stream (the engine does it after copying the sampled tokens to the host). A
+        set word means a peer missed the bounded spin: the custom all-reduce is retired (later messages go
+        to RCCL) and :class:`RankFailure` is raised so serving marks the step's requests failed."""
+        car = self.custom_ar
+        if car is None:
+            return
+        try:
+            car.check()
+        except RankFailure:
+            self.custom_ar = None
+            raise
 
     def tp_all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate the per-rank shards along the last dim (vocab-parallel logits)."""

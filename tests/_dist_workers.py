@@ -238,10 +238,20 @@ def tp_sp_worker(rank, world, port, out_dir):
             eng = LLMEngine(model, tok, EngineConfig(num_blocks=64, max_model_len=256, use_graphs=False,
                                                      decode_steps=1))
             first = eng.add_request(list(range(5, 16)), SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
-            eng.step()  # prefill of the first request
+            if eng.leader:  # TP engine: rank 0 plans the step, the follower executes the same plan
+                eng.step()  # prefill of the first request
+                eng.release_followers()
+            else:
+                assert eng.follow() == "yield"
             eng.add_request(list(range(7, 7 + 26)), SamplingParams(temperature=0.0, max_tokens=1))
-            b = eng.sched.schedule()  # 1 decode token + 26 prefill tokens = 27 (odd)
-            fb, _ = eng._make_batch(b)
+            if eng.leader:  # only the leader's scheduler is authoritative: ship its plan to the follower
+                plan = eng._plan_eager(eng.sched.schedule())  # 1 decode token + 26 prefill tokens = 27 (odd)
+                if eng.chan is not None:
+                    eng.chan.send(plan)
+            else:
+                plan = eng.chan.recv()
+            assert len(plan["arr"][0]) == 27
+            fb = eng._batch_from_plan(plan)
             res[mode] = model.forward(fb, eng.kv).float()
             del first
         ctx.sequence_parallel = False
@@ -279,6 +289,8 @@ def custom_ar_worker(rank, world, port, out_dir):
             if n * (2 if dtype == torch.bfloat16 else 4) > car.max_bytes:
                 continue
             x, ref = inputs(n, dtype, 100 * it + (dtype == torch.float32))
+            torch.cuda.synchronize()
+            dist.barrier()  # ranks time-slice ONE GPU here: launch together so no spin outlives its peer's host
             if it % 2:
                 y = car.all_reduce(x)  # in place
             else:
@@ -306,6 +318,8 @@ def custom_ar_worker(rank, world, port, out_dir):
     for rep in range(4):
         x, ref = inputs(n, torch.bfloat16, 7000 + rep)
         static.copy_(x)
+        torch.cuda.synchronize()
+        dist.barrier()
         g.replay()
         torch.cuda.synchronize()
         want = ref * 0.5 * world
@@ -362,4 +376,59 @@ def cp_ring_worker(rank, world, port, out_dir, causal, device="cpu"):
     err = (mine - want).abs().max().item()
     with open(os.path.join(out_dir, f"cp_{rank}.json"), "w") as f:
         json.dump({"err": err}, f)
+    dist.destroy_process_group()
+
+
+def tp_engine_worker(rank, world, port, out_dir):
+    """TP=world serving engine (rank 0 schedules and publishes step plans, the others follow them) must
+    generate exactly what a single-process engine generates: greedy and seeded sampling, chunked prefill,
+    multi-step decode runs, and an abort issued on rank 0 mid-generation. fp32 weights so the TP partial
+    sums cannot flip a near-tie."""
+    import json
+
+    ctx = _init(rank, world, port, world)
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+
+    cfg = LlamaConfig.tiny(num_heads=8, num_kv_heads=8, head_dim=32, hidden_size=256, intermediate_size=512,
+                           vocab_size=512)
+    ref = LlamaModel(cfg, device="cpu", dtype=torch.float32, dist_ctx=DistContext()).random_init(11)
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32, dist_ctx=ctx).load_hf_state(ref.export_hf_state())
+    tok = small_byte_tokenizer(512)
+    ecfg = dict(num_blocks=96, max_model_len=256, use_graphs=False, decode_steps=4, max_num_seqs=8,
+                max_batched_tokens=48, prefill_chunk=32, prefix_cache=False)
+    eng = LLMEngine(m, tok, EngineConfig(**ecfg))
+    if not eng.leader:
+        assert eng.follow() == "stop"
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    prompts = [list(range(9 + i, 9 + i + n)) for i, n in enumerate((5, 37, 61, 18))]
+    sps = [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in (9, 14, 6, 11)]
+    sps[3] = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=11, ignore_eos=True, seed=1234)
+
+    def drive(e):  # same request stream and the same abort point on both engines (same seeds / step counts)
+        reqs = [e.add_request(p, sp, request_id=f"r{i}") for i, (p, sp) in enumerate(zip(prompts, sps))]
+        victim = e.add_request(list(range(100, 150)), SamplingParams(temperature=0.0, max_tokens=40,
+                                                                     ignore_eos=True), request_id="victim")
+        steps = 0
+        while e.has_work():
+            e.step()
+            steps += 1
+            if steps == 4:
+                assert e.abort("victim")
+        return reqs, victim
+
+    reqs, victim = drive(eng)
+    free_ok = eng.sched.num_free_blocks() == eng.sched.num_blocks()
+    multi = eng.stats["multi_step_runs"]
+    eng.release_followers(stop=True)
+    single, _ = drive(LLMEngine(ref, tok, EngineConfig(**ecfg)))
+    with open(os.path.join(out_dir, "tp_engine.json"), "w") as f:
+        json.dump({"tp": [r.output_ids for r in reqs], "ref": [r.output_ids for r in single],
+                   "victim": victim.finish_reason, "victim_len": len(victim.output_ids), "free_ok": free_ok,
+                   "multi": multi, "plans": eng.chan.sent}, f)
+    dist.barrier()
     dist.destroy_process_group()

@@ -86,3 +86,35 @@ def test_faiss_compat_roundtrip(tmp_path):
     db2 = FAISS.load_local(str(tmp_path / "faiss"), LCEmb(), allow_dangerous_deserialization=True, device="cpu")
     assert db2.similarity_search("fact number 13", k=1)[0].page_content == "fact number 13"
     assert len(db2.as_retriever(search_kwargs={"k": 3}).invoke("fact number 2")) == 3
+
+
+def test_bash_tool_rejects_escapes(tmp_path):
+    (tmp_path / "a.txt").write_text("x")
+    t = BashTool(str(tmp_path))
+    assert t("find . -name '*.txt' -exec rm {} +").startswith("error: option -exec")
+    assert t("find . -delete").startswith("error: option -delete")
+    assert t("find / -execdir sh -c id +").startswith("error")
+    assert "outside the working directory" in t("cat /etc/shadow")
+    assert "outside the working directory" in t("ls ../")
+    assert "outside the working directory" in t("head ~/.bashrc")
+    assert (tmp_path / "a.txt").exists()
+    assert t("cat a.txt") == "x"
+    assert "a.txt" in t("find . -name *.txt")
+
+
+def test_pandas_sandbox_allowlist():
+    import pandas as pd
+    import pytest
+
+    from generativeaiexamples_amd.examples.structured_data import safe_pandas_eval
+
+    df = pd.DataFrame({"a": [1, 2, 3], "b": ["x", "y", "x"]})
+    assert safe_pandas_eval("df.groupby('b')['a'].sum().to_dict()", df) == {"x": 4, "y": 2}
+    assert safe_pandas_eval("df[df['a'] > 1].shape[0]", df) == 2
+    assert safe_pandas_eval("df['a'].mean()", df) == 2.0
+    for bad in ("pd.read_pickle('x.pkl')", "pd.read_csv('data.csv')", "df.to_json('/tmp/x')",
+                "df.to_markdown(buf='out.md')", "df.to_hdf('x.h5', key='k')", "df.apply(print)",
+                "df.eval('a+1')", "df.query('a>1')", "df.pipe(len)", "df.__class__",
+                "df.to_string(buf='f')", "pd.io", "df['a'].map(print)"):
+        with pytest.raises(ValueError):
+            safe_pandas_eval(bad, df)

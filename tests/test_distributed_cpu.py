@@ -58,3 +58,16 @@ def test_tp2_sequence_parallel_matches(tmp_path):
             scale = res["ref"].abs().max().item()
             assert (res["sp"] - res["tp"]).abs().max().item() < 0.02 * scale + 0.02, name
             assert (res["sp"] - res["ref"]).abs().max().item() < 0.03 * scale + 0.03, name
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_engine_follows_leader_plans(tmp_path, world):
+    """Rank-0-scheduled TP engine (step plans over the shared-memory channel) == single-process engine."""
+    import json
+
+    mp.spawn(W.tp_engine_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    d = json.loads((tmp_path / "tp_engine.json").read_text())
+    assert d["tp"] == d["ref"], (d["tp"], d["ref"])
+    assert d["victim"] == "abort" and d["victim_len"] < 40
+    assert d["free_ok"] and d["multi"] > 0 and d["plans"] > 5
