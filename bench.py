@@ -18,6 +18,20 @@ TTFT = query arrival (step start) -> first generated token, per query; p50/p90 r
 vs_baseline = value / 0.2141 queries/s: the reference's own published single-stream L40S figures
 for Llama-3-8B (TTFT 0.062 s + 249 x 18.5 ms TPOT = 4.67 s per query).
 
+Launch: ``python bench.py --gpus N`` spawns N ranks itself (one process per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 set before any GPU call) unless it already runs under torchrun.
+
+Retrieval workload: random-init e5 embeddings of different questions are ~0.99 cosine-similar, so a
+random index returns the same chunks for every query. Before each step (untimed) the bench therefore
+*plants* 4 rows per query of that step (its embedding + 2% noise) at hashed row ids and restores them to
+random vectors afterwards: every query retrieves 4 chunks of its own through the full 1M-row scan,
+as a real corpus would (``unique_chunks_retrieved`` = 4 x queries).
+
+After the timed steps (untimed, reported alongside): ``p50_ttft_c1_s`` - 8 queries one at a time, TTFT
+from query arrival to first token; and an open-loop run (Poisson arrivals at 0.8x the measured rate,
+``poisson``), both on the rank-local index shard. ``retrieval_breakdown_ms`` splits the per-step query
+path into embed / scan / prompt build / tokenize / add_request.
+
 Notes: the KV prefix cache is off (every query prefills its full prompt); score_threshold is disabled (random-init embeddings give near-zero cosine to a random
 index; thresholding would drop every chunk); EOS is ignored so every query generates exactly
 max_tokens (fixed work per step).
@@ -27,7 +41,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import random
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -61,10 +78,39 @@ def parse():
                          "chunks for every query, so caching would skip most of the prefill work)")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache size per rank (default: 50%% of free HBM)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-plant", action="store_true", help="do not plant per-query relevant chunks")
+    ap.add_argument("--no-probes", action="store_true", help="skip the untimed c1 / open-loop TTFT probes")
+    ap.add_argument("--probe-c1", type=int, default=8, help="queries of the concurrency-1 TTFT probe")
     from generativeaiexamples_amd.benchmarks import CONFIGS, module
     for c in CONFIGS:
         module(c).add_args(ap)
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """Run this script as n ranks (one per GPU) when not already under a launcher; returns the worst exit
+    code. Children are started before this process touches the GPU; a failing rank stops the others."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def log(*a):
@@ -91,8 +137,77 @@ def run_other_config(args):
         torch.distributed.destroy_process_group()
 
 
+def run_probes(args, embedder, index, engine, build_requests, plant, unplant, new_phase, qps_per_rank):
+    """c1 TTFT and open-loop Poisson TTFT (untimed). Every query: embed -> local 1M scan -> prompt ->
+    engine; TTFT = scheduled arrival -> first token. c1 queries are aborted after their first token."""
+    rank = int(os.environ.get("RANK", "0"))
+
+    def retrieve(qids):
+        qs = [synthetic_question(q) for q in qids]
+        e = embedder.embed(qs, input_type="query")
+        _, rows = index.search_raw(e, args.top_k)
+        return build_requests(qs, rows.cpu().tolist(), new_phase())
+
+    # concurrency 1
+    c1 = []
+    base = 900_000 + 1000 * rank
+    for i in range(args.probe_c1):
+        qid = base + i
+        planted = plant([qid], [synthetic_question(qid)])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        req = retrieve([qid])[0]
+        while req.first_token_time is None:
+            engine.step()
+        c1.append(req.first_token_time - t0)
+        engine.abort(req.request_id)
+        while engine.has_work():
+            engine.step()
+        unplant(planted)
+    # open loop: Poisson arrivals at 0.8x the measured per-rank burst rate
+    rate = 0.8 * qps_per_rank
+    rng = random.Random(4242 + rank)
+    n = args.batch
+    arrivals, t = [], 0.0
+    for _ in range(n):
+        t += rng.expovariate(rate)
+        arrivals.append(t)
+    qids = [base + 500 + i for i in range(n)]
+    planted = plant(qids, [synthetic_question(q) for q in qids])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reqs, nxt = [], 0
+    while nxt < n or engine.has_work():
+        now = time.perf_counter() - t0
+        due = []
+        while nxt < n and arrivals[nxt] <= now:
+            due.append(nxt)
+            nxt += 1
+        if due:
+            for i, r in zip(due, retrieve([qids[i] for i in due])):
+                reqs.append((arrivals[i], r))
+        if engine.has_work():
+            engine.step()
+        elif nxt < n:
+            time.sleep(max(0.0, min(0.002, arrivals[nxt] - (time.perf_counter() - t0))))
+    span = time.perf_counter() - t0
+    unplant(planted)
+    tt = sorted(r.first_token_time - t0 - a for a, r in reqs)
+    return {"p50_ttft_c1_s": round(statistics.median(c1), 4), "ttft_c1_s": [round(x, 4) for x in c1],
+            "poisson": {"rate_qps_per_gpu": round(rate, 3), "queries": n, "achieved_qps_per_gpu": round(n / span, 3),
+                        "p50_ttft_s": round(tt[len(tt) // 2], 4),
+                        "p90_ttft_s": round(tt[min(len(tt) - 1, int(0.9 * len(tt)))], 4)}}
+
+
+def synthetic_question(q: int) -> str:
+    from generativeaiexamples_amd.rag import synthetic
+    return synthetic.question(q)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     if args.config != 2:
         return run_other_config(args)
     args.batch = args.batch or 64
@@ -163,29 +278,72 @@ def main():
     params = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=args.max_tokens, ignore_eos=True)
     doc_of = lambda g: index.document(ShardedIndex.split_row(g)[1]) if world > 1 else index.document(g)  # noqa
 
-    def run_step(step_idx: int):
+    # ---------------- per-query relevant chunks (see module docstring)
+    N = args.index_size
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77 + rank)
+
+    def plant_rows(qid: int):
+        return [(qid * 2654435761 + j * 40503 + 12345) % N for j in range(args.top_k)]
+
+    def plant(qids, questions):
+        if args.no_plant:
+            return []
+        e = embedder.embed(questions, input_type="query").float()
+        e = torch.nn.functional.normalize(e, dim=-1)
+        rows = [r for q in qids for r in plant_rows(q)]
+        v = e.repeat_interleave(args.top_k, 0)
+        v = v + 0.02 * torch.randn(v.shape, device=v.device, generator=gen) / (v.shape[1] ** 0.5)
+        index.set_vectors(rows, v)
+        return rows
+
+    def unplant(rows):
+        if rows:
+            r = torch.randn(len(rows), index.dim, device=dev, generator=gen)
+            index.set_vectors(rows, r)
+
+    def build_requests(questions, rows, phase):
+        """rows: retrieved global row ids per query -> engine requests (timed by phase)."""
+        t = time.perf_counter()
+        texts = []
+        for qi, q in enumerate(questions):
+            docs = [doc_of(g) for g in rows[qi] if g >= 0]
+            texts.append(rag_user_message("\n\n".join(d.page_content for d in docs), q))
+        t1 = time.perf_counter()
+        prompts = [apply_chat_template([{"role": "system", "content": RAG_TEMPLATE},
+                                        {"role": "user", "content": u}], ltok) for u in texts]
+        t2 = time.perf_counter()
+        reqs = [engine.add_request(pr, params) for pr in prompts]
+        t3 = time.perf_counter()
+        phase["prompt_build"] += t1 - t
+        phase["tokenize"] += t2 - t1
+        phase["add_request"] += t3 - t2
+        return reqs
+
+    def run_step(step_idx: int, phase: dict):
         qids = [(step_idx * world + rank) * args.batch + i for i in range(args.batch)]
         questions = [synthetic.question(q) for q in qids]
+        planted = plant(qids, questions)
         ctx.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         emb = embedder.embed(questions, input_type="query")
+        torch.cuda.synchronize()
+        t_e = time.perf_counter()
         rel, rows = sharded.search_raw(emb, args.top_k)
         rows = rows.cpu().tolist()
+        t_s = time.perf_counter()
+        phase["embed"] += t_e - t0
+        phase["scan"] += t_s - t_e
         uniq.update(g for r in rows for g in r)
-        reqs = []
-        for qi, q in enumerate(questions):
-            docs = [doc_of(g) for g in rows[qi] if g >= 0]
-            context = "\n\n".join(d.page_content for d in docs)
-            msgs = [{"role": "system", "content": RAG_TEMPLATE},
-                    {"role": "user", "content": rag_user_message(context, q)}]
-            reqs.append(engine.add_request(apply_chat_template(msgs, ltok), params))
+        reqs = build_requests(questions, rows, phase)
         t_retrieved = time.perf_counter()
         while engine.has_work():
             engine.step()
         torch.cuda.synchronize()
         ctx.barrier()
         t1 = time.perf_counter()
+        unplant(planted)
         ttft = [r.first_token_time - t0 for r in reqs]
         ntok = sum(len(r.output_ids) for r in reqs)
         short = [len(r.output_ids) for r in reqs if len(r.output_ids) != args.max_tokens]
@@ -193,19 +351,31 @@ def main():
         plen = statistics.mean(len(r.prompt_ids) for r in reqs)
         return t1 - t0, ttft, ntok, plen, t_retrieved - t0
 
+    def new_phase():
+        return dict(embed=0.0, scan=0.0, prompt_build=0.0, tokenize=0.0, add_request=0.0)
+
     uniq = set()
     for w in range(args.warmup):
-        dt, *_ = run_step(10_000 + w)
+        dt, *_ = run_step(10_000 + w, new_phase())
         log(f"warmup {w}: {dt:.2f}s")
+    uniq = set()
+    phase = new_phase()
     times, ttfts, toks, plens, rtimes = [], [], 0, [], []
     for s in range(args.steps):
-        dt, ttft, ntok, plen, rt = run_step(s)
+        dt, ttft, ntok, plen, rt = run_step(s, phase)
         times.append(dt)
         ttfts += ttft
         toks += ntok
         plens.append(plen)
         rtimes.append(rt)
         log(f"step {s}: {dt:.3f}s  p50 TTFT {statistics.median(ttft):.3f}s  retrieval {rt * 1000:.1f} ms")
+
+    # ---------------- untimed TTFT probes on the rank-local shard (no collectives: ranks run them freely)
+    probes = {}
+    if not args.no_probes:
+        probes = run_probes(args, embedder, index, engine, build_requests, plant, unplant, new_phase,
+                            args.batch * args.steps * world / max(1e-9, max(ctx.all_gather_obj(sum(times)))) / world)
+        log(f"probes: {probes}")
 
     total = sum(times)
     # max over ranks
@@ -250,6 +420,9 @@ def main():
         "unique_chunks_retrieved": len(uniq),
         "prefix_cache": bool(args.prefix_cache),
         "baseline_qps": round(BASELINE_QPS, 4),
+        "retrieval_breakdown_ms": {k: round(1000 * v / max(1, args.steps), 2) for k, v in phase.items()},
+        "planted_chunks": not args.no_plant,
+        **probes,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -9,8 +9,8 @@ All ranks form ONE serving instance (strong scaling of a fixed global batch):
     are all-gathered and merged (index DP);
   * each rank reranks the 40 candidates of its own queries (reranker DP) and the top-4 ids are
     all-gathered, so every rank builds the same prompts;
-  * the 70B generator runs TP=N: every rank holds 1/N of each layer and the engines advance in
-    lockstep (identical requests, seeds and scheduler decisions; logits all-gathered before sampling).
+  * the 70B generator runs TP=N as ONE engine: rank 0 owns the scheduler and the requests and publishes
+    every step plan; ranks 1..N-1 execute the plans (LLMEngine.follow, parallel/step_channel.py).
 On one MI355X (TP=1) the whole 141 GB bf16 model plus a 20 GB index shard fits in its 288 GB.
 """
 from __future__ import annotations
@@ -102,6 +102,9 @@ def run(args, ctx) -> dict:
                 merged.update(part)
             top = merged
         t_ret = time.perf_counter() - t0
+        if not engine.leader:  # TP follower: execute rank 0's step plans until it yields
+            assert engine.follow() == "yield"
+            return dict(ttft=[], tokens=0, retrieval_s=t_ret, prompt=0.0)
         reqs = []
         for j, q in enumerate(qs):
             context = "\n\n".join(doc(g).page_content for g in top[j])
@@ -109,12 +112,13 @@ def run(args, ctx) -> dict:
             reqs.append(engine.add_request(apply_chat_template(msgs, tok), params, request_id=f"s{i}-q{j}"))
         while engine.has_work():
             engine.step()
+        engine.release_followers()
         assert all(len(r.output_ids) == args.max_tokens for r in reqs), "a query was cut short"
         return dict(ttft=[r.first_token_time - t0 for r in reqs], tokens=sum(len(r.output_ids) for r in reqs),
                     retrieval_s=t_ret, prompt=sum(len(r.prompt_ids) for r in reqs) / len(reqs))
 
     total, stats = timed_steps(ctx, step, args.steps, args.warmup)
-    ttft = [x for s in stats for x in s["ttft"]]  # identical engines on every TP rank: rank-local list
+    ttft = [x for s in stats for x in s["ttft"]]  # rank 0 (the TP leader) owns the requests
     toks = sum(s["tokens"] for s in stats)
     nq = gbatch * args.steps
     return {

@@ -126,6 +126,17 @@ class HBMIndex:
             self.docs.extend([None] * n)
             self.doc_fn = doc_fn
 
+    def set_vectors(self, rows: Sequence[int], vectors: torch.Tensor) -> None:
+        """Overwrite the vectors of existing rows (same preparation as ``add``). Synthetic benchmarks plant
+        a question's relevant chunks this way so that every query retrieves its own rows."""
+        v = self._prep(vectors if vectors.ndim == 2 else vectors[None])
+        idx = torch.as_tensor(list(rows), dtype=torch.long, device=self.device)
+        assert idx.numel() == v.shape[0] and (idx.numel() == 0 or int(idx.max()) < self.n)
+        with self.lock:
+            self.vectors[idx] = v.to(self.dtype)
+            if self.metric == "l2":
+                self.bias[idx] = -0.5 * v.to(self.dtype).float().pow(2).sum(-1)
+
     def delete(self, predicate) -> int:
         """Tombstone every row whose document satisfies predicate(doc). Returns #deleted."""
         with self.lock:
