@@ -175,6 +175,18 @@ void apply_penalties(Tensor& logits, const Tensor& tok_ids, const Tensor& tok_cn
                       pres.data_ptr<float>(), rep.data_ptr<float>(), cur_stream());
 }
 
+void token_mask(Tensor& logits, const Tensor& rows, const Tensor& mask) {
+  check_f32(logits, "logits");
+  check_i32(rows, "rows");
+  TORCH_CHECK(mask.scalar_type() == at::kInt && mask.dim() == 2 && mask.is_contiguous(),
+              "token_mask: mask must be int32 [R, W] (uint32 bit words)");
+  TORCH_CHECK(mask.size(0) == rows.numel(), "token_mask: one mask row per logits row");
+  const int V = logits.size(1), W = mask.size(1);
+  TORCH_CHECK((int64_t)W * 32 >= V, "token_mask: mask narrower than the vocabulary");
+  gai_token_mask(logits.data_ptr<float>(), logits.stride(0), V, rows.data_ptr<int>(), rows.numel(),
+                 reinterpret_cast<const uint32_t*>(mask.data_ptr<int>()), W, cur_stream());
+}
+
 void sim_topk(const Tensor& Q, const Tensor& X, const Tensor& bias, int64_t n_rows, int64_t k, Tensor& ws_v,
               Tensor& ws_i, int64_t nwg, int64_t rows_per_wg, Tensor& out_v, Tensor& out_i) {
   check_bf16(Q, "Q");
@@ -476,6 +488,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode);
   m.def("sample", &sample);
   m.def("apply_penalties", &apply_penalties);
+  m.def("token_mask", &token_mask);
   m.def("sim_topk", &sim_topk);
   m.def("topk_cap", [](int64_t k) { return gai_topk_cap(k); });
   m.def("moe_route", &moe_route);

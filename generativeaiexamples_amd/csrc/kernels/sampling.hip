@@ -195,7 +195,30 @@ __global__ void penalty_kernel(float* logits, long ld, const int* __restrict__ t
   }
 }
 
+// Constrained decoding: logits[rows[r], t] = -inf wherever bit t of mask[r] is clear. One thread per
+// 32-token mask word; a 64-lane wave covers 2048 vocabulary entries with coalesced 128-B row loads.
+__global__ void token_mask_kernel(float* logits, long ld, int V, const int* __restrict__ rows,
+                                  const uint32_t* __restrict__ mask, int W) {
+  const int r = blockIdx.y;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  const uint32_t bits = mask[(size_t)r * W + w];
+  if (bits == 0xFFFFFFFFu) return;
+  float* row = logits + (size_t)rows[r] * ld;
+  const int t0 = w * 32;
+#pragma unroll 4
+  for (int b = 0; b < 32; ++b)
+    if (!(bits >> b & 1u) && t0 + b < V) row[t0 + b] = -INFINITY;
+}
+
 }  // namespace
+
+void gai_token_mask(float* logits, long ld, int V, const int* rows, int R, const uint32_t* mask, int W,
+                    hipStream_t st) {
+  if (R == 0) return;
+  token_mask_kernel<<<dim3((W + 255) / 256, R), 256, 0, st>>>(logits, ld, V, rows, mask, W);
+  GAI_LAUNCH_CHECK();
+}
 
 void gai_sample(const float* logits, int B, int V, long ld, const float* temperature, const float* top_p,
                 const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, hipStream_t st) {

@@ -6,11 +6,37 @@
 #include <cstring>
 
 #include "block_manager.h"
+#include "grammar.h"
 #include "scheduler.h"
 #include "shm_channel.h"
 
 namespace py = pybind11;
 using namespace gai;
+
+// compiled schema node (engine/guided.py) -> GNode
+static GNode gnode_from(const py::dict& d) {
+  GNode n;
+  n.kind = d["kind"].cast<int>();
+  auto get_i = [&](const char* k, int dflt) { return d.contains(k) ? d[k].cast<int>() : dflt; };
+  n.item = get_i("item", -1);
+  n.min_items = get_i("min_items", 0);
+  n.max_items = get_i("max_items", 1 << 20);
+  n.min_len = get_i("min_len", 0);
+  n.max_len = get_i("max_len", 256);
+  n.disc_prop = get_i("disc_prop", -1);
+  n.dep_prop = get_i("dep_prop", -1);
+  if (d.contains("keys")) n.keys = d["keys"].cast<std::vector<std::string>>();
+  if (d.contains("props")) n.props = d["props"].cast<std::vector<int>>();
+  if (d.contains("required")) {
+    for (bool r : d["required"].cast<std::vector<bool>>()) n.required.push_back(r ? 1 : 0);
+  }
+  if (d.contains("dep_alts")) n.dep_alts = d["dep_alts"].cast<std::vector<int>>();
+  if (d.contains("lits")) n.lits = d["lits"].cast<std::vector<std::string>>();
+  if (d.contains("alts")) n.alts = d["alts"].cast<std::vector<int>>();
+  n.required.resize(n.props.size(), 1);
+  if (n.keys.size() != n.props.size()) throw std::invalid_argument("grammar node: keys/props size mismatch");
+  return n;
+}
 
 template <typename T>
 py::array_t<T> arr(const std::vector<T>& v) {
@@ -95,6 +121,41 @@ PYBIND11_MODULE(_rt, m) {
       .def("has_work", &Scheduler::has_work)
       .def("num_tokens", &Scheduler::num_tokens)
       .def("num_generated", &Scheduler::num_generated);
+
+  py::class_<Grammar>(m, "Grammar")
+      .def(py::init([](const py::list& nodes, int root, const py::list& vocab, std::vector<int> eos) {
+             std::vector<GNode> ns;
+             for (auto& o : nodes) ns.push_back(gnode_from(o.cast<py::dict>()));
+             if (root < 0 || root >= (int)ns.size()) throw std::invalid_argument("grammar: bad root");
+             std::vector<std::string> vb;
+             vb.reserve(vocab.size());
+             for (auto& o : vocab) vb.push_back(o.is_none() ? std::string() : o.cast<std::string>());
+             return new Grammar(std::move(ns), root, vb, std::move(eos));
+           }),
+           py::arg("nodes"), py::arg("root"), py::arg("vocab"), py::arg("eos"),
+           "nodes: compiled schema (list of dicts); vocab: bytes of every token id (None = never allowed)")
+      .def_property_readonly("vocab_size", &Grammar::vocab_size)
+      .def_property_readonly("max_token_len", &Grammar::max_token_len)
+      .def("minlen", &Grammar::minlen);
+
+  py::class_<Matcher>(m, "Matcher")
+      .def(py::init<const Grammar*>(), py::arg("grammar"), py::keep_alive<1, 2>())
+      .def("fill_mask",
+           [](Matcher& mt, int budget, py::array_t<uint32_t, py::array::c_style> out) {
+             if (out.size() * 32 < mt.vocab_size()) throw std::invalid_argument("fill_mask: mask too small");
+             uint32_t* p = out.mutable_data();  // with the GIL held
+             py::gil_scoped_release nogil;
+             mt.fill_mask(budget, p);
+           },
+           py::arg("budget"), py::arg("out"),
+           "allowed-token bitmask (uint32 words) for the next token, `budget` tokens left including it")
+      .def("advance", &Matcher::advance, py::arg("token"))
+      .def("feed_bytes", [](Matcher& mt, py::bytes b) { return mt.feed_bytes(std::string(b)); })
+      .def_property_readonly("done", &Matcher::done)
+      .def_property_readonly("dead", &Matcher::dead)
+      .def_property_readonly("can_finish", &Matcher::can_finish)
+      .def_property_readonly("min_chars", &Matcher::min_chars)
+      .def_property_readonly("cache_size", &Matcher::cache_size);
 
   py::class_<ShmChannel>(m, "ShmChannel")
       .def_static("create", &ShmChannel::create, py::arg("name"), py::arg("num_readers"),

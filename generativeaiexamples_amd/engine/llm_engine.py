@@ -26,7 +26,7 @@ import os
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -83,6 +83,8 @@ class Request:
     seed: int = 0
     token_counts: Dict[int, int] = field(default_factory=dict)
     lora_slot: int = 0
+    max_new: int = 0
+    matcher: Any = None  # constrained decoding (engine/guided.py): this request's grammar state
 
     @property
     def text(self) -> str:
@@ -110,8 +112,8 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
-        if self.device.type == "cuda":
-            ops.enable_tuned_blas()
+        if self.device.type == "cuda" and ops.TUNER.mode != "native":
+            ops.enable_tuned_blas()  # library GEMMs are only used under GAI_GEMM_POLICY=tune|hipblaslt
         if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
@@ -141,6 +143,7 @@ class LLMEngine:
                                                                   getattr(model, "max_cross_tokens", 0)),
                                                  self.device)
         self.stager = HostStager(self.device)
+        self._masks = None  # guided-decoding mask builder (lazy)
         self._timing = os.environ.get("GAI_STEP_TIMING") == "1"
         self.phase_ms: Dict[str, float] = {}
         self._t_mark = 0.0
@@ -191,6 +194,9 @@ class LLMEngine:
                 max_new = 1
             req = Request(rid, list(prompt_ids), params, sid, IncrementalDetokenizer(self.tok, params.stop),
                           seed=params.seed if params.seed is not None else (sid * 7919) & 0x7FFFFFFF)
+            req.max_new = max_new
+            if params.guided is not None:
+                req.matcher = params.guided.matcher()
             if lora:
                 req.lora_slot = self.model.lora_slot(lora)
             self.requests[sid] = req
@@ -522,6 +528,7 @@ class LLMEngine:
         toks = None
         if self.leader and logits is not None:
             self._penalize(logits, reqs)
+            self._guide(logits, reqs)
             temp, top_p, top_k, seeds = self._to_device(plan["samp"])
             self._mark("penalize_pack")
             t = ops.sample(logits, temp, top_p, top_k, seeds, plan["step"])
@@ -656,6 +663,24 @@ class LLMEngine:
             f[i], p[i], rp[i] = r.params.frequency_penalty, r.params.presence_penalty, r.params.repetition_penalty
         ops.apply_penalties(logits, *self.stager.stage([ids, cnt, n, f, p, rp]))
 
+    def _guide(self, logits, reqs):
+        """Constrained decoding: -inf on every token the grammar of a guided row does not allow next
+        (host matcher masks -> token_mask HIP kernel), before sampling."""
+        rows = [i for i, r in enumerate(reqs) if r is not None and r.matcher is not None and not r.finished]
+        if not rows:
+            return
+        if self._masks is None:
+            from .guided import MaskBuilder
+            self._masks = MaskBuilder()
+        words = (logits.shape[1] + 31) // 32
+        gw = max(reqs[i].params.guided.words for i in rows)
+        mask = self._masks.build(rows, [reqs[i].matcher for i in rows],
+                                 [reqs[i].max_new - len(reqs[i].output_ids) for i in rows], gw)
+        if gw < words:  # logits wider than the tokenizer's vocabulary: the extra ids stay disallowed
+            mask = np.concatenate([mask, np.zeros((len(rows), words - gw), np.int32)], 1)
+        mask = np.ascontiguousarray(mask[:, :words])
+        ops.token_mask(logits, *self._to_device([np.asarray(rows, np.int32), mask]))
+
     def _process(self, seq_order, reqs, toks, defer_append: bool = False) -> List[RequestOutput]:
         """Apply one sampled token per sequence. defer_append: the caller hands the tokens of
         continuing sequences to the scheduler itself (multi-step runs)."""
@@ -670,6 +695,8 @@ class LLMEngine:
             req.output_ids.append(t)
             if req.params.has_penalty:
                 req.token_counts[t] = req.token_counts.get(t, 0) + 1
+            if req.matcher is not None:
+                req.matcher.advance(int(t))
             ntok = len(req.output_ids)
             reason = None
             is_eos = (t in self.eos and not req.params.ignore_eos) or t in req.params.stop_token_ids
@@ -680,6 +707,8 @@ class LLMEngine:
                 delta = req.detok.add(t)
                 if req.detok.stopped:
                     reason = "stop"
+                elif req.matcher is not None and (req.matcher.done or req.matcher.dead):
+                    reason = "stop"  # the constrained value is complete
                 elif ntok >= req.params.max_tokens or len(req.prompt_ids) + ntok >= self.cfg.max_model_len:
                     reason = "length"
                 if reason:

@@ -55,7 +55,7 @@ def native_available() -> bool:
 
 
 EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6, "quick_gelu": 7}
-_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "large": 3}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
+_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "large": 3, "ring": 4}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -308,20 +308,36 @@ def enable_tuned_blas() -> bool:
 
     import torch.cuda.tunable as tunable
 
+    import atexit
+    import warnings
+
     tunable.enable(True)
     tunable.tuning_enable(False)
     tunable.record_untuned_enable(False)
-    # results are written back to the *current* filename at exit: point it at a scratch file
-    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"gai_tunableop_{os.getpid()}.csv"))
+    # results are written back to the *current* filename at exit: point it at a scratch file, removed
+    # again at exit
+    scratch = os.path.join(tempfile.gettempdir(), f"gai_tunableop_{os.getpid()}.csv")
+    tunable.set_filename(scratch)
+    atexit.register(lambda: os.path.exists(scratch) and os.remove(scratch))
     _TUNED_BLAS = bool(tunable.read_file(path))
+    if not _TUNED_BLAS:
+        # validator rows of another hipBLASLt / PyTorch build: the table does not apply
+        warnings.warn(f"TunableOp table {path} was rejected by this hipBLASLt/PyTorch build; "
+                      "using hipBLASLt's default heuristics")
+        tunable.enable(False)
     return _TUNED_BLAS
 
 
 class GemmTuner:
-    """Per-shape choice between the hand-written MFMA GEMM (fused epilogue) and hipBLASLt + an
-    elementwise epilogue kernel, decided by timing both on the first call of each (M-bucket, N, K,
-    epilogue) outside graph capture (engines warm their shapes up before capturing). Policy via
-    GAI_GEMM_POLICY = tune (default) | native | hipblaslt."""
+    """GEMM backend policy, GAI_GEMM_POLICY = tune (default) | native | hipblaslt.
+
+    native: every projection runs on the hand-written MFMA kernels (ring-pipelined 256x256 kernel for
+    prefill, weight-streaming split-K for decode) with their fused epilogues. tune: per-shape choice
+    between those and hipBLASLt + an elementwise epilogue kernel, decided by timing both on the first
+    call of each (M-bucket, N, K, epilogue) outside graph capture. hipblaslt: library GEMMs only.
+    Headline bench on MI355X (profiles/r2/bench_policy.json): native 13.38 q/s vs tune 14.86 q/s - the
+    ring kernel reaches 0.78-0.85x hipBLASLt at M = 16K and the M = 64 decode gate_up / lm_head still
+    trail it, so tune stays the default until they do."""
 
     def __init__(self):
         self.mode = os.environ.get("GAI_GEMM_POLICY", "tune")
@@ -488,6 +504,14 @@ def sample(logits, temperature, top_p, top_k, seeds, step: int, out=None):
     out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device) if out is None else out
     native().sample(logits, temperature, top_p, top_k, seeds, int(step), out)
     return out
+
+
+def token_mask(logits, rows, mask):
+    """Constrained decoding: logits[rows[r], t] = -inf where bit t of mask[r] (int32 words) is clear."""
+    if not logits.is_cuda:
+        return ref.token_mask(logits, rows, mask)
+    native().token_mask(logits, rows, mask)
+    return logits
 
 
 def apply_penalties(logits, tok_ids, tok_cnt, n, freq, pres, rep):

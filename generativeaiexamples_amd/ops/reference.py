@@ -208,6 +208,15 @@ def sample(logits, temperature, top_p, top_k, seeds, step, generator=None):
     return out
 
 
+def token_mask(logits, rows, mask):
+    V = logits.shape[1]
+    bits = (mask.long().unsqueeze(-1) >> torch.arange(32, device=mask.device)) & 1  # [R, W, 32]
+    allowed = bits.reshape(mask.shape[0], -1)[:, :V].bool()
+    for r, row in enumerate(rows.tolist()):
+        logits[row] = torch.where(allowed[r], logits[row], torch.full_like(logits[row], float("-inf")))
+    return logits
+
+
 def apply_penalties(logits, tok_ids, tok_cnt, n, freq, pres, rep):
     for b in range(logits.shape[0]):
         m = int(n[b])

@@ -163,7 +163,9 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = os.environ.get("GAI_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        # RCCL refuses two ranks on one device: a single-GPU rehearsal (GAI_SINGLE_DEVICE=1) uses gloo
+        single = os.environ.get("GAI_SINGLE_DEVICE") == "1"
+        backend = os.environ.get("GAI_DIST_BACKEND") or ("nccl" if use_gpu and not single else "gloo")
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend if world > 1 else "none")
     if sequence_parallel is None:
         sequence_parallel = os.environ.get("GAI_SEQUENCE_PARALLEL") == "1"

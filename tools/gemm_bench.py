@@ -1,0 +1,82 @@
+"""Prefill GEMM A/B: the hand-written kernels (ring / large) vs hipBLASLt (default + tuned table) on the
+Llama-3-8B projection shapes at M = 16384 (one 16K-token prefill chunk), random operands, interleaved
+rounds in one process (cdna_hip_programming §5.4 rules 24/25). One JSON line per shape.
+
+usage: python tools/gemm_bench.py [--m 16384] [--rounds 5] [--out FILE]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from generativeaiexamples_amd import ops  # noqa: E402
+
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          "e5_ffn_up": (4096, 1024), "e5_qkv": (3072, 1024)}
+
+
+def timeit(fn, iters=10):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    nat = ops.native()
+    rows = []
+    for name in a.shapes.split(","):
+        N, K = SHAPES[name]
+        M = a.m
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        arms = {"ring": lambda: nat.gemm(x, w, out, None, None, 0, 4),
+                "w4": lambda: nat.gemm(x, w, out, None, None, 0, 7),
+                "large": lambda: nat.gemm(x, w, out, None, None, 0, 3),
+                "hipblaslt": lambda: torch.mm(x, w.t())}
+        ts = {k: [] for k in arms}
+        for _ in range(a.rounds):
+            for k, f in arms.items():
+                ts[k].append(timeit(f))
+        fl = 2 * M * N * K
+        r = {"gemm": name, "M": M, "N": N, "K": K}
+        for k, v in ts.items():
+            v.sort()
+            r[f"{k}_ms"] = round(v[len(v) // 2], 4)
+            r[f"{k}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
+        r["ring_vs_blas"] = round(r["hipblaslt_ms"] / r["ring_ms"], 3)
+        r["w4_vs_blas"] = round(r["hipblaslt_ms"] / r["w4_ms"], 3)
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+    if ops.enable_tuned_blas():
+        for r in rows:
+            M, N, K = r["M"], r["N"], r["K"]
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+            t = sorted(timeit(lambda: torch.mm(x, w.t())) for _ in range(a.rounds))[a.rounds // 2]
+            r["hipblaslt_tuned_ms"] = round(t, 4)
+            r["hipblaslt_tuned_tflops"] = round(2 * M * N * K / t / 1e9, 1)
+            print(json.dumps({"gemm": r["gemm"], "tuned_tflops": r["hipblaslt_tuned_tflops"]}), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,26 @@
+"""Run one GEMM arm repeatedly (for rocprofv3 PMC passes): python tools/gemm_one.py ARM N K [M] [iters]
+ARM: ring | ring_noilv | large | blas (hipBLASLt)."""
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from generativeaiexamples_amd import ops  # noqa: E402
+
+arm, N, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+M = int(sys.argv[4]) if len(sys.argv) > 4 else 16384
+iters = int(sys.argv[5]) if len(sys.argv) > 5 else 30
+x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+force = {"ring": 4, "ring_noilv": 5, "ring_ilv2bar": 6, "large": 3}.get(arm)
+nat = ops.native()
+for _ in range(iters):
+    if force is None:
+        torch.mm(x, w.t(), out=out)
+    else:
+        nat.gemm(x, w, out, None, None, 0, force)
+torch.cuda.synchronize()
+print("done", arm, M, N, K)

@@ -1,0 +1,10 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r2e
+mkdir -p $O
+timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+for arm in ring blas; do
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES -d $O/p1_$arm -o p1 --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/p1_$arm.log 2>&1 || exit 3
+  timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM -d $O/p2_$arm -o p2 --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/p2_$arm.log 2>&1 || exit 4
+done
