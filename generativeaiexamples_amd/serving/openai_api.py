@@ -65,6 +65,9 @@ class ChatRequest(BaseModel):
     stream_options: Optional[Dict[str, Any]] = None
     ignore_eos: bool = False
     min_tokens: int = 0
+    # NIM / vLLM structured-generation extensions: {"guided_json": <schema>}
+    nvext: Optional[Dict[str, Any]] = None
+    guided_json: Optional[Union[Dict[str, Any], str]] = None
 
 
 class CompletionRequest(BaseModel):
@@ -170,6 +173,37 @@ def parse_tool_calls(text: str, tools: List[Dict[str, Any]]) -> Optional[List[Di
     return calls or None
 
 
+def guide_for(req, tok):
+    """Constrained-decoding grammar a chat request asks for (engine/guided.py), or None:
+    ``tool_choice: "required"`` / ``{"type": "function", "function": {"name": ...}}`` -> a tool-call
+    object whose parameters follow the chosen tool's schema; ``response_format`` json_schema /
+    json_object; ``guided_json`` (top level or under ``nvext``). ``tool_choice: "auto"`` stays free."""
+    from ..engine.guided import Guide
+
+    tools = getattr(req, "tools", None)
+    choice = getattr(req, "tool_choice", None)
+    if tools and choice not in (None, "auto", "none"):
+        name = None
+        if isinstance(choice, dict):
+            name = (choice.get("function") or {}).get("name")
+            if name is None:
+                raise ValueError("tool_choice object needs function.name")
+        elif choice != "required":
+            raise ValueError(f"unsupported tool_choice {choice!r}")
+        return Guide.tool_call(tools, tok, name)
+    gj = getattr(req, "guided_json", None) or ((getattr(req, "nvext", None) or {}).get("guided_json"))
+    if gj is not None:
+        return Guide.json_schema(json.loads(gj) if isinstance(gj, str) else gj, tok)
+    rf = getattr(req, "response_format", None) or {}
+    if rf.get("type") == "json_schema":
+        js = rf.get("json_schema") or {}
+        schema = js.get("schema", js if "type" in js or "properties" in js else None)
+        return Guide.json_schema(schema, tok) if schema else Guide.json_object(tok)
+    if rf.get("type") == "json_object":
+        return Guide.json_object(tok)
+    return None
+
+
 def _images_of(req: ChatRequest) -> List[str]:
     """OpenAI/NIM vision content parts: {"type": "image_url", "image_url": {"url": "data:image/...;base64,..."}}
     (W12 image_url chat); also accepts a bare string url field."""
@@ -269,6 +303,10 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
         tok = llm.tokenizer
         ids = apply_chat_template(_messages_for_template(req), tok)
         params = _params(req, hub.default_max_tokens)
+        try:
+            params.guided = guide_for(req, tok)
+        except (ValueError, KeyError) as e:  # SchemaError is a ValueError
+            return _err(400, f"structured output: {e}")
         images = _images_of(req) or None
         lora = hub.lora_for(req.model)
         if images and not hasattr(llm.engine.model, "register_request"):

@@ -97,3 +97,67 @@ def test_tool_call_parsing():
     assert json.loads(calls[0]["function"]["arguments"]) == {"city": "Austin"}
     assert parse_tool_calls("no tools here", tools) is None
     assert parse_tool_calls('{"name": "other", "parameters": {}}', tools) is None
+
+
+SCHEMA = {"type": "object", "properties": {"answer": {"type": "string", "maxLength": 20},
+                                           "confidence": {"type": "number"},
+                                           "sources": {"type": "array", "items": {"type": "integer"}, "maxItems": 3}},
+          "required": ["answer", "confidence"]}
+TOOLS = [{"type": "function", "function": {"name": "search", "parameters": {
+    "type": "object", "properties": {"query": {"type": "string", "maxLength": 16}}, "required": ["query"]}}},
+         {"type": "function", "function": {"name": "multiply", "parameters": {
+             "type": "object", "properties": {"a": {"type": "integer"}, "b": {"type": "integer"}},
+             "required": ["a", "b"]}}}]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_structured_output_json_schema(client, seed):
+    """with_structured_output: random-init weights, yet every answer parses and validates."""
+    from generativeaiexamples_amd.engine.guided import validate
+
+    r = client.post("/v1/chat/completions", json={
+        "max_tokens": 120, "temperature": 1.0, "seed": seed, "messages": [{"role": "user", "content": "q"}],
+        "response_format": {"type": "json_schema", "json_schema": {"name": "Answer", "schema": SCHEMA}}})
+    assert r.status_code == 200, r.text
+    v = json.loads(r.json()["choices"][0]["message"]["content"])
+    assert validate(v, SCHEMA)
+
+
+def test_structured_output_json_object_and_nvext(client):
+    r = client.post("/v1/chat/completions", json={"max_tokens": 80, "temperature": 1.0, "seed": 5,
+                                                   "messages": [{"role": "user", "content": "q"}],
+                                                   "response_format": {"type": "json_object"}})
+    assert isinstance(json.loads(r.json()["choices"][0]["message"]["content"]), dict)
+    r = client.post("/v1/chat/completions", json={"max_tokens": 40, "temperature": 1.0, "seed": 6,
+                                                   "messages": [{"role": "user", "content": "q"}],
+                                                   "nvext": {"guided_json": {"type": "array", "items": {"type": "boolean"},
+                                                                             "minItems": 2, "maxItems": 2}}})
+    v = json.loads(r.json()["choices"][0]["message"]["content"])
+    assert isinstance(v, list) and len(v) == 2 and all(isinstance(x, bool) for x in v)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_tool_choice_required_always_calls_a_declared_tool(client, seed):
+    """bind_tools(..., tool_choice="required"): the reply is always a valid call of a declared tool."""
+    from generativeaiexamples_amd.engine.guided import validate
+
+    r = client.post("/v1/chat/completions", json={"max_tokens": 100, "temperature": 1.0, "seed": seed,
+                                                   "messages": [{"role": "user", "content": "what is 3*4?"}],
+                                                   "tools": TOOLS, "tool_choice": "required"})
+    j = r.json()
+    assert j["choices"][0]["finish_reason"] == "tool_calls", j
+    call = j["choices"][0]["message"]["tool_calls"][0]["function"]
+    schema = next(t["function"]["parameters"] for t in TOOLS if t["function"]["name"] == call["name"])
+    assert validate(json.loads(call["arguments"]), schema)
+    r = client.post("/v1/chat/completions", json={"max_tokens": 100, "temperature": 1.0, "seed": seed,
+                                                   "messages": [{"role": "user", "content": "find mi355x"}],
+                                                   "tools": TOOLS,
+                                                   "tool_choice": {"type": "function", "function": {"name": "search"}}})
+    assert r.json()["choices"][0]["message"]["tool_calls"][0]["function"]["name"] == "search"
+
+
+def test_structured_output_bad_schema(client):
+    r = client.post("/v1/chat/completions", json={"max_tokens": 5, "messages": [{"role": "user", "content": "q"}],
+                                                   "response_format": {"type": "json_schema",
+                                                                       "json_schema": {"schema": {"type": "tuple"}}}})
+    assert r.status_code == 400

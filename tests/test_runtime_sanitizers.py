@@ -1,4 +1,4 @@
-"""Native runtime (block manager + scheduler) randomised self-test under ASan + UBSan."""
+"""Native runtime (block manager + scheduler + constrained-decoding matcher) randomised self-test under ASan + UBSan."""
 import os
 import shutil
 import subprocess
@@ -15,4 +15,5 @@ def test_runtime_selftest_asan_ubsan(tmp_path):
                        env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "runtime selftest OK" in r.stdout
+    assert "grammar selftest:" in r.stdout  # constrained-decoding matcher walks
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
