@@ -42,9 +42,7 @@ import argparse
 import json
 import os
 import random
-import socket
 import statistics
-import subprocess
 import sys
 import time
 
@@ -85,32 +83,6 @@ def parse():
     for c in CONFIGS:
         module(c).add_args(ap)
     return ap.parse_args()
-
-
-def spawn_ranks(n: int) -> int:
-    """Run this script as n ranks (one per GPU) when not already under a launcher; returns the worst exit
-    code. Children are started before this process touches the GPU; a failing rank stops the others."""
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    while procs:
-        for p in list(procs):
-            code = p.poll()
-            if code is None:
-                continue
-            procs.remove(p)
-            if code != 0:
-                rc = rc or code
-                for q in procs:
-                    q.terminate()
-        time.sleep(0.2)
-    return rc
 
 
 def log(*a):
@@ -207,6 +179,8 @@ def synthetic_question(q: int) -> str:
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from generativeaiexamples_amd.parallel.launch import spawn_ranks
+
         sys.exit(spawn_ranks(args.gpus))
     if args.config != 2:
         return run_other_config(args)

@@ -630,8 +630,9 @@ class LLMEngine:
 
     def release_followers(self, stop: bool = False) -> None:
         """Leader: hand control back to the followers' callers ('yield') or end their loops ('stop')."""
-        if self.chan is not None and self.leader:
+        if self.chan is not None and self.leader and not getattr(self, "_stopped", False):
             self.chan.send({"op": "stop" if stop else "yield"})
+            self._stopped = stop
 
     def _mark(self, phase: str):
         """GAI_STEP_TIMING=1: synchronise and accumulate wall time per step phase in ``self.phase_ms``."""

@@ -65,8 +65,9 @@ def _is_hf_dir(p: Optional[str]) -> bool:
     return bool(p) and os.path.isfile(os.path.join(p, "config.json"))
 
 
-def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=None, seed: int = 0):
-    """-> (model, tokenizer, served_name)."""
+def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=None, seed: int = 0, dtype=None):
+    """-> (model, tokenizer, served_name). Under a tensor-parallel context (parallel.dist.init_distributed
+    with tp_size > 1) Llama-family models are built as this rank's shard (checkpoints are sliced on load)."""
     if _is_hf_dir(weights):
         import json
 
@@ -75,6 +76,8 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
             m = OPTModel(OPTConfig.from_hf(weights), device=device)
         elif arch == "qwen3_next":
             m = Qwen3NextModel(Qwen3NextConfig.from_hf(weights), device=device)
+        elif dtype is not None:
+            m = LlamaModel(LlamaConfig.from_hf(weights), device=device, dtype=dtype)
         else:
             m = LlamaModel(LlamaConfig.from_hf(weights), device=device)
         m.load_safetensors_dir(weights) if hasattr(m, "load_safetensors_dir") else _load_st(m, weights)

@@ -1,0 +1,65 @@
+"""Single-node multi-rank launcher: one process per GPU, started before this process touches the GPU.
+
+``python bench.py --gpus N`` and ``python -m generativeaiexamples_amd.serving --tp N`` re-run themselves
+as N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set) unless they already
+run under torchrun. Children are plain subprocesses (never exec from a process that initialised HIP); a
+failing rank stops the others and its exit code is returned. SIGTERM / SIGINT are forwarded.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List, Optional
+
+
+def under_launcher() -> bool:
+    return "WORLD_SIZE" in os.environ
+
+
+def free_port() -> int:
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: Optional[List[str]] = None, script: Optional[str] = None) -> int:
+    """Run ``script argv`` (default: this program and its arguments) as n ranks; worst exit code."""
+    port = free_port()
+    script = script or os.path.abspath(sys.argv[0])
+    argv = sys.argv[1:] if argv is None else argv
+    cmd = [sys.executable, script] + argv if not script.startswith("-m ") else [sys.executable, "-m",
+                                                                                script[3:]] + argv
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc

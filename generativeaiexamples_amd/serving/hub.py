@@ -36,6 +36,10 @@ class HubSpec:
     kv_memory_fraction: float = 0.6
     lora_adapters: Dict[str, str] = field(default_factory=dict)
     device: Optional[str] = None
+    # tensor parallelism of the generator across the ranks of this job (one process per GPU, RCCL):
+    # rank 0 serves the API and plans every step, the other ranks execute its plans (LLMEngine.follow)
+    tp: int = 1
+    dtype: Optional[str] = None  # generator dtype override ("float32" for exact CPU rehearsals)
 
     @staticmethod
     def from_env() -> "HubSpec":
@@ -53,11 +57,13 @@ class HubSpec:
         s.max_num_seqs = int(g("APP_ENGINE_MAXBATCH", s.max_num_seqs))
         s.max_model_len = int(g("APP_ENGINE_MAXMODELLEN", s.max_model_len))
         s.device = g("APP_ENGINE_DEVICE")
+        s.tp = int(g("APP_ENGINE_TP", s.tp))
         return s
 
 
 class ServiceHub:
     def __init__(self):
+        self.follower_engine: Optional[LLMEngine] = None  # TP follower ranks: the engine they execute
         self.llms: Dict[str, AsyncLLMEngine] = {}
         self.embedders: Dict[str, Embedder] = {}
         self.rerankers: Dict[str, Reranker] = {}
@@ -131,6 +137,18 @@ class ServiceHub:
     def shutdown(self):
         for a in self.llms.values():
             a.shutdown()
+            a.engine.release_followers(stop=True)  # TP: end the followers' plan loops
+
+    @property
+    def is_follower(self) -> bool:
+        return self.follower_engine is not None
+
+    def serve_follower(self) -> str:
+        """TP follower ranks: execute rank 0's step plans until it stops serving."""
+        op = "yield"
+        while op == "yield":
+            op = self.follower_engine.follow()
+        return op
 
     # ---------------------------------------------------------------- construction
     @classmethod
@@ -141,12 +159,23 @@ class ServiceHub:
 
         dev = torch.device(spec.device) if spec.device else default_device()
         hub = cls()
+        if spec.tp > 1:
+            from ..parallel.dist import init_distributed
+
+            ctx = init_distributed(tp_size=spec.tp)
+            if ctx.world_size != spec.tp:
+                raise ValueError(f"tp={spec.tp} needs a job of exactly {spec.tp} ranks (WORLD_SIZE={ctx.world_size})")
+            dev = ctx.device if dev.type == "cuda" else dev
+        dtype = getattr(torch, spec.dtype) if spec.dtype else None
         if spec.llm:
-            m, tok, name = build_llm(spec.llm, spec.llm_weights, device=dev)
+            m, tok, name = build_llm(spec.llm, spec.llm_weights, device=dev, dtype=dtype)
             eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=spec.max_num_seqs, max_model_len=spec.max_model_len,
                                                  max_batched_tokens=spec.max_batched_tokens,
                                                  use_graphs=spec.use_graphs and dev.type == "cuda",
                                                  kv_memory_fraction=spec.kv_memory_fraction))
+            if not eng.leader:  # TP follower: no API, no embedder / reranker
+                hub.follower_engine = eng
+                return hub
             hub.add_llm(spec.served_llm_name or name, eng)
             for alias, path in spec.lora_adapters.items():
                 hub.add_alias(alias, spec.served_llm_name or name)

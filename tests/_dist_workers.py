@@ -432,3 +432,83 @@ def tp_engine_worker(rank, world, port, out_dir):
                    "multi": multi, "plans": eng.chan.sent}, f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def write_tiny_llama_ckpt(path, seed=21):
+    """A tiny Llama in HF layout (config.json + model.safetensors) for checkpoint-serving tests."""
+    import json
+
+    from safetensors.torch import save_file
+
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+
+    cfg = LlamaConfig.tiny(num_heads=8, num_kv_heads=4, head_dim=32, hidden_size=256, intermediate_size=512,
+                           vocab_size=512)
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32, dist_ctx=DistContext()).random_init(seed)
+    os.makedirs(path, exist_ok=True)
+    save_file({k: v.contiguous() for k, v in m.export_hf_state().items()}, os.path.join(path, "model.safetensors"))
+    with open(os.path.join(path, "config.json"), "w") as f:
+        json.dump({"model_type": "llama", "vocab_size": 512, "hidden_size": 256, "intermediate_size": 512,
+                   "num_hidden_layers": cfg.num_layers, "num_attention_heads": 8, "num_key_value_heads": 4,
+                   "head_dim": 32, "max_position_embeddings": 2048, "rms_norm_eps": cfg.rms_eps,
+                   "rope_theta": cfg.rope_theta, "bos_token_id": 1, "eos_token_id": 2,
+                   "tie_word_embeddings": False}, f)
+
+
+def tp_serving_worker(rank, world, port, out_dir, ckpt):
+    """`/v1` serving of a TP=world generator: rank 0 runs the API (ServiceHub + FastAPI), the other ranks
+    follow its step plans; completions must equal a single-process engine on the same checkpoint, a
+    client-side abort mid-stream must not desynchronise the ranks, and shutdown must end the followers."""
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from generativeaiexamples_amd.serving.hub import HubSpec, ServiceHub
+
+    spec = HubSpec(llm="tiny-llama", llm_weights=ckpt, embedder=None, device="cpu", tp=world, dtype="float32",
+                   max_num_seqs=8, max_model_len=512, max_batched_tokens=64, use_graphs=False)
+    hub = ServiceHub.build(spec)
+    if hub.is_follower:
+        assert hub.serve_follower() == "stop"
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    from fastapi.testclient import TestClient
+
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import apply_chat_template
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd.serving.openai_api import create_openai_app
+
+    msgs = [[{"role": "user", "content": f"question {i}: " + "x" * (7 * i)}] for i in range(3)]
+    res = {"api": [], "stream_ok": False}
+    with TestClient(create_openai_app(hub)) as c:
+        for m in msgs:
+            r = c.post("/v1/chat/completions", json={"messages": m, "max_tokens": 12, "temperature": 0,
+                                                      "ignore_eos": True})
+            assert r.status_code == 200, r.text
+            res["api"].append(r.json()["choices"][0]["message"]["content"])
+        # client disconnects after two chunks: the request is aborted on rank 0 only
+        with c.stream("POST", "/v1/chat/completions", json={"messages": msgs[0], "max_tokens": 200, "stream": True,
+                                                             "ignore_eos": True}) as s:
+            for i, _ in enumerate(s.iter_lines()):
+                if i > 2:
+                    break
+        r = c.post("/v1/chat/completions", json={"messages": msgs[1], "max_tokens": 12, "temperature": 0,
+                                                  "ignore_eos": True})
+        res["after_abort"] = r.json()["choices"][0]["message"]["content"]
+    tok = hub.llm().tokenizer
+    hub.shutdown()
+    ref = LlamaModel(LlamaConfig.from_hf(ckpt), device="cpu", dtype=torch.float32,
+                     dist_ctx=DistContext()).load_safetensors_dir(ckpt)
+    eng = LLMEngine(ref, tok, EngineConfig(max_num_seqs=8, max_model_len=512, max_batched_tokens=64,
+                                           use_graphs=False))
+    outs = eng.generate([apply_chat_template(m, tok) for m in msgs],
+                        SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True))
+    res["ref"] = [o.text for o in outs]
+    with open(os.path.join(out_dir, "tp_serving.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()

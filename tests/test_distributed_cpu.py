@@ -71,3 +71,18 @@ def test_tp_engine_follows_leader_plans(tmp_path, world):
     assert d["tp"] == d["ref"], (d["tp"], d["ref"])
     assert d["victim"] == "abort" and d["victim_len"] < 40
     assert d["free_ok"] and d["multi"] > 0 and d["plans"] > 5
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_serving_hub(tmp_path, world):
+    """/v1 chat on a TP=world generator served from rank 0 == single-process engine on the same checkpoint;
+    an aborted stream leaves the ranks in step; shutdown ends the follower loops."""
+    import json
+
+    ckpt = str(tmp_path / "ckpt")
+    W.write_tiny_llama_ckpt(ckpt)
+    mp.spawn(W.tp_serving_worker, args=(world, _port(), str(tmp_path), ckpt), nprocs=world, join=True)
+    d = json.loads((tmp_path / "tp_serving.json").read_text())
+    assert d["api"] == d["ref"], (d["api"], d["ref"])
+    assert d["after_abort"] == d["ref"][1]
