@@ -13,6 +13,8 @@
 //   insertion; after warm-up almost every candidate is rejected by one compare).
 //   The workgroup's lists are merged through LDS into one list per query.
 //   stage 2: one workgroup per query merges the per-workgroup lists.
+#include <algorithm>
+
 #include "gai_common.h"
 #include "gai_kernels.h"
 
@@ -155,6 +157,150 @@ __global__ __launch_bounds__(512) void sim_topk_stage1(const bf16* __restrict__ 
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Streaming stage 1 for k <= 8 (the RAG path: top-4 of 1M-10M rows): one workgroup per CU-sized row
+// range, X streamed at HBM rate.
+//  * operands swapped (MFMA A = 16 X rows, B = 16 queries): lane l ends a 16-row group owning query
+//    l&15 (+16i) and rows 4(l>>4)..+3 - it inserts its 4 candidates straight from the accumulator, no LDS
+//    transpose, no wave barrier per group;
+//  * X fragments flow through a 16-deep register ring (16 KiB in flight per wave) that runs across
+//    group boundaries: the two 64-B halves of every 128-B X line are issued back to back;
+//  * per-lane register top-K lists; the 32 lists of a query (8 waves x 4 row-lanes) are merged in LDS
+//    once at the end.
+// ------------------------------------------------------------------------------------------------
+template <int MT, int K, int RING>
+__global__ __launch_bounds__(512) void sim_topk_stream(const bf16* __restrict__ Q, const bf16* __restrict__ X,
+                                                       const float* __restrict__ bias, int nq, int N, int D,
+                                                       int rows_per_wg, float* __restrict__ ws_v,
+                                                       int* __restrict__ ws_i) {
+  constexpr int NQ = 16 * MT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* qimg = smem;
+  float* bsm = reinterpret_cast<float*>(smem + (size_t)NQ * D * 2);  // this workgroup's bias rows
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q0 = blockIdx.y * NQ;
+  const int ncols = D / 8;
+  const int wg_row0 = blockIdx.x * rows_per_wg;
+  for (int e = tid; e < NQ * ncols; e += 512) {
+    const int r = e / ncols, u = e % ncols;
+    bf16x8 v = (q0 + r < nq) ? load8(Q + (size_t)(q0 + r) * D + u * 8) : bf16x8{};
+    *reinterpret_cast<bf16x8*>(qimg + (size_t)r * D * 2 + ((u ^ (r & 15)) << 4)) = v;
+  }
+  // bias through LDS: a global load inside the X stream would make every wait drain the ring
+  for (int r = tid; r < rows_per_wg; r += 512) bsm[r] = wg_row0 + r < N ? bias[wg_row0 + r] : -INFINITY;
+  __syncthreads();
+
+  TopK<K> tk[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) tk[i].init();
+  const int wave_rows = rows_per_wg / 8;  // multiple of 16
+  const int r_begin = wg_row0 + wid * wave_rows;
+  const int r_end = min(N, r_begin + wave_rows);
+  const int ngroups = r_end > r_begin ? (r_end - r_begin + 15) / 16 : 0;
+  const int nk = D / 32;             // k-steps per 16-row group; RING divides it
+  const int total = ngroups * nk;    // a multiple of RING: no tail guard inside the stream
+  // the stream position advances by RING k-steps per chunk; pointers are stepped, never divided
+  const bf16* const xlast = X + (size_t)(N - 1) * D + (D - 32) + 8 * (lane >> 4);
+  const bf16* xrow = X + (size_t)min(r_begin + (lane & 15), N - 1) * D + 8 * (lane >> 4);  // group g row
+  const size_t gstep = (size_t)16 * D;                                                    // next group
+  int pf_t = 0;                  // k-step of the prefetch pointer within its group
+  const bf16* pf = xrow;         // prefetch pointer (k-step j0 + RING)
+  auto advance_pf = [&]() {      // RING k-steps ahead
+    pf_t += RING;
+    if (pf_t == nk) {
+      pf_t = 0;
+      pf += gstep - (size_t)32 * (nk - RING);
+    } else {
+      pf += 32 * RING;
+    }
+  };
+  bf16x8 ring[RING];
+#pragma unroll
+  for (int u = 0; u < RING; ++u) ring[u] = load8(pf + 32 * u);
+  advance_pf();
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int g = 0, t0 = 0;
+  for (int j0 = 0; j0 < total; j0 += RING) {
+    // past the stream's end the prefetch re-reads the last row (clamped, harmless)
+    const bf16* p = j0 + RING < total ? pf : xlast - 32 * (RING - 1);
+    // query fragments one k-step ahead (LDS latency hides under the previous step's MFMAs)
+    auto rdq = [&](bf16x8* qf, int t) {
+      const int uu = 4 * t + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int qr = 16 * i + (lane & 15);
+        qf[i] = *reinterpret_cast<const bf16x8*>(qimg + (size_t)qr * D * 2 + ((uu ^ (qr & 15)) << 4));
+      }
+    };
+    bf16x8 qa[MT], qb[MT];
+    rdq(qa, t0);
+#pragma unroll
+    for (int u = 0; u < RING; ++u) {
+      bf16x8* qc = (u & 1) ? qb : qa;
+      bf16x8* qn = (u & 1) ? qa : qb;
+      if (u + 1 < RING) rdq(qn, t0 + u + 1);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[u], qc[i], acc[i], 0, 0, 0);  // D[x row][query]
+      ring[u] = load8(p + 32 * u);  // consumed first, then refilled: the slot keeps its registers
+    }
+    advance_pf();
+    t0 += RING;
+    if (t0 == nk) {  // a 16-row group is complete: 4 candidate rows per lane and query tile
+      const int rl = r_begin - wg_row0 + 16 * g + 4 * (lane >> 4);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(bsm + rl);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wg_row0 + rl + r;
+        if (row < r_end) {
+#pragma unroll
+          for (int i = 0; i < MT; ++i) tk[i].insert(acc[i][r] + bv[r], row);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      t0 = 0;
+      ++g;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // merge the 32 lists of every query (list = 4 * wave + row-lane group) in LDS (aliases the Q image)
+  __syncthreads();
+  float* mv = reinterpret_cast<float*>(smem);
+  int* mi = reinterpret_cast<int*>(smem + (size_t)NQ * 32 * K * 4);
+  const int list = wid * 4 + (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int q = 16 * i + (lane & 15);
+#pragma unroll
+    for (int jj = 0; jj < K; ++jj) {
+      mv[(q * 32 + list) * K + jj] = tk[i].v[jj];
+      mi[(q * 32 + list) * K + jj] = tk[i].i[jj];
+    }
+  }
+  __syncthreads();
+  if (tid < NQ && q0 + tid < nq) {
+    TopK<K> m;
+    m.init();
+    for (int l = 0; l < 32; ++l)
+      for (int jj = 0; jj < K; ++jj) {
+        const float v = mv[(tid * 32 + l) * K + jj];
+        if (!(v > m.v[K - 1])) break;
+        m.insert(v, mi[(tid * 32 + l) * K + jj]);
+      }
+    const size_t base = ((size_t)blockIdx.x * nq + q0 + tid) * K;
+#pragma unroll
+    for (int jj = 0; jj < K; ++jj) {
+      ws_v[base + jj] = m.v[jj];
+      ws_i[base + jj] = m.i[jj];
+    }
+  }
+}
+
 // stage 2: one 256-thread workgroup per query merges nwg lists of K.
 template <int K>
 __global__ __launch_bounds__(256) void sim_topk_stage2(const float* __restrict__ ws_v, const int* __restrict__ ws_i,
@@ -226,9 +372,49 @@ void run_topk(const void* Q, const void* X, const float* bias, int nq, int N, in
   GAI_LAUNCH_CHECK();
 }
 
+template <int MT, int K, int RING>
+void run_stream_r(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,
+                  int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st) {
+  constexpr int NQ = 16 * MT;
+  const size_t lds = std::max((size_t)NQ * D * 2 + (size_t)rows_per_wg * 4, (size_t)NQ * 32 * K * 8);
+  auto k1 = sim_topk_stream<MT, K, RING>;
+  static bool once = false;
+  if (!once) {
+    set_max_lds(k1, 160 * 1024);
+    once = true;
+  }
+  const int qtiles = (nq + NQ - 1) / NQ;
+  k1<<<dim3(nwg, qtiles), 512, lds, st>>>((const bf16*)Q, (const bf16*)X, bias, nq, N, D, rows_per_wg, ws_v, ws_i);
+  GAI_LAUNCH_CHECK();
+  sim_topk_stage2<K><<<nq, 256, 0, st>>>(ws_v, ws_i, nwg, nq, k, out_v, out_i);
+  GAI_LAUNCH_CHECK();
+}
+
+template <int MT, int K>
+void run_stream(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v, int* ws_i,
+                int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st) {
+  const int nk = D / 32;
+  if (nk % 16 == 0) return run_stream_r<MT, K, 16>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+  if (nk % 8 == 0) return run_stream_r<MT, K, 8>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+  if (nk % 4 == 0) return run_stream_r<MT, K, 4>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+  return run_stream_r<MT, K, 1>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+}
+
 template <int K>
 void run_topk_k(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v, int* ws_i,
                 int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st) {
+  if constexpr (K <= 8) {
+    // streaming kernel (host sizes rows_per_wg as a multiple of 128 for it)
+    if (rows_per_wg % 128 == 0 && rows_per_wg <= 8192) {
+      auto fits = [&](int nq_tile) { return (size_t)nq_tile * D * 2 + (size_t)rows_per_wg * 4 <= 160 * 1024; };
+      if (nq > 32 && fits(64))
+        return run_stream<4, K>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+      if (nq > 16 && fits(32))
+        return run_stream<2, K>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+      if (fits(16))
+        return run_stream<1, K>(Q, X, bias, nq, N, D, k, ws_v, ws_i, nwg, rows_per_wg, out_v, out_i, st);
+    }
+  }
   // largest query tile that fits LDS (Q image + scratch, with room for the K-merge buffer)
   auto fits = [&](int mt) {
     const size_t lds = (size_t)16 * mt * D * 2 + (size_t)8 * 16 * mt * 17 * 4;

@@ -536,8 +536,12 @@ def sim_topk(Q: torch.Tensor, X: torch.Tensor, bias: torch.Tensor, n_rows: int, 
     if not Q.is_cuda or n_rows == 0:
         return ref.sim_topk(Q, X, bias, n_rows, k_eff)
     nq = Q.shape[0]
-    rows_per_wg = max(128, ((n_rows + 1023) // 1024 + 127) // 128 * 128)
-    rows_per_wg = min(rows_per_wg, 8192)
+    if topk_cap(k_eff) <= 8:
+        # streaming kernel: ~one workgroup per CU, its bias rows staged in LDS (<= 4096 rows)
+        rows_per_wg = min(4096, max(128, ((n_rows + 255) // 256 + 127) // 128 * 128))
+    else:
+        rows_per_wg = max(128, ((n_rows + 1023) // 1024 + 127) // 128 * 128)
+        rows_per_wg = min(rows_per_wg, 8192)
     nwg = (n_rows + rows_per_wg - 1) // rows_per_wg
     cap = topk_cap(k_eff)
     ws_v = torch.empty(nwg * nq * cap, dtype=torch.float32, device=Q.device)

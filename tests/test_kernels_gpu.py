@@ -228,6 +228,24 @@ def test_sim_topk(cuda, nq, N, D, k):
     assert (i.cpu() % 7 != 0).all()
 
 
+@pytest.mark.parametrize("nq", [1, 16, 40, 64])
+def test_sim_topk_stream_large(cuda, nq):
+    """Streaming k <= 8 path at index scale (1M rows, several workgroups per CU-range), vs fp32 torch."""
+    torch.manual_seed(nq)
+    N, D = 1_000_003, 1024
+    X = torch.randn(N, D, device=cuda, dtype=torch.bfloat16)
+    Q = torch.randn(nq, D, device=cuda, dtype=torch.bfloat16)
+    bias = torch.zeros(N, device=cuda)
+    bias[5::11] = float("-inf")
+    for k in (4, 8):
+        v, i = ops.sim_topk(Q, X, bias, N, k)
+        s = Q.float() @ X.float().t() + bias
+        vr, _ = torch.topk(s, k, dim=-1)
+        _close(v, vr, 2e-2, 2e-3, f"stream topk k={k}")
+        _close(torch.gather(s, 1, i), vr, 2e-2, 2e-3, "scores of returned ids")
+        assert ((i % 11) != 5).all() and (i < N).all()
+
+
 def test_embedding_pool_act(cuda):
     torch.manual_seed(10)
     table = torch.randn(1000, 256, device=cuda, dtype=torch.bfloat16)
