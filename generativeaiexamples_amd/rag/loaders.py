@@ -30,11 +30,21 @@ def load(path: str, filename: str | None = None) -> List[Document]:
     meta = {"source": path, "filename": filename}
     with open(path, "rb") as f:
         data = f.read()
-    if ext == ".pdf":
-        pages = pdf_pages(data)
+    if ext in (".pdf", ".pptx"):
+        # structured parse (rag/pdf.py: ToUnicode / CID fonts, ruled tables, layout); images need a vision
+        # model and are handled by the multimodal example
+        from .multimodal_ingest import pdf_documents, pptx_documents
+
+        try:
+            docs = (pdf_documents if ext == ".pdf" else pptx_documents)(data, filename)
+        except Exception:  # a file the structured parser cannot read: fall back to the stream scan
+            docs = []
+        docs = [Document(d.page_content, dict(meta, **{k: v for k, v in d.metadata.items() if k != "source"}))
+                for d in docs if d.metadata.get("type") != "image" and d.page_content.strip()]
+        if docs:
+            return docs
+        pages = pdf_pages(data) if ext == ".pdf" else pptx_slides(data)
         return [Document(t, dict(meta, page=i + 1)) for i, t in enumerate(pages) if t.strip()]
-    if ext == ".pptx":
-        return [Document(t, dict(meta, page=i + 1)) for i, t in enumerate(pptx_slides(data)) if t.strip()]
     if ext == ".docx":
         return [Document(docx_text(data), meta)]
     if ext in (".html", ".htm", ".xml"):

@@ -141,7 +141,7 @@ class AsyncLLMEngine:
                     self.engine.abort(rid)
 
     def generate_sync(self, prompt_ids: List[int], params: SamplingParams,
-                      request_id: Optional[str] = None) -> Iterator[StreamItem]:
+                      request_id: Optional[str] = None, images: Optional[list] = None) -> Iterator[StreamItem]:
         """Blocking streaming API for worker threads (chain-server example pipelines)."""
         import queue as _q
 
@@ -156,7 +156,7 @@ class AsyncLLMEngine:
         self.queues[rid] = (_Shim, q)
         t0 = time.perf_counter()
         with self.cv:
-            req = self.engine.add_request(prompt_ids, params, rid)
+            req = self.engine.add_request(prompt_ids, params, rid, images=images)
             self.cv.notify()
         METRICS.requests_total.inc()
         if req.finished:
