@@ -512,3 +512,47 @@ def tp_serving_worker(rank, world, port, out_dir, ckpt):
         json.dump(res, f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def interleave_dp(iters):
+    """One process replaying a DP=len(iters) job: each global batch = the ranks' micro-batches stacked."""
+    while True:
+        parts = [next(it) for it in iters]
+        yield torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+
+
+def full_sft_worker(rank, world, tp, port, out_dir):
+    """Full-weight SFT at TP=tp x DP=world/tp. Every rank also replays the job in one process (TP=1, the DP
+    ranks' micro-batches stacked) and compares its own shard of those weights with what it trained."""
+    import json
+
+    ctx = _init(rank, world, port, tp)
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.llama import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd.training.data import batches, synthetic_rows
+    from generativeaiexamples_amd.training.full import FullTrainer
+    from generativeaiexamples_amd.training.trainer import TrainConfig
+
+    cfg = LlamaConfig.tiny(num_layers=2, num_heads=4, num_kv_heads=2, head_dim=32, hidden_size=128,
+                           intermediate_size=256)
+    init = LlamaModel(cfg, device="cpu", dist_ctx=DistContext(), dtype=torch.float32).random_init(seed=5)
+    sd0 = init.export_hf_state()
+    m = LlamaModel(cfg, device="cpu", dist_ctx=ctx, dtype=torch.float32).load_hf_state(sd0)
+    tok = small_byte_tokenizer(512)
+    rows = synthetic_rows(64)
+    dpn, dp = ctx.dp_size, ctx.dp_rank
+    tcfg = dict(steps=3, global_batch=dpn, seq_len=64, lr=1e-3, warmup=1)
+    tr = FullTrainer(m, tok, TrainConfig(micro_batch=1, **tcfg), batches(rows[dp::dpn], tok, 64, 1, seed=dp))
+    hist = tr.train()
+    one = LlamaModel(cfg, device="cpu", dist_ctx=DistContext(), dtype=torch.float32).load_hf_state(sd0)
+    ref = FullTrainer(one, tok, TrainConfig(micro_batch=dpn, **tcfg),
+                      interleave_dp([batches(rows[d::dpn], tok, 64, 1, seed=d) for d in range(dpn)]))
+    ref_hist = ref.train()
+    mine = LlamaModel(cfg, device="cpu", dist_ctx=ctx, dtype=torch.float32).load_hf_state(
+        {k: v.detach() for k, v in one.export_hf_state().items()})
+    err = max(float((m.w[k].detach() - mine.w[k]).abs().max()) for k in m.w)
+    with open(os.path.join(out_dir, f"full_sft_{rank}.json"), "w") as f:
+        json.dump({"loss": hist, "ref_loss": ref_hist, "max_err": err}, f)
+    dist.barrier()
+    dist.destroy_process_group()

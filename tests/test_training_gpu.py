@@ -44,3 +44,24 @@ def test_embed_finetune_on_gpu(cuda):
         train_side = ft._encode(texts, "passage").float()
     serve_side = emb.embed(texts, "passage").float()
     torch.testing.assert_close(train_side, serve_side, rtol=0, atol=5e-2)
+
+
+def test_full_weight_pretrain_gpu(cuda):
+    """From-scratch pretraining of a small Llama in bf16 on the GPU (fp32 masters + AdamW): loss falls."""
+    import torch
+
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.llama import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd.rag import synthetic
+    from generativeaiexamples_amd.training.full import FullTrainer, pretrain_batches
+    from generativeaiexamples_amd.training.trainer import TrainConfig
+
+    tok = small_byte_tokenizer(512)
+    m = LlamaModel(LlamaConfig.tiny(num_layers=4), device=cuda, dist_ctx=DistContext()).random_init(1)
+    texts = [synthetic.chunk_document(i, 120).page_content for i in range(200)]
+    tr = FullTrainer(m, tok, TrainConfig(steps=30, global_batch=8, micro_batch=8, seq_len=128, lr=2e-3, warmup=3),
+                     pretrain_batches(texts, tok, 128, 8))
+    h = tr.train()
+    assert h[-1] < h[0] - 1.0, h
+    assert all(p.dtype == torch.bfloat16 for p in tr.params) and all(mm.dtype == torch.float32 for mm in tr.master)
