@@ -6,6 +6,10 @@ knowledge base is on, like pages/converse.py:100-119) and ``/kb`` (upload, list 
 5 s - and delete documents). The browser talks to this server's ``/api/*`` routes, which forward to
 the chain server through :class:`ChatClient`, so the chain server needs no CORS exposure.
 Config: ``APP_SERVERURL`` / ``APP_SERVERPORT`` / ``APP_MODELNAME`` (same names as the reference).
+``/speech`` is the reference's speech playground (rag_playground/speech): microphone -> streaming ASR into
+the question box, answers read back by TTS, through the pluggable backend of :mod:`.speech`
+(``RIVA_API_URI``; routes ``/api/speech/status``, ``/api/speech/asr`` (WAV in), ``/api/speech/tts``
+(WAV out)).
 """
 from __future__ import annotations
 
@@ -25,7 +29,7 @@ STATIC = Path(__file__).parent / "static"
 
 
 def create_app(server_url: str | None = None, model_name: str | None = None,
-               client: ChatClient | None = None) -> FastAPI:
+               client: ChatClient | None = None, speech=None) -> FastAPI:
     host = server_url or os.environ.get("APP_SERVERURL", "http://localhost")
     port = os.environ.get("APP_SERVERPORT", "8081")
     if server_url is None and ":" not in host.split("//")[-1]:
@@ -33,6 +37,10 @@ def create_app(server_url: str | None = None, model_name: str | None = None,
     client = client or ChatClient(host, model_name or os.environ.get("APP_MODELNAME", "meta/llama3-8b-instruct"))
     app = FastAPI(title="RAG Playground")
     app.state.client = client
+    from .speech import backend_from_env, pcm_chunks, pcm_to_wav, wav_to_pcm16
+
+    speech = speech if speech is not None else backend_from_env()
+    app.state.speech = speech
     app.mount("/static", StaticFiles(directory=STATIC), name="static")
 
     @app.get("/")
@@ -90,6 +98,54 @@ def create_app(server_url: str | None = None, model_name: str | None = None,
             except Exception as e:
                 return JSONResponse(status_code=500, content={"message": str(e)})
         return {"uploaded": names}
+
+    @app.get("/speech")
+    async def speech_page():
+        return FileResponse(STATIC / "speech.html")
+
+    @app.get("/api/speech/status")
+    async def speech_status():
+        ok = speech.available()
+        return {"asr": ok, "tts": ok, "message": "" if ok else
+                "Speech is unavailable: set RIVA_API_URI to a Riva server with ASR / TTS enabled."}
+
+    @app.post("/api/speech/asr")
+    async def speech_asr(req: Request):
+        if not speech.available():
+            return JSONResponse(status_code=503, content={"message": "no ASR service configured"})
+        lang = req.query_params.get("language", "en-US")
+        pcm = wav_to_pcm16(await req.body(), 16000)
+
+        def run():
+            last = ""
+            for last in speech.transcribe(pcm_chunks(pcm, 16000), lang, 16000):
+                pass
+            return last
+
+        try:
+            return {"transcript": await run_in_threadpool(run)}
+        except Exception as e:
+            return JSONResponse(status_code=502, content={"message": f"ASR failed: {e}"})
+
+    @app.post("/api/speech/tts")
+    async def speech_tts(req: Request):
+        if not speech.available():
+            return JSONResponse(status_code=503, content={"message": "no TTS service configured"})
+        body = await req.json()
+        text = (body.get("text") or "").strip()
+        if not text:
+            return JSONResponse(status_code=400, content={"message": "no text to synthesize"})
+
+        def run():
+            return b"".join(speech.synthesize(text, body.get("language", "en-US"), body.get("voice", "")))
+
+        try:
+            pcm = await run_in_threadpool(run)
+        except Exception as e:
+            return JSONResponse(status_code=502, content={"message": f"TTS failed: {e}"})
+        from fastapi.responses import Response
+
+        return Response(pcm_to_wav(pcm, speech.sample_rate_tts), media_type="audio/wav")
 
     @app.get("/health")
     async def health():
