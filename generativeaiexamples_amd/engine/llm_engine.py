@@ -171,7 +171,10 @@ class LLMEngine:
             nbytes = self.cfg.kv_memory_bytes
         elif self.device.type == "cuda":
             free, _total = torch.cuda.mem_get_info(self.device)
-            nbytes = int(free * self.cfg.kv_memory_fraction)
+            frac = self.cfg.kv_memory_fraction
+            if os.environ.get("GAI_SINGLE_DEVICE") == "1":  # rehearsal: every rank shares this one GPU
+                frac /= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+            nbytes = int(free * frac)
         else:
             nbytes = 256 << 20
         nb = KVCache.blocks_for_memory(nbytes, self._kv_layers(), self.model.hkv, mc.head_dim, self.model.dtype)
