@@ -75,6 +75,9 @@ def parse():
                     help="enable KV prefix caching (off by default: random-init embeddings retrieve the same "
                          "chunks for every query, so caching would skip most of the prefill work)")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache size per rank (default: 50%% of free HBM)")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="fp8 = OCP e4m3fn KV cache (an option, not the headline configuration: the JSON line "
+                         "reports it in config.kv_cache_dtype)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-plant", action="store_true", help="do not plant per-query relevant chunks")
     ap.add_argument("--no-probes", action="store_true", help="skip the untimed c1 / open-loop TTFT probes")
@@ -242,7 +245,8 @@ def main():
                         decode_steps=args.decode_steps,
                         prefix_cache=args.prefix_cache,
                         kv_memory_fraction=0.5,
-                        kv_memory_bytes=int(args.kv_gb * (1 << 30)) if args.kv_gb else None)
+                        kv_memory_bytes=int(args.kv_gb * (1 << 30)) if args.kv_gb else None,
+                        kv_cache_dtype=args.kv_cache_dtype)
     engine = LLMEngine(llm, ltok, ecfg)
     if not args.no_graphs:
         engine.capture_graphs(max_bs=args.batch)
@@ -385,6 +389,7 @@ def main():
             "prompt_tokens": int(statistics.mean(plens)),
             "max_tokens": args.max_tokens,
             "top_k": args.top_k,
+            "kv_cache_dtype": "bf16" if args.kv_cache_dtype == "auto" else "fp8_e4m3",
         },
         "p50_ttft_s": round(p50, 4),
         "p90_ttft_s": round(p90, 4),

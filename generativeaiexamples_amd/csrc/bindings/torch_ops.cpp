@@ -66,21 +66,33 @@ void layernorm(const Tensor& x, const Tensor& w, const optional<Tensor>& b, doub
                 opt_ptr(b), out.data_ptr(), T, D, (float)eps, cur_stream());
 }
 
+// KV caches are bf16, or 1-byte OCP e4m3fn (torch.float8_e4m3fn / uint8 storage) for the fp8 KV option
+int kv_cache_fp8(const Tensor& k, const Tensor& v) {
+  check_dev(k, "k_cache");
+  check_dev(v, "v_cache");
+  TORCH_CHECK(k.scalar_type() == v.scalar_type(), "k / v caches must share a dtype");
+  const auto t = k.scalar_type();
+  if (t == at::kBFloat16) return 0;
+  TORCH_CHECK(t == at::kFloat8_e4m3fn || t == at::kByte, "KV cache must be bf16 or float8_e4m3fn");
+  TORCH_CHECK(k.is_contiguous() && v.is_contiguous(), "KV caches must be contiguous");
+  return 1;
+}
+
 void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, const Tensor& slots, Tensor& q_out,
-                   Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, bool rope) {
+                   Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, bool rope, double k_scale,
+                   double v_scale) {
   check_bf16(qkv, "qkv");
   check_i32(pos, "positions");
   check_f32(cos_sin, "cos_sin");
   check_i32(slots, "slot_mapping");
   check_bf16(q_out, "q_out");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  const int f8 = kv_cache_fp8(k_cache, v_cache);
   const int T = qkv.size(0);
   TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_kv_write: qkv width mismatch");
   TORCH_CHECK(k_cache.size(-2) == 16 && k_cache.size(-1) == D && v_cache.size(-1) == 16, "bad kv cache layout");
   gai_rope_kv_write(qkv.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(),
-                    q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D, rope ? 1 : 0,
-                    cur_stream());
+                    q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D, rope ? 1 : 0, f8,
+                    (float)k_scale, (float)v_scale, cur_stream());
 }
 
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
@@ -107,10 +119,10 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                   const Tensor& tiles, const Tensor& cu_q, const Tensor& ctx_lens, Tensor& out, int64_t Hq,
-                  int64_t Hkv, double scale, bool causal, const optional<Tensor>& lse) {
+                  int64_t Hkv, double scale, bool causal, const optional<Tensor>& lse, double k_scale,
+                  double v_scale) {
   check_bf16(q, "q");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  const int f8 = kv_cache_fp8(k_cache, v_cache);
   check_i32(block_tables, "block_tables");
   check_i32(tiles, "tiles");
   check_i32(cu_q, "cu_q");
@@ -125,16 +137,15 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   }
   gai_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                    block_tables.size(1), tiles.data_ptr<int>(), tiles.numel() / 2, cu_q.data_ptr<int>(),
-                   ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, lse_p,
-                   cur_stream());
+                   ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, lse_p, f8,
+                   (float)k_scale, (float)v_scale, cur_stream());
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                  const Tensor& ctx_lens, Tensor& out, Tensor& ws_o, Tensor& ws_ml, double scale, int64_t split_keys,
-                 int64_t max_splits) {
+                 int64_t max_splits, double k_scale, double v_scale) {
   check_bf16(q, "q");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  const int f8 = kv_cache_fp8(k_cache, v_cache);
   check_i32(block_tables, "block_tables");
   check_i32(ctx_lens, "ctx_lens");
   check_bf16(out, "out");
@@ -146,7 +157,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   TORCH_CHECK(ws_ml.numel() >= (int64_t)max_splits * B * Hq * 2, "attn_decode: ws_ml too small");
   gai_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                   block_tables.size(1), ctx_lens.data_ptr<int>(), out.data_ptr(), ws_o.data_ptr<float>(),
-                  ws_ml.data_ptr<float>(), B, Hq, Hkv, D, (float)scale, split_keys, max_splits, cur_stream());
+                  ws_ml.data_ptr<float>(), B, Hq, Hkv, D, (float)scale, split_keys, max_splits, f8, (float)k_scale,
+                  (float)v_scale, cur_stream());
 }
 
 void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p, const Tensor& top_k,

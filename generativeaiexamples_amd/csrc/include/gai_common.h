@@ -51,6 +51,29 @@ __device__ __forceinline__ float group_max(float v) {
 __device__ __forceinline__ bf16x8 load8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void store8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
 
+// ---- fp8 KV cache (OCP e4m3fn, gfx950 native conversions) ----
+typedef uint8_t fp8;
+// 8 fp8 values (one 8-byte load) -> 8 bf16, each multiplied by `s` (v_cvt_scalef32_pk_bf16_fp8)
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(uint2 v, float s) {
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, s, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, s, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, s, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, s, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+// 4 floats * inv_s -> 4 packed e4m3fn bytes, saturated to +-448
+__device__ __forceinline__ uint32_t f32x4_to_fp8(float a, float b, float c, float d, float inv_s) {
+  auto sat = [&](float x) { return fminf(fmaxf(x * inv_s, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
+  return (uint32_t)w;
+}
+// 8 cache elements -> bf16x8: a plain 16-byte load for bf16, an 8-byte load + conversion for fp8
+__device__ __forceinline__ bf16x8 load_kv8(const bf16* p, float) { return load8(p); }
+__device__ __forceinline__ bf16x8 load_kv8(const fp8* p, float s) {
+  return fp8x8_to_bf16(*reinterpret_cast<const uint2*>(p), s);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_tanh(float x) {

@@ -13,8 +13,10 @@ void gai_layernorm(const void* x, const void* residual_in, void* residual_out, c
                    void* out, int T, int D, float eps, hipStream_t st);
 
 // rope_kv.hip
+// kv_fp8: caches hold OCP e4m3fn x / {k,v}_scale (fp8 KV cache option); scales are ignored for bf16 caches
 void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, const int* slots, void* q_out,
-                       void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, hipStream_t st);
+                       void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, int kv_fp8,
+                       float k_scale, float v_scale, hipStream_t st);
 
 // gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu, 7 bias+quick-gelu;
 //            force: 0 auto, 1 skinny, 2 tiled 128x128, 3 large 256x256)
@@ -36,11 +38,13 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
-                      int Hq, int Hkv, int D, float scale, int causal, float* lse, hipStream_t st);
+                      int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
+                      float v_scale, hipStream_t st);
 int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
-                     int Hkv, int D, float scale, int split_keys, int max_splits, hipStream_t st);
+                     int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
+                     float v_scale, hipStream_t st);
 
 // sampling.hip
 void gai_sample(const float* logits, int B, int V, long ld, const float* temperature, const float* top_p,

@@ -18,6 +18,8 @@
 // column, so K and V^T are read once per kv head with 16-B / 8-B loads straight to
 // VGPRs (memory-bound decode row of the glds-vs-register table); the 4 waves
 // combine through LDS, splits are merged by attn_decode_reduce.
+#include <type_traits>
+
 #include "gai_common.h"
 #include "gai_kernels.h"
 
@@ -57,12 +59,16 @@ __device__ __forceinline__ int k_lds_off(int key, int u) {
 // V^T image: row = d (64 keys = 128 B), 8-B unit u (0..15) stored at u ^ ((d >> 1) & 15)
 __device__ __forceinline__ int v_lds_off(int d, int u) { return d * 128 + ((u ^ ((d >> 1) & 15)) << 3); }
 
-template <int D, int HPW>
+__device__ __forceinline__ bf16x8 kv_to_bf16(bf16x8 v, float) { return v; }
+__device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to_bf16(v, s); }
+
+// KV = bf16 or fp8 (OCP e4m3fn cache, dequantised by the per-layer scale when the tile is written to LDS)
+template <int D, int HPW, typename KV>
 __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
-    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
-    float scale, int causal, float* __restrict__ lse) {
+    float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale) {
   using Cfg = PrefillCfg<D>;
   constexpr int RPW = 4 / HPW;  // row groups per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -90,8 +96,9 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     for (int t = 0; t < D / 16; ++t) qf[t] = load8(qp + 16 * t);
   }
 
-  // staging registers
-  bf16x8 kst[Cfg::CH], vst[Cfg::CH];
+  // staging registers (raw cache bytes: the fp8 conversion happens at the LDS write, after the prefetch)
+  using Stage = typename std::conditional<sizeof(KV) == 1, uint2, bf16x8>::type;
+  Stage kst[Cfg::CH], vst[Cfg::CH];
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
@@ -100,8 +107,8 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
       const int pidx = kt * 4 + page;
       const int blk = (pidx * kBS < ctx) ? bt[pidx] : bt[0];
       const size_t pbase = ((size_t)blk * Hkv + g) * kBS * D;
-      kst[c] = load8(kc + pbase + (size_t)w * 8);  // K page is [16][D] contiguous
-      vst[c] = load8(vc + pbase + (size_t)w * 8);  // V^T page is [D][16] contiguous
+      kst[c] = *reinterpret_cast<const Stage*>(kc + pbase + (size_t)w * 8);  // K page is [16][D] contiguous
+      vst[c] = *reinterpret_cast<const Stage*>(vc + pbase + (size_t)w * 8);  // V^T page is [D][16] contiguous
     }
   };
   auto write_tile = [&](int buf) {
@@ -112,12 +119,13 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
       const int id = c * 256 + tid;
       const int page = id / (2 * D), w = id % (2 * D);
       const int key = page * 16 + w / Cfg::KU, u = w % Cfg::KU;
-      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kst[c];
+      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(kst[c], k_scale);
       const int d = w >> 1, half = w & 1;
       const int u8 = 4 * page + 2 * half;
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      const bf16x4_t lo = {vst[c][0], vst[c][1], vst[c][2], vst[c][3]};
-      const bf16x4_t hi = {vst[c][4], vst[c][5], vst[c][6], vst[c][7]};
+      const bf16x8 vv = kv_to_bf16(vst[c], v_scale);
+      const bf16x4_t lo = {vv[0], vv[1], vv[2], vv[3]};
+      const bf16x4_t hi = {vv[4], vv[5], vv[6], vv[7]};
       *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8)) = lo;
       *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8 + 1)) = hi;
     }
@@ -240,12 +248,13 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
 // ----------------------------------------------------------------------------------------------
 // Decode
 // ----------------------------------------------------------------------------------------------
-template <int D, bool PIPE, int H, bool V16>
+template <int D, bool PIPE, int H, bool V16, typename KV>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
-    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int Hq, int Hkv, float scale, int split_keys,
-    int max_splits) {
+    int max_splits, float k_scale, float v_scale) {
+  static_assert(sizeof(KV) == 2 || V16, "fp8 KV decode uses the 16-key V^T loads");
   __shared__ __attribute__((aligned(16))) float red_o[4][D][16];
   __shared__ float red_m[4][16], red_l[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, gq = lane >> 4;
@@ -283,10 +292,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   // Addresses of a chunk past the split are clamped to its last page (unconditional loads: a
   // data-dependent branch around them would force vmcnt(0) waits), and such keys are masked.
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  // fp8 caches: chunks hold the raw 8-byte pieces, converted to bf16 right before their MFMA
+  using Raw = typename std::conditional<sizeof(KV) == 1, uint2, bf16x8>::type;
   struct Chunk {
-    bf16x8 k[H][2][D / 32];
+    Raw k[H][2][D / 32];
     bf16x4_t vlo[H][V16 ? 1 : D / 16], vhi[H][V16 ? 1 : D / 16];
-    bf16x8 v8[H][V16 ? D / 16 : 1];
+    Raw v8[H][V16 ? D / 16 : 1];
   };
   const int last_page = (kend - 1) / kBS;
   auto load_chunk = [&](int kb, Chunk& c) {
@@ -303,23 +314,24 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
           const int key = 8 * (m >> 2) + 4 * i + (m & 3);  // 0..31 inside the half
           const size_t pb = key < 16 ? pb0 : pb1;
 #pragma unroll
-          for (int t = 0; t < D / 32; ++t) c.k[h][i][t] = load8(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
+          for (int t = 0; t < D / 32; ++t)
+            c.k[h][i][t] = *reinterpret_cast<const Raw*>(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
         }
         const size_t pbv = gq < 2 ? pb0 : pb1;
 #pragma unroll
         for (int dt = 0; dt < D / 16; ++dt)
-          c.v8[h][dt] = load8(vc + pbv + (size_t)(16 * dt + (lane & 15)) * kBS + 8 * (gq & 1));
-      } else {
+          c.v8[h][dt] = *reinterpret_cast<const Raw*>(vc + pbv + (size_t)(16 * dt + (lane & 15)) * kBS + 8 * (gq & 1));
+      } else if constexpr (sizeof(KV) == 2) {
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
-          c.k[h][0][t] = load8(kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
-          c.k[h][1][t] = load8(kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+          c.k[h][0][t] = load8((const bf16*)kc + pb0 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
+          c.k[h][1][t] = load8((const bf16*)kc + pb1 + (size_t)(lane & 15) * D + 32 * t + 8 * gq);
         }
 #pragma unroll
         for (int dt = 0; dt < D / 16; ++dt) {
           const size_t off = (size_t)(16 * dt + (lane & 15)) * kBS + 4 * gq;
-          c.vlo[h][dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb0 + off);
-          c.vhi[h][dt] = *reinterpret_cast<const bf16x4_t*>(vc + pb1 + off);
+          c.vlo[h][dt] = *reinterpret_cast<const bf16x4_t*>((const bf16*)vc + pb0 + off);
+          c.vhi[h][dt] = *reinterpret_cast<const bf16x4_t*>((const bf16*)vc + pb1 + off);
         }
       }
     }
@@ -334,7 +346,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         s[h][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
-          s[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[h][i][t], qf[t], s[h][i], 0, 0, 0);
+          s[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kv_to_bf16(c.k[h][i][t], k_scale), qf[t], s[h][i], 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb + 32 * h + (V16 ? 8 * gq + 4 * i + r : 16 * i + 4 * gq + r);
@@ -369,8 +381,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         bf16x8 vf;
-        if (V16) {
-          vf = c.v8[h][dt];
+        if constexpr (V16) {
+          vf = kv_to_bf16(c.v8[h][dt], v_scale);
         } else {
           vf = bf16x8{c.vlo[h][dt][0], c.vlo[h][dt][1], c.vlo[h][dt][2], c.vlo[h][dt][3],
                       c.vhi[h][dt][0], c.vhi[h][dt][1], c.vhi[h][dt][2], c.vhi[h][dt][3]};
@@ -473,18 +485,27 @@ void set_max_lds(F* f, int bytes) {
 
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
-                      int Hq, int Hkv, int D, float scale, int causal, float* lse, hipStream_t st) {
+                      int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
+                      float v_scale, hipStream_t st) {
   if (ntiles == 0) return;
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
 #define GAI_PF(DD, HP)                                                                                         \
   if (D == DD && hpw == HP) {                                                                                  \
     const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
-    auto kern = attn_prefill_kernel<DD, HP>;                                                                   \
-    set_max_lds(kern, lds);                                                                                    \
-    kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,  \
-                                                  block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq, \
-                                                  Hkv, scale, causal, lse);                                    \
+    if (kv_fp8) {                                                                                              \
+      auto kern = attn_prefill_kernel<DD, HP, fp8>;                                                            \
+      set_max_lds(kern, lds);                                                                                  \
+      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,  \
+                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale);            \
+    } else {                                                                                                   \
+      auto kern = attn_prefill_kernel<DD, HP, bf16>;                                                           \
+      set_max_lds(kern, lds);                                                                                  \
+      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, \
+                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale);            \
+    }                                                                                                          \
     GAI_LAUNCH_CHECK();                                                                                        \
     return;                                                                                                    \
   }
@@ -509,7 +530,8 @@ int gai_attn_prefill_rows_per_tile(int Hq, int Hkv) {
 
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
-                     int Hkv, int D, float scale, int split_keys, int max_splits, hipStream_t st) {
+                     int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
+                     float v_scale, hipStream_t st) {
   if (B == 0) return;
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
   if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
@@ -519,13 +541,22 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   static const int variant = getenv("GAI_DECODE_VARIANT") ? atoi(getenv("GAI_DECODE_VARIANT")) : 1;
 #define GAI_DEC(DD)                                                                                             \
   if (D == DD) {                                                                                                \
-    auto kern = variant == 0   ? attn_decode_kernel<DD, false, 1, false>                                       \
-                : variant == 2 ? attn_decode_kernel<DD, false, 2, true>                                        \
-                : variant == 3 ? attn_decode_kernel<DD, true, 1, true>                                         \
-                               : attn_decode_kernel<DD, false, 1, true>;                                       \
-    kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,    \
-                                                 block_tables, max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, \
-                                                 Hq, Hkv, scale, split_keys, max_splits);                       \
+    if (kv_fp8) {                                                                                               \
+      auto kern = variant == 2   ? attn_decode_kernel<DD, false, 2, true, fp8>                                  \
+                  : variant == 3 ? attn_decode_kernel<DD, true, 1, true, fp8>                                   \
+                                 : attn_decode_kernel<DD, false, 1, true, fp8>;                                 \
+      kern<<<grid, 256, 0, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache, block_tables,        \
+                                 max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
+                                 max_splits, k_scale, v_scale);                                                  \
+    } else {                                                                                                    \
+      auto kern = variant == 0   ? attn_decode_kernel<DD, false, 1, false, bf16>                                \
+                  : variant == 2 ? attn_decode_kernel<DD, false, 2, true, bf16>                                 \
+                  : variant == 3 ? attn_decode_kernel<DD, true, 1, true, bf16>                                  \
+                                 : attn_decode_kernel<DD, false, 1, true, bf16>;                                \
+      kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables,      \
+                                 max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
+                                 max_splits, k_scale, v_scale);                                                  \
+    }                                                                                                           \
     GAI_LAUNCH_CHECK();                                                                                         \
     if (max_splits > 1) {                                                                                       \
       attn_decode_reduce_kernel<DD><<<dim3(B, Hq), DD, 0, st>>>(ws_o, ws_ml, ctx_lens, (bf16*)out, B, Hq,       \

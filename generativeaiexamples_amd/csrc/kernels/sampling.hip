@@ -7,7 +7,9 @@
 // the token is drawn with the Gumbel-max trick restricted to the surviving set,
 // argmax(z_i + G_i) with G_i = -log(-log(u_i)) from a counter-based hash of
 // (seed, step, i) -- exact sampling from the renormalised nucleus in a single
-// extra pass, reproducible for a fixed seed.
+// extra pass, reproducible for a fixed seed. Top-p without top-k first tries the
+// LDS fast path (nucleus_fast: one fused mass + compaction pass, exact cut resolved
+// on <= 4096 candidates in LDS) and falls back to the radix passes.
 #include "gai_common.h"
 #include "gai_kernels.h"
 
@@ -61,6 +63,39 @@ __device__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   ArgMax r{sv[0], si[0]};
   for (int w = 1; w < kThreads / 64; ++w) r = argmax_merge(r, ArgMax{sv[w], si[w]});
   return r;
+}
+
+// Calls f(value, index) for every element of a row; 16-byte loads, four in flight per thread, when the
+// row is 16-byte aligned (the per-row passes are latency-bound with one workgroup per row).
+template <class F>
+__device__ __forceinline__ void row_for_each(const float* x, int V, F&& f) {
+  if ((V & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const int V4 = V >> 2;
+    int i = threadIdx.x;
+    for (; i + 3 * kThreads < V4; i += 4 * kThreads) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = x4[i + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = 4 * (i + u * kThreads);
+        f(v[u].x, b);
+        f(v[u].y, b + 1);
+        f(v[u].z, b + 2);
+        f(v[u].w, b + 3);
+      }
+    }
+    for (; i < V4; i += kThreads) {
+      const float4 v = x4[i];
+      f(v.x, 4 * i);
+      f(v.y, 4 * i + 1);
+      f(v.z, 4 * i + 2);
+      f(v.w, 4 * i + 3);
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += kThreads) f(x[i], i);
+  }
 }
 
 // Finds the largest key threshold K* with weight(key >= K*) >= target, where the weight of
@@ -131,6 +166,132 @@ __device__ uint32_t radix_select(const float* x, int V, float mx, float invT, ui
   return prefix;
 }
 
+__device__ __forceinline__ float key_to_float(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Top-p fast path. With the temperatures LLM serving uses, the nucleus lies within a few temperatures
+// of the max logit, so ONE fused pass sums the softmax mass S in registers and compacts every element
+// with d = (mx - x) / T < kCut into LDS (wave-aggregated slots, no histogram atomics). The exact cut is
+// resolved there: bitonic sort of (key, index), prefix sum of the weights, cut at the first prefix >=
+// p * S -- the same set as the radix path (largest key K* with mass(key >= K*) >= p * S), since every
+// element outside the list has a smaller key. Gumbel-max then runs over the candidates only. Returns
+// false (the caller takes the full radix path) when more than kCap elements qualify or the candidates
+// hold less than p of the mass (flat distributions).
+constexpr int kCap = 4096;
+constexpr float kCut = 12.f;  // candidates: logits within 12 temperatures of the max (weight >= e^-12)
+
+__device__ bool nucleus_fast(const float* x, int V, float mx, float invT, float p, uint64_t seed, int64_t step,
+                             float* sv, int* si, uint64_t* cand, int* cnt, int* out) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) cnt[0] = 0, cnt[1] = 0x7fffffff;
+  __syncthreads();
+  // one fused pass: S = sum of exp(-d) in registers, elements with d < kCut compacted into LDS
+  // (wave-aggregated slots; every lane runs the same trip count so each ballot sees the whole wave)
+  float S = 0.f;
+  auto visit = [&](float xv, int i, bool valid) {
+    const float d = (mx - xv) * invT;
+    S += valid ? __expf(-d) : 0.f;
+    const bool c = valid && d < kCut;
+    const unsigned long long m = __ballot(c);
+    if (m == 0) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&cnt[0], __popcll(m));
+    base = __shfl(base, 0, 64);
+    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (c && pos < kCap) cand[pos] = ((uint64_t)fkey(xv) << 32) | (uint32_t)i;
+  };
+  if ((V & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const int V4 = V >> 2;
+    for (int j0 = 0; j0 < V4; j0 += 2 * kThreads) {
+      float4 v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = j0 + u * kThreads + tid;
+        v[u] = j < V4 ? x4[j] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = j0 + u * kThreads + tid;
+        const bool ok = j < V4;
+        visit(v[u].x, 4 * j, ok);
+        visit(v[u].y, 4 * j + 1, ok);
+        visit(v[u].z, 4 * j + 2, ok);
+        visit(v[u].w, 4 * j + 3, ok);
+      }
+    }
+  } else {
+    for (int i0 = 0; i0 < V; i0 += kThreads) {
+      const int i = i0 + tid;
+      visit(i < V ? x[i] : -INFINITY, i, i < V);
+    }
+  }
+  S = block_sum(S, sv);  // (its barriers also publish the candidate list)
+  const float target = p * S;
+  const int n = cnt[0];
+  if (n > kCap) return false;
+  int P = 2;
+  while (P < n) P <<= 1;
+  for (int j = n + tid; j < P; j += kThreads) cand[j] = 0ull;
+  __syncthreads();
+  // bitonic sort, descending
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < P / 2; t += kThreads) {
+        const int a = (t / j) * 2 * j + (t % j), b = a + j;
+        const uint64_t va = cand[a], vb = cand[b];
+        if (((a & k) == 0) ? (va < vb) : (va > vb)) {
+          cand[a] = vb;
+          cand[b] = va;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // inclusive prefix of weights in sorted order; 4 consecutive candidates per thread
+  float w[4], s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 4 * tid + q;
+    w[q] = j < n ? __expf((key_to_float((uint32_t)(cand[j] >> 32)) - mx) * invT) : 0.f;
+    s += w[q];
+  }
+  float incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) sv[wid] = incl;
+  __syncthreads();
+  float run = incl - s;
+  for (int q = 0; q < wid; ++q) run += sv[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    run += w[q];
+    if (4 * tid + q < n && run >= target) {
+      atomicMin(&cnt[1], 4 * tid + q);
+      break;
+    }
+  }
+  __syncthreads();
+  if (cnt[1] >= n) return false;  // the candidates hold less than p of the mass: the nucleus reaches past kCut
+  const int jcut = cnt[1];
+  const uint32_t kcut = (uint32_t)(cand[jcut] >> 32);
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int j = tid; j < n; j += kThreads) {
+    const uint64_t e = cand[j];
+    const uint32_t kk = (uint32_t)(e >> 32);
+    if (kk < kcut) continue;
+    const uint32_t idx = (uint32_t)e;
+    best = argmax_merge(best, ArgMax{(key_to_float(kk) - mx) * invT + gumbel(seed, (uint64_t)step, idx), (int)idx});
+  }
+  best = block_argmax(best, sv, si);
+  if (tid == 0) *out = best.i;
+  return true;
+}
+
 __global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restrict__ logits, int V, long ld,
                                                           const float* __restrict__ temperature,
                                                           const float* __restrict__ top_p,
@@ -141,18 +302,27 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restric
   __shared__ float sv[16];
   __shared__ int si[16];
   __shared__ float red[4];
+  __shared__ uint64_t cand[kCap];
+  __shared__ int cnt[2];
   const int row = blockIdx.x;
   const float* x = logits + (size_t)row * ld;
   const float T = temperature[row];
 
   ArgMax am{-INFINITY, 0x7fffffff};
-  for (int i = threadIdx.x; i < V; i += kThreads) am = argmax_merge(am, ArgMax{x[i], i});
+  row_for_each(x, V, [&](float xv, int i) { am = argmax_merge(am, ArgMax{xv, i}); });
   am = block_argmax(am, sv, si);
   if (T <= 0.f) {
     if (threadIdx.x == 0) out_tokens[row] = am.i;
     return;
   }
   const float mx = am.v, invT = 1.f / T;
+  {
+    const int k = top_k[row];
+    const float p = top_p[row];
+    if ((k <= 0 || k >= V) && p < 1.f &&
+        nucleus_fast(x, V, mx, invT, p, (uint64_t)seeds[row], step, sv, si, cand, cnt, out_tokens + row))
+      return;
+  }
   uint32_t floor_key = 0;
   const int k = top_k[row];
   if (k > 0 && k < V) floor_key = radix_select<false>(x, V, mx, invT, 0u, (float)k, hist, red);

@@ -33,7 +33,7 @@ import torch
 
 from .. import ops
 from ..models.common import ForwardBatch
-from .kv_cache import KVCache
+from .kv_cache import KVCache, cache_dtype
 from .sampling import SamplingBatch, SamplingParams
 from .staging import HostStager
 from ..utils.profiling import roctx_range
@@ -65,6 +65,10 @@ class EngineConfig:
     # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)
     # and return to the host once per run. 1 disables it.
     decode_steps: int = 8
+    # "auto" = the model dtype; "fp8" = OCP e4m3fn KV cache (twice the cached tokens per GB, half the decode
+    # attention bytes; static per-layer scales kv_scale), for models whose attention path supports it
+    kv_cache_dtype: str = "auto"
+    kv_scale: float = 1.0
 
 
 @dataclass
@@ -121,8 +125,13 @@ class LLMEngine:
         ctx = getattr(model, "ctx", None)
         self.tp_size = ctx.tp_size if ctx is not None else 1
         self.leader = self.tp_size == 1 or ctx.tp_rank == 0
+        if self.tp_size > 1 and self.device.type == "cuda" and ctx.backend != "nccl":
+            cfg.use_graphs = False  # host (gloo) collectives, e.g. a one-GPU TP rehearsal, are not capturable
         if self.tp_size > 1 and hasattr(model, "register_request"):
             raise NotImplementedError(f"{mc.name}: per-request model state is not replicated to TP followers")
+        self.kv_dtype = cache_dtype(cfg.kv_cache_dtype, model.dtype)
+        if self.kv_dtype == torch.float8_e4m3fn and not getattr(model, "supports_fp8_kv", False):
+            raise ValueError(f"{mc.name}: the fp8 KV cache is not supported by this model's attention path")
         nb = cfg.num_blocks or self._blocks_from_memory()
         if self.tp_size > 1:  # every rank's cache must hold the leader's block ids: agree on the minimum
             import torch.distributed as dist
@@ -132,7 +141,8 @@ class LLMEngine:
             nb = int(t.item())
         # one extra block, never handed out, is the scratch page of padded graph rows
         # models with non-KV layers (cross-attention) report how many layers own a paged KV cache
-        self.kv = KVCache(self._kv_layers(), nb + 1, model.hkv, mc.head_dim, self.device, model.dtype)
+        self.kv = KVCache(self._kv_layers(), nb + 1, model.hkv, mc.head_dim, self.device, self.kv_dtype,
+                          k_scale=cfg.kv_scale, v_scale=cfg.kv_scale)
         self.pad_block = nb
         self.sched = _rt().Scheduler(nb, cfg.max_num_seqs, cfg.max_batched_tokens, cfg.max_model_len,
                                      cfg.prefix_cache, cfg.prefill_chunk)
@@ -177,7 +187,7 @@ class LLMEngine:
             nbytes = int(free * frac)
         else:
             nbytes = 256 << 20
-        nb = KVCache.blocks_for_memory(nbytes, self._kv_layers(), self.model.hkv, mc.head_dim, self.model.dtype)
+        nb = KVCache.blocks_for_memory(nbytes, self._kv_layers(), self.model.hkv, mc.head_dim, self.kv_dtype)
         return max(nb, 2 * self.max_blocks_per_seq)
 
     # ------------------------------------------------------------------ requests
@@ -187,6 +197,8 @@ class LLMEngine:
         """images: inputs for a multimodal model (encoded once here by ``model.register_request``);
         lora: name of an adapter registered with ``model.add_lora`` (multi-LoRA serving)."""
         params = params or SamplingParams()
+        if params.resume_ids:
+            prompt_ids = list(prompt_ids) + list(params.resume_ids)
         with self.lock:
             sid = next(self._ids)
             rid = request_id or f"req-{sid}"
@@ -200,6 +212,12 @@ class LLMEngine:
             req.max_new = max_new
             if params.guided is not None:
                 req.matcher = params.guided.matcher()
+                for t in params.resume_ids:
+                    req.matcher.advance(int(t))
+            if params.resume_ids:
+                req.detok.prime(params.resume_ids, params.resume_sent_chars)
+            for t in params.resume_ids:
+                req.token_counts[t] = req.token_counts.get(t, 0) + 1
             if lora:
                 req.lora_slot = self.model.lora_slot(lora)
             self.requests[sid] = req

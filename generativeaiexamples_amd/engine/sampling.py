@@ -24,6 +24,11 @@ class SamplingParams:
     logprobs: bool = False
     # constrained decoding (engine/guided.py): a compiled grammar / JSON-schema matcher, or None
     guided: Optional[object] = None
+    # elastic re-queue (serving/router.py): tokens of this completion already delivered by a replica that
+    # failed mid-stream. They extend the prompt, count for the penalties and are replayed into the grammar
+    # matcher; the caller has already taken them off max_tokens / min_tokens.
+    resume_ids: List[int] = field(default_factory=list)
+    resume_sent_chars: Optional[int] = None  # characters of their text the client already has
 
     @property
     def greedy(self) -> bool:

@@ -174,11 +174,8 @@ class IncrementalDetokenizer:
         self.hold = max((len(s) for s in self.stop), default=1) - 1
         self.stopped = False
 
-    def add(self, token: int) -> str:
-        if self.stopped:
-            return ""
-        self.ids.append(int(token))
-        raw = self.tok.decode_bytes(self.ids)
+    def _decode(self) -> str:
+        raw = self.tok.decode_bytes(self.ids) if self.ids else b""
         # only decode complete UTF-8 sequences
         cut = len(raw)
         for back in range(1, min(4, len(raw)) + 1):
@@ -189,7 +186,21 @@ class IncrementalDetokenizer:
             if need > back:
                 cut = len(raw) - back
             break
-        self.text = raw[:cut].decode("utf-8", errors="replace")
+        return raw[:cut].decode("utf-8", errors="replace")
+
+    def prime(self, ids: Sequence[int], sent_chars: Optional[int] = None) -> None:
+        """Continue a completion another replica started (elastic re-queue): ``ids`` were generated there and
+        ``sent_chars`` characters of their text already reached the client (default: all complete ones)."""
+        for t in ids:
+            self.ids.append(int(t))
+        self.text = self._decode()
+        self.sent = len(self.text) if sent_chars is None else min(int(sent_chars), len(self.text))
+
+    def add(self, token: int) -> str:
+        if self.stopped:
+            return ""
+        self.ids.append(int(token))
+        self.text = self._decode()
         for s in self.stop:
             k = self.text.find(s, max(0, self.sent - len(s)))
             if k >= 0:

@@ -172,6 +172,8 @@ class LlamaConfig:
 class LlamaModel:
     """Weights + forward. Weights are plain tensors (no nn.Module): the engine owns execution."""
 
+    supports_fp8_kv = True  # the attention path passes the KV cache's per-layer scales (EngineConfig.kv_cache_dtype)
+
     def __init__(self, cfg: LlamaConfig, device=None, dtype=torch.bfloat16, dist_ctx: DistContext | None = None):
         self.cfg = cfg
         self.ctx = dist_ctx or get_context()
@@ -504,13 +506,15 @@ class LlamaModel:
             if c.qk_norm:
                 self._qk_norm(qkv, p)
             kc, vc = kv.layer(i)
-            ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True)
+            ks, vs = kv.scales(i)
+            ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True, ks, vs)
             if P > 0:
                 ops.attention_prefill(q[:P], kc, vc, fb.prefill_block_tables, fb.cu_q, fb.prefill_ctx, self.scale,
-                                      True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P])
+                                      True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P], k_scale=ks,
+                                      v_scale=vs)
             if T > P:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
-                                     max_ctx=fb.max_decode_ctx, out=attn[P:])
+                                     max_ctx=fb.max_decode_ctx, out=attn[P:], k_scale=ks, v_scale=vs)
             a2 = attn.view(T, -1)
             if fuse:
                 x = ops.linear_add_rmsnorm(a2, w[p + "o"], res, w[p + "mlp_norm"], c.rms_eps, bias=w.get(p + "o_b"))
@@ -567,13 +571,15 @@ class LlamaModel:
             if c.qk_norm:
                 self._qk_norm(qkv, p)
             kc, vc = kv.layer(i)
+            ks, vs = kv.scales(i)
             ops.rope_kv_write(qkv[:T], fb.positions, self.cos_sin, fb.slots, q[:T], kc, vc, self.hq, self.hkv, hd,
-                              True)
+                              True, ks, vs)
             ops.attention_prefill(q[:P], kc, vc, fb.prefill_block_tables, fb.cu_q, fb.prefill_ctx, self.scale,
-                                  True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P])
+                                  True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P], k_scale=ks,
+                                  v_scale=vs)
             if T > P:
                 ops.attention_decode(q[P:T], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
-                                     max_ctx=fb.max_decode_ctx, out=attn[P:T])
+                                     max_ctx=fb.max_decode_ctx, out=attn[P:T], k_scale=ks, v_scale=vs)
             a2 = attn.view(Tp, -1)
             h = ctx.tp_reduce_scatter_rows(
                 self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb))

@@ -44,6 +44,8 @@ class MixtralConfig(LlamaConfig):
 
 
 class MixtralModel(LlamaModel):
+    supports_fp8_kv = False  # own attention call sites (no per-layer KV scales)
+
     def _alloc(self):
         c = self.cfg
         tp, r = self.ctx.tp_size, self.ctx.tp_rank

@@ -180,6 +180,8 @@ class CrossCache:
 class MllamaModel(LlamaModel):
     """Vision encoder + projector + Llama decoder with cross-attention layers (TP = 1)."""
 
+    supports_fp8_kv = False  # own attention call sites (no per-layer KV scales)
+
     def __init__(self, cfg: MllamaConfig, device=None, dtype=torch.bfloat16, dist_ctx=None,
                  max_images_in_flight: int = 64):
         self.mcfg = cfg

@@ -404,10 +404,14 @@ TUNER = GemmTuner()
 # ---------------------------------------------------------------------------------------------
 # RoPE + paged KV write, attention
 # ---------------------------------------------------------------------------------------------
-def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope=True):
+def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope=True, k_scale=1.0,
+                  v_scale=1.0):
+    """KV caches are bf16, or torch.float8_e4m3fn (fp8 KV option: the cache holds x / {k,v}_scale)."""
     if not qkv.is_cuda:
-        return ref.rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope)
-    native().rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope)
+        return ref.rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope,
+                                 k_scale, v_scale)
+    native().rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope, k_scale,
+                           v_scale)
 
 
 def prefill_rows_per_tile(Hq: int, Hkv: int) -> int:
@@ -424,11 +428,12 @@ def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device) -> tor
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, tiles=None,
-                      q_lens: Sequence[int] | None = None, out=None, lse=None):
+                      q_lens: Sequence[int] | None = None, out=None, lse=None, k_scale=1.0, v_scale=1.0):
     """Varlen paged flash attention. ``lse`` (optional fp32 [T, Hq]) receives each row's natural-log
     softmax normaliser, used to merge partial attentions (parallel/context_parallel.py)."""
     if not q.is_cuda:
-        o, l = ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal, return_lse=True)
+        o, l = ref.attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal, return_lse=True,
+                                     k_scale=k_scale, v_scale=v_scale)
         if lse is not None:
             lse.copy_(l)
         return _into(out, o)
@@ -439,7 +444,8 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
             q_lens = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
         tiles = build_prefill_tiles(q_lens, Hq, Hkv, q.device)
     out = torch.empty_like(q) if out is None else out
-    native().attn_prefill(q, k_cache, v_cache, block_tables, tiles, cu_q, ctx_lens, out, Hq, Hkv, scale, causal, lse)
+    native().attn_prefill(q, k_cache, v_cache, block_tables, tiles, cu_q, ctx_lens, out, Hq, Hkv, scale, causal, lse,
+                          k_scale, v_scale)
     return out
 
 
@@ -480,9 +486,9 @@ class DecodeWorkspace:
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
-                     max_ctx: int | None = None, out=None):
+                     max_ctx: int | None = None, out=None, k_scale=1.0, v_scale=1.0):
     if not q.is_cuda:
-        return _into(out, ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale))
+        return _into(out, ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, k_scale, v_scale))
     B, Hq, D = q.shape
     mc = max_ctx if max_ctx is not None else int(ctx_lens.max())
     if ws is None:
@@ -491,7 +497,8 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
     nsplit = (mc + split - 1) // split
     assert nsplit <= ws.max_splits, "decode workspace too small for this context"
     out = torch.empty_like(q) if out is None else out
-    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, split, nsplit)
+    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, split, nsplit, k_scale,
+                         v_scale)
     return out
 
 

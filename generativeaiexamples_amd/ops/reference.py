@@ -94,7 +94,19 @@ def rope_cos_sin(max_pos: int, head_dim: int, theta: float = 500000.0, scaling: 
     return torch.cat([f.cos(), f.sin()], -1).float().to(device)
 
 
-def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope=True):
+def _to_cache(x, cache, scale):
+    """Values -> cache dtype; fp8 caches hold x / scale saturated to the e4m3fn range (like the kernel)."""
+    if cache.dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-448.0, 448.0).to(cache.dtype)
+    return x.to(cache.dtype)
+
+
+def _from_cache(x, scale):
+    return x.float() * scale if x.dtype == torch.float8_e4m3fn else x.float()
+
+
+def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, rope=True, k_scale=1.0,
+                  v_scale=1.0):
     T = qkv.shape[0]
     x = qkv.view(T, Hq + 2 * Hkv, D).float()
     q, k, v = x[:, :Hq], x[:, Hq:Hq + Hkv], x[:, Hq + Hkv:]
@@ -113,8 +125,9 @@ def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, H
     if valid.any():
         sl = slots[valid].long()
         blk, off = sl // BLOCK, sl % BLOCK
-        k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
-        v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+        # the kernel rounds k (after RoPE) and v to bf16 before an fp8 conversion
+        k_cache[blk, :, off, :] = _to_cache(k[valid].to(qkv.dtype), k_cache, k_scale)
+        v_cache[blk, :, :, off] = _to_cache(v[valid].to(qkv.dtype), v_cache, v_scale)
 
 
 def gather_kv(k_cache, v_cache, block_table, n):
@@ -126,7 +139,8 @@ def gather_kv(k_cache, v_cache, block_table, n):
     return k, v
 
 
-def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, return_lse=False):
+def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, return_lse=False,
+                      k_scale=1.0, v_scale=1.0):
     """q [Tq, Hq, D]; per sequence b the queries are the last q_len positions of ctx_lens[b] keys.
     return_lse: also return the fp32 [Tq, Hq] natural-log softmax normalisers (-1e30 for empty rows)."""
     out = torch.empty_like(q)
@@ -140,8 +154,8 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
             continue
         n = int(ctx_lens[b])
         k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
-        k = k.float().repeat_interleave(Hq // Hkv, dim=1)
-        v = v.float().repeat_interleave(Hq // Hkv, dim=1)
+        k = _from_cache(k, k_scale).repeat_interleave(Hq // Hkv, dim=1)
+        v = _from_cache(v, v_scale).repeat_interleave(Hq // Hkv, dim=1)
         qq = q[s:e].float()
         att = torch.einsum("qhd,khd->hqk", qq, k) * scale
         if causal:
@@ -154,11 +168,12 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
     return (out, lse) if return_lse else out
 
 
-def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale):
+def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, k_scale=1.0, v_scale=1.0):
     """q [B, Hq, D], one token per sequence attending to its ctx_lens[b] cached keys."""
     B = q.shape[0]
     cu = torch.arange(B + 1, dtype=torch.int32)
-    return attention_prefill(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, causal=True)
+    return attention_prefill(q, k_cache, v_cache, block_tables, cu, ctx_lens, scale, causal=True, k_scale=k_scale,
+                             v_scale=v_scale)
 
 
 def attention_dense(q, k, v, cu_seqlens, scale, causal):

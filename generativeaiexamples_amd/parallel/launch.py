@@ -3,7 +3,8 @@
 ``python bench.py --gpus N`` and ``python -m generativeaiexamples_amd.serving --tp N`` re-run themselves
 as N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set) unless they already
 run under torchrun. Children are plain subprocesses (never exec from a process that initialised HIP); a
-failing rank stops the others and its exit code is returned. SIGTERM / SIGINT are forwarded.
+failing rank stops the others (SIGTERM, then SIGKILL after GAI_RANK_STOP_GRACE_S) and its exit code
+is returned: a TP group fails as a unit, and serving/supervisor.py restarts it. SIGTERM / SIGINT are forwarded.
 """
 from __future__ import annotations
 
@@ -46,6 +47,7 @@ def spawn_ranks(n: int, argv: Optional[List[str]] = None, script: Optional[str] 
 
     old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
+    kill_at = None  # ranks asked to stop after a failure get this long before SIGKILL
     try:
         live = list(procs)
         while live:
@@ -56,8 +58,13 @@ def spawn_ranks(n: int, argv: Optional[List[str]] = None, script: Optional[str] 
                 live.remove(p)
                 if code != 0:
                     rc = rc or code
-                    for q in live:
-                        q.terminate()
+                    if kill_at is None:
+                        kill_at = time.monotonic() + float(os.environ.get("GAI_RANK_STOP_GRACE_S", "15"))
+                        for q in live:
+                            q.terminate()
+            if kill_at is not None and time.monotonic() > kill_at:
+                for q in live:
+                    q.kill()
             time.sleep(0.2)
     finally:
         for s, h in old.items():

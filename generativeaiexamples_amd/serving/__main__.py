@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--tp", type=int, default=int(os.environ.get("APP_ENGINE_TP", "1")),
                     help="tensor-parallel degree of the generator (one process per GPU)")
     ap.add_argument("--dtype", default=None, help="generator dtype override, e.g. float32")
+    ap.add_argument("--kv-cache-dtype", default=os.environ.get("APP_ENGINE_KVCACHEDTYPE", "auto"),
+                    help="auto | fp8 (OCP e4m3fn paged KV cache: 2x cached tokens, half the decode KV bytes)")
     a = ap.parse_args()
     if a.tp > 1 and "WORLD_SIZE" not in os.environ:
         import sys
@@ -56,7 +58,7 @@ def main():
                    embedder_weights=a.embedder_weights, reranker=a.reranker, reranker_weights=a.reranker_weights,
                    served_llm_name=a.served_model_name, max_num_seqs=a.max_num_seqs, max_model_len=a.max_model_len,
                    use_graphs=not a.no_graphs, lora_adapters=dict((x.split("=", 1) + [""])[:2] for x in a.lora), device=a.device,
-                   tp=a.tp, dtype=a.dtype)
+                   tp=a.tp, dtype=a.dtype, kv_cache_dtype=a.kv_cache_dtype)
     hub = ServiceHub.build(spec)
     if hub.is_follower:
         hub.serve_follower()

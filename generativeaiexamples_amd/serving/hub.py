@@ -40,6 +40,7 @@ class HubSpec:
     # rank 0 serves the API and plans every step, the other ranks execute its plans (LLMEngine.follow)
     tp: int = 1
     dtype: Optional[str] = None  # generator dtype override ("float32" for exact CPU rehearsals)
+    kv_cache_dtype: str = "auto"  # "fp8": OCP e4m3fn paged KV cache (NIM / TRT-LLM kv_cache_dtype option)
 
     @staticmethod
     def from_env() -> "HubSpec":
@@ -58,6 +59,7 @@ class HubSpec:
         s.max_model_len = int(g("APP_ENGINE_MAXMODELLEN", s.max_model_len))
         s.device = g("APP_ENGINE_DEVICE")
         s.tp = int(g("APP_ENGINE_TP", s.tp))
+        s.kv_cache_dtype = g("APP_ENGINE_KVCACHEDTYPE", s.kv_cache_dtype)
         return s
 
 
@@ -172,7 +174,8 @@ class ServiceHub:
             eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=spec.max_num_seqs, max_model_len=spec.max_model_len,
                                                  max_batched_tokens=spec.max_batched_tokens,
                                                  use_graphs=spec.use_graphs and dev.type == "cuda",
-                                                 kv_memory_fraction=spec.kv_memory_fraction))
+                                                 kv_memory_fraction=spec.kv_memory_fraction,
+                                                 kv_cache_dtype=spec.kv_cache_dtype))
             if not eng.leader:  # TP follower: no API, no embedder / reranker
                 hub.follower_engine = eng
                 return hub

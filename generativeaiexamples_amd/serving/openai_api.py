@@ -307,6 +307,15 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
             params.guided = guide_for(req, tok)
         except (ValueError, KeyError) as e:  # SchemaError is a ValueError
             return _err(400, f"structured output: {e}")
+        # elastic re-queue (serving/router.py): the router asks for token ids in the stream and resumes a
+        # completion a failed replica started by sending the ids it already delivered
+        nv = req.nvext or {}
+        want_ids = bool(nv.get("return_token_ids"))
+        resume = [int(t) for t in nv.get("resume_token_ids") or []]
+        if resume:
+            params.max_tokens = max(0, params.max_tokens - len(resume))
+            params.min_tokens = max(0, params.min_tokens - len(resume))
+            params.resume_ids, params.resume_sent_chars = resume, nv.get("resume_text_chars")
         images = _images_of(req) or None
         lora = hub.lora_for(req.model)
         if images and not hasattr(llm.engine.model, "register_request"):
@@ -330,7 +339,9 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
                         ch = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
                               "choices": [{"index": 0, "delta": {"content": it.delta} if it.delta else {},
                                            "logprobs": None, "finish_reason": it.finish_reason if it.finished else None}]}
-                        if it.delta or it.finished:
+                        if want_ids and it.token_id >= 0:
+                            ch["nvext"] = {"token_ids": [it.token_id]}
+                        if it.delta or it.finished or "nvext" in ch:
                             yield f"data: {json.dumps(ch)}\n\n"
                 except Exception as e:  # report in-band, SSE cannot change status mid-stream
                     yield f"data: {json.dumps({'error': {'message': str(e)}})}\n\n"

@@ -134,6 +134,32 @@ def test_attention_prefill(cuda, D, Hq, Hkv, causal):
     _close(o, o_ref, 2e-2, 2e-2, "prefill")
 
 
+@pytest.mark.parametrize("L,D,Hq,Hkv", [(2048, 128, 32, 8), (4096, 128, 32, 8), (8192, 128, 32, 8),
+                                         (2048, 256, 16, 8), (4096, 256, 8, 4), (8192, 256, 8, 1)])
+def test_attention_prefill_long(cuda, L, D, Hq, Hkv):
+    """Long-context causal GQA prefill (one 2K-8K sequence plus a short one, D 128 / 256) against an
+    fp32 dense reference computed per head on the GPU (the CPU reference would need GBs of scores)."""
+    torch.manual_seed(L + D)
+    ctx = [L, 300]
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, cuda, seed=L)
+    cu = torch.tensor([0, L, L + 300], dtype=torch.int32, device=cuda)
+    q = torch.randn(L + 300, Hq, D, device=cuda, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    o = ops.attention_prefill(q, kc, vc, bt, cu, torch.tensor(ctx, dtype=torch.int32, device=cuda), scale, True,
+                              q_lens=ctx)
+    for s, n in enumerate(ctx):
+        blocks = bt[s, :(n + 15) // 16].long()
+        k = kc[blocks].permute(1, 0, 2, 3).reshape(Hkv, -1, D)[:, :n].float()  # [Hkv, n, D]
+        v = vc[blocks].permute(1, 0, 3, 2).reshape(Hkv, -1, D)[:, :n].float()
+        qs = q[int(cu[s]):int(cu[s]) + n].float()
+        mask = torch.ones(n, n, device=cuda, dtype=torch.bool).tril()
+        for h in range(Hq):
+            kv = h // (Hq // Hkv)
+            sc = (qs[:, h] @ k[kv].t()) * scale
+            ref_o = sc.masked_fill(~mask, float("-inf")).softmax(-1) @ v[kv]
+            _close(o[int(cu[s]):int(cu[s]) + n, h], ref_o, 2e-2, 2e-2, f"prefill L={n} h={h}")
+
+
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 64, 8), (64, 8, 8), (128, 4, 4)])
 def test_attention_decode(cuda, D, Hq, Hkv):
     torch.manual_seed(6)
@@ -147,6 +173,67 @@ def test_attention_decode(cuda, D, Hq, Hkv):
         o = ops.attention_decode(q, kc, vc, bt, ctx_t.to(cuda), scale, ws=ws)
         o_ref = ref.attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx_t, scale)
         _close(o, o_ref, 2e-2, 2e-2, f"decode split={ws.split_keys}")
+
+
+F8 = torch.float8_e4m3fn
+
+
+@pytest.mark.parametrize("D", [64, 128, 256])
+def test_rope_kv_write_fp8(cuda, D):
+    torch.manual_seed(14)
+    Hq, Hkv, T = 8, 2, 45
+    qkv = (torch.randn(T, (Hq + 2 * Hkv) * D, device=cuda) * 4).to(torch.bfloat16)
+    pos = torch.randint(0, 1000, (T,), device=cuda, dtype=torch.int32)
+    cs = ops.rope_cos_sin(2048, D, 500000.0, device=cuda)
+    slots = torch.randperm(10 * 16, device=cuda)[:T].int()
+    kc = torch.zeros(10, Hkv, 16, D, device=cuda, dtype=F8)
+    vc = torch.zeros(10, Hkv, D, 16, device=cuda, dtype=F8)
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.rope_kv_write(qkv, pos, cs, slots, q, kc, vc, Hq, Hkv, D, True, 0.5, 2.0)
+    kr = torch.zeros(10, Hkv, 16, D, dtype=F8)
+    vr = torch.zeros(10, Hkv, D, 16, dtype=F8)
+    qr = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    ref.rope_kv_write(qkv.cpu(), pos.cpu(), cs.cpu(), slots.cpu(), qr, kr, vr, Hq, Hkv, D, True, 0.5, 2.0)
+    # same bf16 inputs, both round-to-nearest into e4m3fn: at most one fp8 step apart (rope's fp32 math)
+    _close(kc.float(), kr.float(), 1e-3, 0.13, "k cache fp8")
+    _close(vc.float(), vr.float(), 0, 0, "v cache fp8")
+    assert (kc.float() == kr.float().to(cuda)).float().mean() > 0.97
+
+
+def _fp8_paged(ctx, Hkv, D, seed):
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, "cpu", seed=seed)
+    return (kc.float() * 3).to(F8).to("cuda"), (vc.float() * 3).to(F8).to("cuda"), bt.to("cuda")
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 8, 8), (256, 8, 2)])
+def test_attention_decode_fp8(cuda, D, Hq, Hkv):
+    torch.manual_seed(15)
+    ctx = [1, 17, 513, 2000, 4097]
+    kc, vc, bt = _fp8_paged(ctx, Hkv, D, 3)
+    q = torch.randn(len(ctx), Hq, D, device=cuda, dtype=torch.bfloat16)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    for split in (128, None):
+        ws = ops.DecodeWorkspace(len(ctx), Hq, D, max(ctx), cuda, split_keys=split)
+        o = ops.attention_decode(q, kc, vc, bt, ctx_t.to(cuda), scale, ws=ws, k_scale=0.25, v_scale=0.5)
+        o_ref = ref.attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx_t, scale, 0.25, 0.5)
+        _close(o, o_ref, 2e-2, 2e-2, f"fp8 decode split={ws.split_keys}")
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 16, 8), (256, 8, 4)])
+def test_attention_prefill_fp8(cuda, D, Hq, Hkv):
+    torch.manual_seed(16)
+    ctx, qlen = [77, 300, 1030], [77, 33, 1030]
+    kc, vc, bt = _fp8_paged(ctx, Hkv, D, 4)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(int(cu[-1]), Hq, D, device=cuda, dtype=torch.bfloat16)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    o = ops.attention_prefill(q, kc, vc, bt, cu.to(cuda), ctx_t.to(cuda), scale, True, q_lens=qlen, k_scale=0.25,
+                              v_scale=0.5)
+    o_ref = ref.attention_prefill(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu, ctx_t, scale, True, k_scale=0.25,
+                                  v_scale=0.5)
+    _close(o, o_ref, 2e-2, 2e-2, "fp8 prefill")
 
 
 def test_sample_greedy_and_topk1(cuda):
@@ -181,6 +268,31 @@ def test_sample_top_p_membership(cuda):
     # determinism for a fixed seed/step
     t2 = ops.sample(logits, temp, top_p, top_k, seeds, 3).long()
     assert torch.equal(t, t2)
+
+
+@pytest.mark.parametrize("scale,T,p", [(1.28, 0.2, 0.7), (3.0, 1.0, 0.9), (0.01, 1.0, 0.9), (1.0, 0.05, 0.95)])
+def test_sample_nucleus_exact(cuda, scale, T, p):
+    """Every sampled token lies in the exact nucleus (largest logit cut with mass >= p), across the LDS
+    fast path (peaked rows) and the full radix fallback (flat rows: > 4096 candidates)."""
+    torch.manual_seed(12)
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=cuda) * scale
+    logits[0, :100] = float("-inf")  # masked tokens (constrained decoding)
+    temp = torch.full((B,), T, device=cuda)
+    top_p = torch.full((B,), p, device=cuda)
+    top_k = torch.zeros(B, dtype=torch.int32, device=cuda)
+    seen = set()
+    for step in range(4):
+        t = ops.sample(logits, temp, top_p, top_k, torch.arange(B, dtype=torch.int64, device=cuda), step).long()
+        x = (logits.double() / T)
+        probs = x.softmax(-1)
+        sp, si = probs.sort(-1, descending=True)
+        cum = sp.cumsum(-1)
+        n_keep = ((cum - sp) < p * (1 + 1e-5)).sum(-1)
+        rank = (si == t[:, None]).float().argmax(-1)
+        assert bool((rank <= n_keep).all()), (rank - n_keep).max()
+        seen.update(t.tolist())
+    assert len(seen) > 1
 
 
 def test_sample_distribution(cuda):
