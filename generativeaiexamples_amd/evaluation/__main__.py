@@ -37,6 +37,8 @@ def main(argv=None):
     ap.add_argument("--judge_base_url", type=str, default="localhost:8000", help="/v1 server for the judge / generator")
     ap.add_argument("--embedding_model", type=str, default="nvidia/nv-embedqa-e5-v5")
     ap.add_argument("--no_embeddings", action="store_true", help="lexical answer similarity/relevancy only")
+    ap.add_argument("--lexical_ragas", action="store_true",
+                    help="ragas metrics from word overlap instead of the judge LLM (no model server needed)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     from .llm import ChatFn
@@ -64,7 +66,9 @@ def main(argv=None):
                 re_ = RemoteEmbeddings(a.judge_base_url if a.judge_base_url.startswith("http") else
                                        "http://" + a.judge_base_url, a.embedding_model)
                 embed = re_.embed_documents
-            print(json.dumps(eval_ragas(a.ev_input, a.ev_result, embed=embed)))
+            judge = None if a.lexical_ragas else ChatFn(a.judge_base_url, a.judge_llm_model, temperature=0.0,
+                                                         max_tokens=512)
+            print(json.dumps(eval_ragas(a.ev_input, a.ev_result, embed=embed, llm=judge)))
         else:
             from .judge import eval_llm_judge
             res = eval_llm_judge(a.ev_input, a.ev_result, ChatFn(a.judge_base_url, a.judge_llm_model, max_tokens=200))

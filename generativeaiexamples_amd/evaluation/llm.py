@@ -20,9 +20,13 @@ class ChatFn:
         self.headers = {"Authorization": f"Bearer {key}"} if key else {}
         self.http = http or httpx.Client(timeout=timeout)
 
-    def __call__(self, messages: List[dict]) -> str:
-        r = self.http.post(self.url, json=dict(model=self.model, messages=messages, stream=False, **self.kw),
-                           headers=self.headers)
+    def __call__(self, messages: List[dict], schema: Optional[dict] = None) -> str:
+        """``schema``: JSON schema the reply must follow (``response_format: json_schema``; the model server
+        enforces it with constrained decoding)."""
+        body = dict(model=self.model, messages=messages, stream=False, **self.kw)
+        if schema is not None:
+            body["response_format"] = {"type": "json_schema", "json_schema": {"name": "reply", "schema": schema}}
+        r = self.http.post(self.url, json=body, headers=self.headers)
         r.raise_for_status()
         return r.json()["choices"][0]["message"]["content"] or ""
 

@@ -12,8 +12,9 @@ Per row (question, answer, contexts, gt_answer, gt_context), every score in [0, 
   ragas_score        harmonic mean of faithfulness, context_relevancy, answer_relevancy, context_recall
                      (reference calculate_ragas_score, evaluator.py:92-94)
 "Supported" is lexical entailment: >= ``support`` of a statement's content words occur in the
-evidence; when a judge LLM is given, faithfulness / context_recall ask it instead (yes/no per
-statement), like ragas.
+evidence. These word-overlap scores are the offline fallback (``--lexical_ragas``); with a judge LLM,
+``eval_ragas`` runs the ragas algorithms themselves (evaluation/ragas_llm.py: statement extraction + NLI
+verdicts, generated-question relevancy, LLM-judged precision / recall / relevancy).
 """
 from __future__ import annotations
 
@@ -105,7 +106,13 @@ def eval_ragas(ev_file: str, ev_result: str, embed=None, llm=None) -> Dict[str, 
     ``<ev_result>.rows.json`` (per row; the reference writes a parquet of the same table)."""
     with open(ev_file, encoding="utf-8") as f:
         data = json.load(f)
-    rows = [dict(d, **score_row(d, embed, llm)) for d in data]
+    if llm is not None:  # the ragas algorithms with a judge LLM (evaluation/ragas_llm.py)
+        from .ragas_llm import RagasJudge
+
+        judge = RagasJudge(llm, embed)
+        rows = [dict(d, **judge.score_row(d)) for d in data]
+    else:
+        rows = [dict(d, **score_row(d, embed)) for d in data]
     agg = {m: statistics.fmean(r[m] for r in rows) for m in METRIC_NAMES if rows}
     four = [agg.get(k, 0.0) for k in ("faithfulness", "context_relevancy", "answer_relevancy", "context_recall")]
     agg["ragas_score"] = statistics.harmonic_mean(four) if all(v > 0 for v in four) else 0.0

@@ -99,3 +99,99 @@ def test_synthetic_answers_and_load_generator(tmp_path):
         from generativeaiexamples_amd.chain_server import utils
         utils.get_config.cache_clear()
         utils.set_hub(None)
+
+
+def _scripted_judge():
+    """A deterministic judge implementing each ragas prompt by word overlap (stands in for the LLM)."""
+    import re as _re
+
+    from generativeaiexamples_amd.evaluation import ragas_llm as R
+
+    def words(t):
+        return set(_re.findall(r"[a-z0-9]+", t.lower())) - {"the", "a", "of", "is", "it", "has"}
+
+    def field(user, name):
+        m = _re.search(rf"{name}:\s*(.*?)(?:\n+(?:Question|Answer|Context|Statements|Return)\b|\Z)", user, _re.S)
+        return m.group(1).strip() if m else ""
+
+    def fn(messages, schema=None):
+        user = messages[-1]["content"]
+        items = [ln[2:] for ln in user.split("\n") if ln.startswith("- ")]
+        ctx = field(user, "Context")
+        if schema is R.S_STATEMENTS:
+            return json.dumps({"statements": R.sentences(field(user, "Answer"))})
+        if schema is R.S_VERDICTS:
+            return json.dumps({"verdicts": [{"statement": s, "verdict": int(words(s) <= words(ctx))} for s in items]})
+        if schema is R.S_QUESTION:
+            a = field(user, "Answer")
+            return json.dumps({"question": a.split("(variant")[0], "noncommittal": int("don't know" in a)})
+        if schema is R.S_VERDICT:
+            c, a = words(field(user, "Context")), words(field(user, "Answer"))
+            return json.dumps({"reason": "", "verdict": int(len(c & a) >= 0.5 * len(a))})
+        if schema is R.S_ATTRIB:
+            return json.dumps({"classifications": [{"statement": s, "attributed": int(words(s) <= words(ctx))}
+                                                   for s in items]})
+        if schema is R.S_SENTENCES:
+            q = words(field(user, "Question"))
+            return json.dumps({"sentences": [s for s in R.sentences(ctx) if len(words(s) & q) >= 2]})
+        raise AssertionError(schema)
+
+    return fn
+
+
+def test_ragas_llm_algorithms_with_scripted_judge(tmp_path):
+    from generativeaiexamples_amd.evaluation.ragas_llm import RagasJudge
+
+    ctx1 = "The MI355X has 288 GB of HBM3E memory. Wavefronts are 64 lanes wide."
+    ctx2 = "Pasta cooks in salted boiling water."
+    emb = lambda texts: [[1.0, 0.2] if "MI355X" in t else [0.1, 1.0] for t in texts]  # noqa: E731
+    j = RagasJudge(_scripted_judge(), emb, n_questions=2)
+    row = {"question": "How much HBM3E memory does the MI355X have?",
+           "answer": "The MI355X has 288 GB of HBM3E memory. It was made of cheese.",
+           "contexts": [ctx2, ctx1], "gt_answer": "The MI355X has 288 GB of HBM3E memory."}
+    s = j.score_row(row)
+    assert s["faithfulness"] == 0.5                 # one of two statements supported
+    assert s["context_precision"] == 0.5            # useful context at rank 2 only: P@2 = 1/2
+    assert s["context_recall"] == 1.0
+    assert abs(s["context_relevancy"] - 1 / 3) < 1e-9  # 1 of 3 context sentences extracted
+    assert s["answer_similarity"] > 0.99 and s["answer_relevancy"] > 0.99 and 0 < s["ragas_score"] < 1
+    vague = j.score_row(dict(row, answer="I don't know."))
+    assert vague["answer_relevancy"] == 0.0 and vague["ragas_score"] == 0.0
+    p = tmp_path / "ev.json"
+    p.write_text(json.dumps([row]))
+    agg = metrics.eval_ragas(str(p), str(tmp_path / "res"), embed=emb, llm=_scripted_judge())
+    assert agg["faithfulness"] == 0.5 and agg["context_precision"] == 0.5
+
+
+def test_ragas_llm_judge_on_served_model_always_parses():
+    """The judge runs on our model server with response_format json_schema: constrained decoding makes every
+    reply valid JSON of the requested shape even from a random-weight model."""
+    from fastapi.testclient import TestClient
+
+    from generativeaiexamples_amd.evaluation import ragas_llm as R
+    from generativeaiexamples_amd.evaluation.llm import ChatFn
+    from generativeaiexamples_amd.serving.hub import HubSpec, ServiceHub
+    from generativeaiexamples_amd.serving.openai_api import create_openai_app
+
+    hub = ServiceHub.build(HubSpec(llm="tiny-llama", embedder=None, device="cpu", max_num_seqs=8, max_model_len=1024,
+                                   use_graphs=False))
+    try:
+        with TestClient(create_openai_app(hub)) as c:
+            judge = ChatFn("http://testserver", "tiny", temperature=0.7, max_tokens=64, http=c)
+            replies = []
+
+            def logged(messages, schema=None):
+                r = judge(messages, schema=schema)
+                replies.append((schema, r))
+                return r
+
+            s = R.RagasJudge(logged, None).score_row(
+                {"question": "What is HBM?", "answer": "High bandwidth memory. It is fast.",
+                 "contexts": ["HBM is high bandwidth memory."], "gt_answer": "High bandwidth memory."})
+            assert all(0.0 <= v <= 1.0 for v in s.values())
+            assert len(replies) >= 4
+            for schema, r in replies:
+                obj = json.loads(r)
+                assert set(schema["required"]) <= set(obj)
+    finally:
+        hub.shutdown()
