@@ -437,6 +437,55 @@ void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>
                        (int)rank, world, slot_bytes, err.data_ptr<int>(), cur_stream());
 }
 
+static void ar_peers(const std::vector<int64_t>& data_ptrs, const std::vector<int64_t>& sig_ptrs, int64_t rank,
+                     void** d, uint32_t** s) {
+  const int world = (int)data_ptrs.size();
+  TORCH_CHECK(world >= 2 && world <= GAI_AR_MAX_WORLD && (int)sig_ptrs.size() == world, "custom_allreduce: world");
+  TORCH_CHECK(rank >= 0 && rank < world, "custom_allreduce: rank");
+  for (int q = 0; q < world; ++q) {
+    d[q] = reinterpret_cast<void*>(data_ptrs[q]);
+    s[q] = reinterpret_cast<uint32_t*>(sig_ptrs[q]);
+  }
+}
+
+void custom_allreduce_twoshot(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
+                              const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
+                              int64_t region_bytes) {
+  check_dev(inp, "inp");
+  check_dev(out, "out");
+  TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.numel() == out.numel(), "two-shot: in/out mismatch");
+  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "two-shot: bf16 or fp32");
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous(), "two-shot: contiguous tensors");
+  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= GAI_AR_MAX_BLOCKS, "two-shot: counters");
+  check_i32(err, "err");
+  void* d[GAI_AR_MAX_WORLD];
+  uint32_t* s[GAI_AR_MAX_WORLD];
+  ar_peers(data_ptrs, sig_ptrs, rank, d, s);
+  gai_custom_allreduce_twoshot(inp.data_ptr(), out.data_ptr(), inp.numel() * inp.element_size(),
+                               inp.scalar_type() == at::kFloat, d, s, reinterpret_cast<uint32_t*>(counters.data_ptr()),
+                               (int)rank, (int)data_ptrs.size(), region_bytes, err.data_ptr<int>(), cur_stream());
+}
+
+void custom_allreduce_rmsnorm(const Tensor& inp, Tensor& out, Tensor& residual, const Tensor& w, double eps,
+                              const std::vector<int64_t>& data_ptrs, const std::vector<int64_t>& sig_ptrs,
+                              Tensor& counters, Tensor& err, int64_t rank, int64_t slot_bytes) {
+  check_bf16(inp, "inp");
+  check_bf16(out, "out");
+  check_bf16(residual, "residual");
+  check_bf16(w, "w");
+  const int D = inp.size(-1);
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && residual.is_contiguous(), "ar_rmsnorm: contiguous");
+  TORCH_CHECK(out.numel() == inp.numel() && residual.numel() == inp.numel() && w.numel() == D, "ar_rmsnorm: shapes");
+  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= GAI_AR_MAX_BLOCKS, "ar_rmsnorm: counters");
+  check_i32(err, "err");
+  void* d[GAI_AR_MAX_WORLD];
+  uint32_t* s[GAI_AR_MAX_WORLD];
+  ar_peers(data_ptrs, sig_ptrs, rank, d, s);
+  gai_custom_allreduce_rmsnorm(inp.data_ptr(), out.data_ptr(), residual.data_ptr(), w.data_ptr(), inp.numel() / D, D,
+                               (float)eps, d, s, reinterpret_cast<uint32_t*>(counters.data_ptr()), (int)rank,
+                               (int)data_ptrs.size(), slot_bytes, err.data_ptr<int>(), cur_stream());
+}
+
 void gemm_splitk_add_rmsnorm(const Tensor& A, const Tensor& B, const optional<Tensor>& bias, Tensor& res,
                              const Tensor& g, Tensor& out, double eps, Tensor& ws, bool psw) {
   check_bf16(A, "A");
@@ -518,6 +567,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_splitk_fusable_norm", [](int64_t M, int64_t N, int64_t K) { return gai_gemm_splitk_fusable_norm(M, N, K) != 0; });
   m.def("gdn_decode", &gdn_decode);
   m.def("custom_allreduce", &custom_allreduce);
+  m.def("custom_allreduce_twoshot", &custom_allreduce_twoshot);
+  m.def("custom_allreduce_rmsnorm", &custom_allreduce_rmsnorm);
   m.def("ipc_malloc", [](int64_t bytes) { return reinterpret_cast<int64_t>(gai_ipc_malloc(bytes)); });
   m.def("ipc_free", [](int64_t p) { gai_ipc_free(reinterpret_cast<void*>(p)); });
   m.def("ipc_get_handle", [](int64_t p) {

@@ -119,6 +119,180 @@ __global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in,
   if (tid == 0) counters[b] = e;
 }
 
+// Fused all-reduce + residual add + RMSNorm (the TP block boundary: row-parallel projection ->
+// all-reduce -> h + residual -> rmsnorm). Steps 1-4 are the one-shot kernel's (same buffers, same
+// block -> byte mapping, so the parity argument above holds across both kernels); step 5 reduces whole
+// rows (the caller guarantees GAI_AR_CHUNK % row_bytes == 0, so a chunk holds complete rows) and
+// applies, with the rounding of the unfused path: h = bf16(sum), r = bf16(h + residual) -> residual,
+// y = bf16(r * rsqrt(mean(r^2) + eps) * w). VPT = 16-byte vectors per thread per row (D = 2048 * VPT).
+template <int W, int VPT>
+__global__ __launch_bounds__(kArThreads) void ar_rmsnorm_kernel(const uint4* in, uint4* out, uint4* residual,
+                                                                const uint4* __restrict__ wgt, ArPtrs p,
+                                                                uint32_t* __restrict__ counters, int rank,
+                                                                int64_t n16, int64_t slot_bytes, float eps, int* err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t e_sh;
+  __shared__ float red[kArThreads / 64];
+  if (tid == 0) e_sh = counters[b] + 1u;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int par = (int)(e & 1u);
+  constexpr int64_t kVec = GAI_AR_CHUNK / 16;
+  constexpr int kRowVec = VPT * kArThreads;  // 16-B vectors per row
+  const int64_t v0 = (int64_t)b * kVec, v1 = min(v0 + kVec, n16);
+  const int64_t my_off = ((int64_t)par * W + rank) * slot_bytes;
+  for (int64_t v = v0 + tid; v < v1; v += kArThreads) {
+    const uint4 x = in[v];
+#pragma unroll
+    for (int q = 0; q < W; ++q) reinterpret_cast<uint4*>(p.data[q] + my_off)[v] = x;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (tid < W) __hip_atomic_store(p.sig[tid] + b * GAI_AR_MAX_WORLD + rank, e, __ATOMIC_RELEASE,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) {
+    uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        atomicOr(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const char* base = p.data[rank] + (int64_t)par * W * slot_bytes;
+  const float inv_d = 1.f / (float)(kRowVec * 8);
+  for (int64_t r0 = v0; r0 < v1; r0 += kRowVec) {
+    float rv[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int64_t v = r0 + j * kArThreads + tid;
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) acc_bf16x8(a, reinterpret_cast<const uint4*>(base + q * slot_bytes)[v]);
+      const uint4 h = uint4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]),
+                            pack_bf16x2(a[6], a[7])};
+      float hr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      acc_bf16x8(hr, h);
+      acc_bf16x8(hr, residual[v]);
+      const uint4 r = uint4{pack_bf16x2(hr[0], hr[1]), pack_bf16x2(hr[2], hr[3]), pack_bf16x2(hr[4], hr[5]),
+                            pack_bf16x2(hr[6], hr[7])};
+      residual[v] = r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rv[j][i] = 0.f;
+      acc_bf16x8(rv[j], r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += rv[j][i] * rv[j][i];
+    }
+    ss = gai::wave_sum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kArThreads / 64; ++i) tot += red[i];
+    __syncthreads();
+    const float rs = rsqrtf(tot * inv_d + eps);
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int64_t v = r0 + j * kArThreads + tid;
+      float wv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      acc_bf16x8(wv, wgt[(v - r0)]);
+      out[v] = uint4{pack_bf16x2(rv[j][0] * rs * wv[0], rv[j][1] * rs * wv[1]),
+                     pack_bf16x2(rv[j][2] * rs * wv[2], rv[j][3] * rs * wv[3]),
+                     pack_bf16x2(rv[j][4] * rs * wv[4], rv[j][5] * rs * wv[5]),
+                     pack_bf16x2(rv[j][6] * rs * wv[6], rv[j][7] * rs * wv[7])};
+    }
+  }
+  if (tid == 0) counters[b] = e;
+}
+
+// Two-shot all-reduce for bandwidth-bound messages: reduce-scatter then all-gather, each over direct
+// peer writes. The one-shot kernel moves the whole message over every link; here each link carries
+// 2/W of it (rank r reduces segment r), at the price of a second signal round. Own buffers (region 0:
+// reduce-scatter inputs, region 1: gathered segments, both [2 parity][W src][region]) and own per-block
+// epochs / signals [block][phase][src]; block b owns bytes [b * CHUNK, (b + 1) * CHUNK) of every
+// segment in both regions, so the one-shot parity argument applies per region.
+template <int W, bool F32>
+__global__ __launch_bounds__(kArThreads) void ar_twoshot_kernel(const uint4* in, uint4* out, ArPtrs p,
+                                                                uint32_t* __restrict__ counters, int rank,
+                                                                int64_t seg16, int64_t region_bytes, int* err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t e_sh;
+  if (tid == 0) e_sh = counters[b] + 1u;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int par = (int)(e & 1u);
+  constexpr int64_t kVec = GAI_AR_CHUNK / 16;
+  const int64_t v0 = (int64_t)b * kVec, v1 = min(v0 + kVec, seg16);
+  const int64_t slot = 2 * region_bytes;
+  const int64_t pbase = (int64_t)par * W * slot;
+  auto wait_phase = [&](int ph) {
+    if (tid < W) {
+      uint32_t* f = p.sig[rank] + (b * 2 + ph) * GAI_AR_MAX_WORLD + tid;
+      uint32_t spins = 0;
+      while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 26)) {
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  };
+  auto signal_phase = [&](int ph) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (tid < W)
+      __hip_atomic_store(p.sig[tid] + (b * 2 + ph) * GAI_AR_MAX_WORLD + rank, e, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  };
+  // 1. reduce-scatter: segment q of my input goes to peer q (region 0, slot `rank`)
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    uint4* dst = reinterpret_cast<uint4*>(p.data[q] + pbase + rank * slot);
+    for (int64_t v = v0 + tid; v < v1; v += kArThreads) dst[v] = in[q * seg16 + v];
+  }
+  signal_phase(0);
+  wait_phase(0);
+  // 2. reduce my segment, keep it, push it to every peer (region 1, slot `rank`)
+  const char* lb = p.data[rank] + pbase;
+  for (int64_t v = v0 + tid; v < v1; v += kArThreads) {
+    uint4 res;
+    if (F32) {
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const uint4 x = reinterpret_cast<const uint4*>(lb + q * slot)[v];
+        s += f32x4_t{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+      }
+      res = uint4{__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
+    } else {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) acc_bf16x8(a, reinterpret_cast<const uint4*>(lb + q * slot)[v]);
+      res = uint4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]), pack_bf16x2(a[6], a[7])};
+    }
+    out[rank * seg16 + v] = res;
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+      if (q != rank) reinterpret_cast<uint4*>(p.data[q] + pbase + rank * slot + region_bytes)[v] = res;
+  }
+  signal_phase(1);
+  wait_phase(1);
+  // 3. all-gather: the other ranks' reduced segments
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    if (q == rank) continue;
+    const uint4* src = reinterpret_cast<const uint4*>(lb + q * slot + region_bytes);
+    for (int64_t v = v0 + tid; v < v1; v += kArThreads) out[q * seg16 + v] = src[v];
+  }
+  if (tid == 0) counters[b] = e;
+}
+
 }  // namespace
 
 void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
@@ -154,6 +328,78 @@ void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, voi
   GAI_AR(7)
 #undef GAI_AR
   gai_launch_error(__FILE__, __LINE__, "custom_allreduce: world size must be 2..8");
+}
+
+void gai_custom_allreduce_twoshot(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
+                                  uint32_t* const* peer_sig, uint32_t* counters, int rank, int world,
+                                  int64_t region_bytes, int* err, hipStream_t st) {
+  if (bytes == 0) return;
+  if (bytes % (16 * world)) gai_launch_error(__FILE__, __LINE__, "allreduce two-shot: bytes % (16 * world) != 0");
+  const int64_t seg = bytes / world;
+  if (seg > region_bytes) gai_launch_error(__FILE__, __LINE__, "allreduce two-shot: message too large");
+  const int64_t nblk = (seg + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
+  if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "allreduce two-shot: too many blocks");
+  ArPtrs p{};
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = static_cast<char*>(peer_data[q]);
+    p.sig[q] = peer_sig[q];
+  }
+#define GAI_AR2(WW)                                                                                          \
+  if (world == WW) {                                                                                         \
+    if (f32)                                                                                                 \
+      ar_twoshot_kernel<WW, true><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p, counters, \
+                                                                    rank, seg / 16, region_bytes, err);      \
+    else                                                                                                     \
+      ar_twoshot_kernel<WW, false><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p,         \
+                                                                     counters, rank, seg / 16, region_bytes, err); \
+    GAI_LAUNCH_CHECK();                                                                                      \
+    return;                                                                                                  \
+  }
+  GAI_AR2(2)
+  GAI_AR2(4)
+  GAI_AR2(8)
+  GAI_AR2(3)
+  GAI_AR2(5)
+  GAI_AR2(6)
+  GAI_AR2(7)
+#undef GAI_AR2
+  gai_launch_error(__FILE__, __LINE__, "allreduce two-shot: world size must be 2..8");
+}
+
+void gai_custom_allreduce_rmsnorm(const void* in, void* out, void* residual, const void* w, int64_t rows, int D,
+                                  float eps, void* const* peer_data, uint32_t* const* peer_sig, uint32_t* counters,
+                                  int rank, int world, int64_t slot_bytes, int* err, hipStream_t st) {
+  if (rows == 0) return;
+  const int64_t row_bytes = (int64_t)D * 2, bytes = rows * row_bytes;
+  if (D % 2048 || GAI_AR_CHUNK % row_bytes || bytes > slot_bytes)
+    gai_launch_error(__FILE__, __LINE__, "allreduce_rmsnorm: D must be 2048 or 4096*k with rows inside a chunk");
+  const int64_t nblk = (bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
+  if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "allreduce_rmsnorm: message too large");
+  ArPtrs p{};
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = static_cast<char*>(peer_data[q]);
+    p.sig[q] = peer_sig[q];
+  }
+  const int vpt = D / 2048;
+#define GAI_ARN(WW, VV)                                                                                       \
+  if (world == WW && vpt == VV) {                                                                             \
+    ar_rmsnorm_kernel<WW, VV><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, (uint4*)residual, \
+                                                                (const uint4*)w, p, counters, rank, bytes / 16,  \
+                                                                slot_bytes, eps, err);                        \
+    GAI_LAUNCH_CHECK();                                                                                       \
+    return;                                                                                                   \
+  }
+#define GAI_ARN_W(WW) GAI_ARN(WW, 1) GAI_ARN(WW, 2) GAI_ARN(WW, 4)
+  GAI_ARN_W(2)
+  GAI_ARN_W(3)
+  GAI_ARN_W(4)
+  GAI_ARN_W(5)
+  GAI_ARN_W(6)
+  GAI_ARN_W(7)
+  GAI_ARN_W(8)
+#undef GAI_ARN_W
+#undef GAI_ARN
+  gai_launch_error(__FILE__, __LINE__, "allreduce_rmsnorm: unsupported world / hidden size");
 }
 
 // --- IPC buffer management (host) ---------------------------------------------------------------

@@ -90,6 +90,15 @@ void gai_vit_embed(const void* patches, const void* cls, const void* pos, void* 
 void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
                           uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
                           int* err, hipStream_t st);
+// two-shot (reduce-scatter + all-gather) over its own buffers: region_bytes per (parity, src, region)
+void gai_custom_allreduce_twoshot(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
+                                  uint32_t* const* peer_sig, uint32_t* counters, int rank, int world,
+                                  int64_t region_bytes, int* err, hipStream_t st);
+// one-shot all-reduce fused with residual add + RMSNorm (bf16 rows of D = 2048 * {1,2,4}); same buffers as
+// gai_custom_allreduce
+void gai_custom_allreduce_rmsnorm(const void* in, void* out, void* residual, const void* w, int64_t rows, int D,
+                                  float eps, void* const* peer_data, uint32_t* const* peer_sig, uint32_t* counters,
+                                  int rank, int world, int64_t slot_bytes, int* err, hipStream_t st);
 void* gai_ipc_malloc(int64_t bytes);
 void gai_ipc_free(void* p);
 void gai_ipc_get_handle(void* p, char* handle64);

@@ -496,6 +496,8 @@ class LlamaModel:
         fuse = (res.is_cuda and ctx.tp_size == 1 and c.norm != "layernorm" and not self.lora_names and T <= 64
                 and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         xn = None
+        # TP: the all-reduce of each row-parallel projection carries the residual add and the next RMSNorm
+        tp_norm = (ctx.tp_size > 1 and c.norm != "layernorm" and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         for i in range(c.num_layers):
             p = f"l{i}."
             if xn is not None:
@@ -520,8 +522,11 @@ class LlamaModel:
                 x = ops.linear_add_rmsnorm(a2, w[p + "o"], res, w[p + "mlp_norm"], c.rms_eps, bias=w.get(p + "o_b"))
             else:
                 h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
-                ctx.tp_all_reduce(h)
-                x = self._norm(h, p + "mlp_norm", residual=res)
+                if tp_norm:  # all-reduce + residual add + RMSNorm in one peer-memory kernel
+                    x = ctx.tp_all_reduce_rmsnorm(h, res, w[p + "mlp_norm"], c.rms_eps)
+                else:
+                    ctx.tp_all_reduce(h)
+                    x = self._norm(h, p + "mlp_norm", residual=res)
             if c.mlp == "gelu_tanh":
                 g = self._lora(ops.linear(x, w[p + "fc"], bias=w.get(p + "fc_b"), act="gelu_tanh"), x, i, "fc", fb)
             else:
@@ -533,7 +538,12 @@ class LlamaModel:
                 h = None
             else:
                 h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
-                ctx.tp_all_reduce(h)
+                if tp_norm and not (last and fb.sample_rows is not None):
+                    nxt = "norm" if last else f"l{i + 1}.attn_norm"
+                    xn = ctx.tp_all_reduce_rmsnorm(h, res, w[nxt], c.rms_eps)
+                    h = None
+                else:
+                    ctx.tp_all_reduce(h)
         if xn is not None:  # the final norm already ran inside the last layer's down projection
             logits = ops.linear(xn, w["lm_head"], out_dtype=torch.float32)
             return ctx.tp_all_gather_last(logits)[:, : c.vocab_size]

@@ -16,6 +16,16 @@ captured into the decode HIP graph like any other kernel. Messages larger than `
 a multiple of 16 bytes go to RCCL. A peer that never arrives makes the kernel give up after a
 bounded spin and set an error word (checked by :meth:`check`), never hang the GPU.
 
+Two more kernels share the machinery:
+
+* two-shot (``algo="twoshot"``, auto above ``GAI_AR_TWOSHOT_MIN_KB`` = 512 KiB at world > 2):
+  reduce-scatter then all-gather, both as direct peer writes, over a second buffer set - each xGMI
+  link carries 2/W of the message instead of all of it, which is what bounds large messages on the
+  point-to-point mesh;
+* ``all_reduce_rmsnorm``: the one-shot exchange fused with the residual add and the next RMSNorm
+  (``DistContext.tp_all_reduce_rmsnorm``, used at every TP block boundary of the Llama family), one
+  kernel and one pass over the activations instead of all-reduce + add&norm.
+
 Reference parity: the reference has no in-repo collective (NCCL is implicit inside TRT-LLM,
 SURVEY §2.4 P1); this is the "custom one-shot xGMI all-reduce for <= 1 MiB" of its MI355X design.
 """
@@ -66,6 +76,27 @@ class CustomAllReduce:
                     self.sig_ptrs.append(ps)
             self.counters = torch.zeros(C.AR_MAX_BLOCKS, dtype=torch.int32, device=self.device)
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            # two-shot buffers: [2 parity][world src][2 regions][region] with region = max_bytes / world,
+            # signals [block][2 phases][8], own epochs
+            self.region_bytes = -(-self.max_bytes // self.world // C.AR_CHUNK) * C.AR_CHUNK
+            self._data2 = C.ipc_malloc(2 * self.world * 2 * self.region_bytes)
+            self._sig2 = C.ipc_malloc(C.AR_MAX_BLOCKS * 2 * 8 * 4)
+            handles2 = (C.ipc_get_handle(self._data2), C.ipc_get_handle(self._sig2))
+            allh2: List = [None] * self.world
+            dist.all_gather_object(allh2, handles2, group=group)
+            self.data2_ptrs, self.sig2_ptrs = [], []
+            for q, (hd, hs) in enumerate(allh2):
+                if q == self.rank:
+                    self.data2_ptrs.append(self._data2)
+                    self.sig2_ptrs.append(self._sig2)
+                else:
+                    pd, ps = C.ipc_open(hd), C.ipc_open(hs)
+                    self._opened += [pd, ps]
+                    self.data2_ptrs.append(pd)
+                    self.sig2_ptrs.append(ps)
+            self.counters2 = torch.zeros(C.AR_MAX_BLOCKS, dtype=torch.int32, device=self.device)
+            # one-shot below this size, two-shot above (2 ranks: one-shot always - same bytes per link)
+            self.twoshot_min = int(os.environ.get("GAI_AR_TWOSHOT_MIN_KB", "512")) << 10
         torch.cuda.synchronize(self.device)
         dist.barrier(group=group)  # every peer has mapped every buffer before the first launch
         self._closed = False
@@ -75,11 +106,37 @@ class CustomAllReduce:
         return (not self._closed and t.is_cuda and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32)
                 and 0 < nbytes <= self.max_bytes and nbytes % 16 == 0)
 
-    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Sum ``t`` over the group (in place unless ``out`` is given). Graph-capturable."""
+    def algo_for(self, nbytes: int) -> str:
+        if self.world > 2 and nbytes >= self.twoshot_min and nbytes % (16 * self.world) == 0:
+            return "twoshot"
+        return "oneshot"
+
+    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None, algo: str = "auto") -> torch.Tensor:
+        """Sum ``t`` over the group (in place unless ``out`` is given). Graph-capturable. ``algo``: oneshot
+        (every rank pushes the whole message to every peer: one hop, latency-bound sizes), twoshot
+        (reduce-scatter + all-gather over direct peer writes: 2/W of the message per link), auto."""
         out = t if out is None else out
-        _native().custom_allreduce(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
-                                   self.max_bytes)
+        nbytes = t.numel() * t.element_size()
+        if algo == "auto":
+            algo = self.algo_for(nbytes)
+        if algo == "twoshot":
+            _native().custom_allreduce_twoshot(t, out, self.data2_ptrs, self.sig2_ptrs, self.counters2, self.err,
+                                               self.rank, self.region_bytes)
+        else:
+            _native().custom_allreduce(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
+                                       self.max_bytes)
+        return out
+
+    def eligible_rmsnorm(self, t: torch.Tensor) -> bool:
+        D = t.shape[-1]
+        return (self.eligible(t) and t.dtype == torch.bfloat16 and D % 2048 == 0 and 16384 % (2 * D) == 0)
+
+    def all_reduce_rmsnorm(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """residual += all_reduce(t); return rmsnorm(residual) * w - one kernel (see custom_ar.hip)."""
+        out = torch.empty_like(t) if out is None else out
+        _native().custom_allreduce_rmsnorm(t, out, residual, w, eps, self.data_ptrs, self.sig_ptrs, self.counters,
+                                           self.err, self.rank, self.max_bytes)
         return out
 
     def check(self) -> None:
@@ -100,6 +157,8 @@ class CustomAllReduce:
             C.ipc_close(p)
         C.ipc_free(self._data)
         C.ipc_free(self._sig)
+        C.ipc_free(self._data2)
+        C.ipc_free(self._sig2)
         self._closed = True
 
 

@@ -69,6 +69,21 @@ class DistContext:
                     t.copy_(f)
         return t
 
+    def tp_all_reduce_rmsnorm(self, h: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float
+                              ) -> torch.Tensor:
+        """The TP block boundary: all-reduce the row-parallel partial sums ``h``, add them to ``residual``
+        (in place) and return rmsnorm(residual) * w. On the custom all-reduce this is ONE kernel (peer push,
+        reduce, residual add and norm over whole rows), otherwise the all-reduce plus the fused add+norm
+        kernel; both round like the unfused path."""
+        from .. import ops
+
+        car = self.custom_ar
+        if self.tp_size > 1 and car is not None and car.eligible_rmsnorm(h):
+            with guard("tp_custom_all_reduce_rmsnorm", self.rank):
+                return car.all_reduce_rmsnorm(h, residual, w, eps)
+        self.tp_all_reduce(h)
+        return ops.rms_norm(h, w, eps, residual=residual)
+
     def check_comm(self) -> None:
         """Poll the device-side error word of the custom all-reduce; call at a point that has already
         synchronised with the stream (the engine does it after copying the sampled tokens to the host). A

@@ -7,6 +7,15 @@ then one variable-split ``all_to_all_single`` of the rows, expert ids and routin
 runs all-to-all as direct peer transfers, one xGMI link per peer); the owner runs its grouped
 GEMMs on the received rows; ``combine`` returns the expert outputs with the reverse all-to-all and
 reduces them with the routing weights into the token order.
+
+``dispatch_padded`` / ``local_experts_padded`` / ``combine_padded`` are the decode-time variant: every
+rank sends each peer a fixed-capacity slab (``capacity`` rows, default T*k = dropless), positions
+inside a slab are computed on the device (scatter / cumsum, no ``bincount`` / ``.tolist()``), padding
+rows carry the sentinel expert id ``e_local`` that the grouped GEMM skips, and both exchanges are
+equal-split ``all_to_all_single`` calls - no host synchronisation anywhere, so a whole MoE decode step
+(routing, dispatch, grouped GEMMs, combine) can be captured in one HIP graph. The price is bandwidth:
+W x capacity rows per exchange instead of the exact counts, which at decode batch sizes (tens of tokens)
+is a few MB over xGMI and far cheaper than a host round trip.
 """
 from __future__ import annotations
 
@@ -83,3 +92,66 @@ def local_experts(rows: torch.Tensor, eid: torch.Tensor, w13: torch.Tensor, w2: 
     y = torch.empty_like(y_sorted)
     y[order] = y_sorted
     return y
+
+
+@dataclass
+class EPPaddedPlan:
+    slot: torch.Tensor  # [T*k] slab row of every (token, choice) pair on the send side
+    capacity: int
+    num_tokens: int
+    top_k: int
+
+
+def _a2a_equal(x: torch.Tensor, group) -> torch.Tensor:
+    out = torch.empty_like(x)
+    if x.is_cuda or x.dtype in (torch.float32, torch.int64, torch.int32):
+        dist.all_to_all_single(out, x.contiguous(), group=group)
+        return out
+    o32 = torch.empty(x.shape, dtype=torch.float32)
+    dist.all_to_all_single(o32, x.float().contiguous(), group=group)
+    return o32.to(x.dtype)
+
+
+def dispatch_padded(x: torch.Tensor, ids: torch.Tensor, num_experts: int, capacity: int | None = None, group=None):
+    """-> (rows [W*C, D], local expert ids [W*C] int32 (e_local = padding), plan). Sync-free, capturable.
+    Pairs beyond ``capacity`` for one destination are dropped (capacity = T*k never drops)."""
+    world = dist.get_world_size(group)
+    e_local = num_experts // world
+    T, k = ids.shape
+    P = T * k
+    C = P if capacity is None else capacity
+    flat = ids.reshape(-1).long()
+    dest = flat // e_local
+    onehot = torch.zeros(P, world, dtype=torch.int32, device=x.device).scatter_(1, dest[:, None], 1)
+    pos = (onehot.cumsum(0) * onehot).sum(1) - 1            # rank of the pair inside its destination slab
+    keep = pos < C
+    slot = torch.where(keep, dest * C + pos, torch.full_like(pos, world * C))  # dropped -> scratch row
+    send = torch.zeros(world * C + 1, x.shape[1], dtype=x.dtype, device=x.device)
+    send[slot] = x[torch.arange(P, device=x.device) // k]
+    send_eid = torch.full((world * C + 1,), e_local, dtype=torch.int32, device=x.device)
+    send_eid[slot] = (flat % e_local).to(torch.int32)
+    rows = _a2a_equal(send[:-1], group)
+    eid = _a2a_equal(send_eid[:-1], group)
+    return rows, eid, EPPaddedPlan(slot, C, T, k)
+
+
+def local_experts_padded(rows: torch.Tensor, eid: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """Grouped expert GEMMs over a padded slab: the device-side dispatch plan sorts the sentinel rows
+    last and the grouped GEMM's tile walk stops at offs[e_local], so padding costs no FLOPs."""
+    from .. import ops
+
+    e_local = w13.shape[0]
+    R = rows.shape[0]
+    a_rows, offs, pos = ops.moe_dispatch(eid.view(-1, 1), e_local + 1)
+    h1 = ops.moe_gemm(rows, a_rows, w13, offs, R, True)
+    y_sorted = ops.moe_gemm(h1, None, w2, offs, R, False)
+    return y_sorted[pos.view(-1).long()]
+
+
+def combine_padded(y: torch.Tensor, weights: torch.Tensor, plan: EPPaddedPlan, group=None) -> torch.Tensor:
+    back = _a2a_equal(y, group)
+    back = torch.cat([back, back.new_zeros(1, back.shape[1])])  # scratch row of dropped pairs
+    pair = back[plan.slot].float()
+    w = weights.reshape(-1, 1).to(torch.float32) * (plan.slot < back.shape[0] - 1).float()[:, None]
+    out = (pair * w).view(plan.num_tokens, plan.top_k, -1).sum(1)
+    return out.to(y.dtype)

@@ -66,6 +66,38 @@ def ep_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def ep_padded_worker(rank, world, port, out_dir):
+    """Sync-free fixed-capacity EP exchange (graph-capturable decode path) vs the single-process oracle."""
+    _init(rank, world, port, 1)
+    from generativeaiexamples_amd import ops
+    from generativeaiexamples_amd.parallel import ep
+
+    E, D, I, k = 8, 64, 32, 2
+    g = torch.Generator().manual_seed(5)
+    w13 = (torch.randn(E, 2 * I, D, generator=g) / 8).to(torch.bfloat16)
+    w2 = (torch.randn(E, D, I, generator=g) / 6).to(torch.bfloat16)
+    x_all = torch.randn(world, 7, D, generator=g).to(torch.bfloat16)
+    logit_all = torch.randn(world, 7, E, generator=g)
+    x, logits = x_all[rank], logit_all[rank]
+    ids, w = ops.moe_route(logits, k)
+    e_local = E // world
+    mine = slice(rank * e_local, (rank + 1) * e_local)
+    rows, eid, plan = ep.dispatch_padded(x, ids, E, None, None)
+    assert rows.shape[0] == world * 7 * k
+    y = ep.local_experts_padded(rows, eid, w13[mine], w2[mine])
+    out = ep.combine_padded(y, w, plan, None)
+    a_rows, offs, pos = ops.moe_dispatch(ids, E)
+    h1 = ops.moe_gemm(x, a_rows, w13, offs, x.shape[0] * k, True)
+    exp = ops.moe_combine(ops.moe_gemm(h1, None, w2, offs, x.shape[0] * k, False), pos, w)
+    # a capacity of 1 row per peer drops pairs: their contribution is zero, never garbage
+    rows1, eid1, plan1 = ep.dispatch_padded(x, ids, E, 1, None)
+    out1 = ep.combine_padded(ep.local_experts_padded(rows1, eid1, w13[mine], w2[mine]), w, plan1, None)
+    torch.save({"out": out.float(), "exp": exp.float(), "out1": out1.float()},
+               os.path.join(out_dir, f"ep_padded_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def sharded_index_worker(rank, world, port, out_dir):
     _init(rank, world, port, 1)
     from generativeaiexamples_amd.index.hbm_index import HBMIndex
@@ -301,6 +333,42 @@ def custom_ar_worker(rank, world, port, out_dir):
             e = (y.float().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
             if not e < tol:
                 errs.append(f"n={n} {dtype} rel err {e}")
+    # explicit algorithms: two-shot (reduce-scatter + all-gather) and one-shot on the same messages
+    for it, n in enumerate([world * 8, world * 4096, world * 8192 + world * 8, 1 << 20, (4 << 20) // 4]):
+        for algo in ("twoshot", "oneshot"):
+            for dtype in (torch.bfloat16, torch.float32):
+                nbytes = n * (2 if dtype == torch.bfloat16 else 4)
+                if nbytes > car.max_bytes or nbytes % (16 * world):
+                    continue
+                x, ref = inputs(n, dtype, 500 + 10 * it + (dtype == torch.float32))
+                torch.cuda.synchronize()
+                dist.barrier()
+                y = car.all_reduce(x.clone(), algo=algo)
+                torch.cuda.synchronize()
+                tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+                e = (y.float().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+                if not e < tol:
+                    errs.append(f"{algo} n={n} {dtype} rel err {e}")
+    # fused all-reduce + residual add + RMSNorm vs the unfused rounding
+    for D in (2048, 4096, 8192):
+        for T in (1, 7, 64):
+            g0 = torch.Generator().manual_seed(D + T)
+            xs = [torch.randn(T, D, generator=g0).to(torch.bfloat16) for _ in range(world)]
+            res0 = torch.randn(T, D, generator=g0).to(torch.bfloat16)
+            wn = (torch.rand(D, generator=g0) + 0.5).to(torch.bfloat16)
+            h = torch.stack([x.float() for x in xs]).sum(0).to(torch.bfloat16)
+            r = (h.float() + res0.float()).to(torch.bfloat16)
+            want = (r.float() * torch.rsqrt(r.float().pow(2).mean(-1, keepdim=True) + 1e-5) * wn.float())
+            res = res0.to(dev)
+            torch.cuda.synchronize()
+            dist.barrier()
+            y = car.all_reduce_rmsnorm(xs[rank].to(dev), res, wn.to(dev), 1e-5)
+            torch.cuda.synchronize()
+            if not torch.equal(res.cpu(), r):
+                errs.append(f"ar_rmsnorm D={D} T={T}: residual differs from bf16(h + res)")
+            e = (y.float().cpu() - want).abs().max().item()
+            if not e < 3e-2 * want.abs().max().item():
+                errs.append(f"ar_rmsnorm D={D} T={T} err {e}")
     # graph capture: three chained all-reduces on static buffers, replayed with new inputs
     n = 64 * 4096
     static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
@@ -311,10 +379,15 @@ def custom_ar_worker(rank, world, port, out_dir):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
+    big = torch.zeros(1 << 20, dtype=torch.bfloat16, device=dev)
+    with torch.cuda.stream(s):
+        car.all_reduce(big, algo="twoshot")  # warm the two-shot epochs too
+    torch.cuda.synchronize()
     with torch.cuda.graph(g):
         car.all_reduce(static)
         static.mul_(0.5)
         car.all_reduce(static)
+        car.all_reduce(big, algo="twoshot")
     for rep in range(4):
         x, ref = inputs(n, torch.bfloat16, 7000 + rep)
         static.copy_(x)
@@ -326,6 +399,14 @@ def custom_ar_worker(rank, world, port, out_dir):
         e = (static.float().cpu() - want).abs().max().item() / (want.abs().max().item() + 1e-6)
         if not e < 3e-2:
             errs.append(f"graph replay {rep} rel err {e}")
+        if rep == 0:
+            big.fill_(1.0)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            if not torch.all(big.float().cpu() == float(world)).item():  # every rank contributed ones
+                errs.append("graph replay two-shot: wrong sum")
     car.check()
     # rough latency (on a shared single GPU: all ranks time-slice one device)
     t = torch.zeros(64 * 8192, dtype=torch.bfloat16, device=dev)

@@ -39,6 +39,17 @@ def test_expert_parallel_all_to_all(tmp_path):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_ep_padded_dispatch(tmp_path, world):
+    """Fixed-capacity, sync-free EP exchange (the graph-capturable decode path) at 2 and 4 ranks."""
+    mp.spawn(W.ep_padded_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        d = torch.load(tmp_path / f"ep_padded_{r}.pt", weights_only=True)
+        assert (d["out"] - d["exp"]).abs().max().item() < 3e-2
+        assert torch.isfinite(d["out1"]).all()
+
+
+@pytest.mark.timeout(300)
 def test_sharded_index_matches_global(tmp_path):
     mp.spawn(W.sharded_index_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):

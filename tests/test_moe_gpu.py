@@ -68,3 +68,45 @@ def test_tuned_linear_paths_agree(cuda):
         finally:
             ops.TUNER.mode = old
         _close(y1, y2, 3e-2, 2e-2, f"paths {act}")
+
+
+def test_ep_padded_step_graph_capture(cuda, monkeypatch):
+    """The fixed-capacity EP exchange has no host synchronisation: routing + dispatch + grouped GEMMs +
+    combine capture in one HIP graph and the replay matches eager execution. One GPU: the equal-split
+    exchange is the identity at world 1 (patched in; the multi-rank numerics run on gloo in
+    test_distributed_cpu.py, RCCL all_to_all_single itself is capturable)."""
+    from generativeaiexamples_amd.parallel import ep
+
+    monkeypatch.setattr(ep.dist, "get_world_size", lambda group=None: 1)
+    monkeypatch.setattr(ep, "_a2a_equal", lambda x, group: x.clone())
+    torch.manual_seed(11)
+    E, D, I, k, T = 8, 1024, 512, 2, 48
+    w13 = (torch.randn(E, 2 * I, D, device=cuda) / 32).to(torch.bfloat16)
+    w2 = (torch.randn(E, D, I, device=cuda) / 22).to(torch.bfloat16)
+    wr = (torch.randn(E, D, device=cuda) / 32).to(torch.bfloat16)
+    x = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
+
+    def step():
+        logits = ops.linear(x, wr, out_dtype=torch.float32)
+        ids, wts = ops.moe_route(logits, k)
+        rows, eid, plan = ep.dispatch_padded(x, ids, E)
+        return ep.combine_padded(ep.local_experts_padded(rows, eid, w13, w2), wts, plan)
+
+    s_ = torch.cuda.Stream()
+    s_.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s_):
+        step()
+    torch.cuda.current_stream().wait_stream(s_)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    x.copy_(torch.randn_like(x))
+    g.replay()
+    torch.cuda.synchronize()
+    _close(out, step(), 2e-2, 2e-2, "graph replay vs eager")
+    ids, wts = ops.moe_route(ops.linear(x, wr, out_dtype=torch.float32), k)
+    a_rows, offs, pos = ops.moe_dispatch(ids, E)
+    dense = ops.moe_combine(ops.moe_gemm(ops.moe_gemm(x, a_rows, w13, offs, T * k, True), None, w2, offs, T * k,
+                                         False), pos, wts)
+    _close(out, dense, 2e-2, 2e-2, "padded EP vs local MoE")
