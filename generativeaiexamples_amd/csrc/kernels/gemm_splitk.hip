@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict
 //  * with KS = 1 the epilogue (SwiGLU on the [gate16|up16] interleave, bias, GELU, residual, fp32
 //    logits) is applied by the workgroup itself: no reduce launch.
 constexpr int kDepth = 3;    // k32 steps in flight per wave
+constexpr int kSlots = kDepth + 1;  // register sets of the ring
 constexpr int kLdsRow = 68;  // fp32 row stride of the reduction tiles
 
 template <int MB>
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
                 : W + (size_t)min(n0 + 16 * j + (lane & 15), N - 1) * K + kbeg + kq;
   constexpr int kStepW = PSW ? 512 : 32;
 
-  bf16x8 ra[kDepth][MB], rw[kDepth][4];
+  bf16x8 ra[kSlots][MB], rw[kSlots][4];
   auto load = [&](int s, bf16x8 (&a)[MB], bf16x8 (&w)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = load8(wp[j] + kStepW * s);
@@ -174,20 +175,27 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
   };
 
-  // prologue, then per step: MFMAs on the oldest ring slot, refill that slot 3 steps ahead
+  // prologue, then per step: MFMAs on the oldest ring slot, refill that slot kDepth steps ahead.
+  // The ring has kSlots = kDepth + 1 register sets: step s first issues the loads of step s + kDepth
+  // into the set step s - 1 has just released, then runs its MFMAs, so kDepth steps are always in
+  // flight. The loop is branch-free (past the end a load re-reads the last step, an L2 hit) and each
+  // step is pinned by a sched_barrier: with a refill under a branch, or reusing the set being
+  // multiplied, hipcc sank the refills below later MFMAs and waited vmcnt(0..3) at the top of every
+  // ring turn, draining the pipeline (measured 2.7-3.5 TB/s at M = 64).
 #pragma unroll
-  for (int d = 0; d < kDepth; ++d)
-    if (d < nsteps) load(d, ra[d], rw[d]);
+  for (int d = 0; d < kDepth; ++d) load(min(d, nsteps - 1), ra[d], rw[d]);
   int s = 0;
-  for (; s + kDepth < nsteps; s += kDepth) {
+  for (; s + kSlots <= nsteps; s += kSlots) {
 #pragma unroll
-    for (int d = 0; d < kDepth; ++d) {
+    for (int d = 0; d < kSlots; ++d) {
+      load(min(s + d + kDepth, nsteps - 1), ra[(d + kDepth) % kSlots], rw[(d + kDepth) % kSlots]);
       mma(ra[d], rw[d]);
-      if (s + d + kDepth < nsteps) load(s + d + kDepth, ra[d], rw[d]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  // tail (< kSlots <= kDepth + 1 steps, all already loaded into sets 0, 1, ...)
 #pragma unroll
-  for (int d = 0; d < kDepth; ++d)
+  for (int d = 0; d < kSlots - 1; ++d)
     if (s + d < nsteps) mma(ra[d], rw[d]);
 
   // in-workgroup K reduction: tile[w][m][n] (row stride kLdsRow)

@@ -99,7 +99,9 @@ def test_ep_padded_step_graph_capture(cuda, monkeypatch):
     torch.cuda.current_stream().wait_stream(s_)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # inference mode as in the engine's captures: an earlier test may have created the CUDA generator's
+    # graph-safe state as an inference tensor, which capture_begin then updates in place
+    with torch.inference_mode(), torch.cuda.graph(g):
         out = step()
     x.copy_(torch.randn_like(x))
     g.replay()

@@ -91,6 +91,49 @@ def bench_psw(rows, shapes):
         del ws_, sh_
 
 
+def bench_dec_hbm(rows, shapes, rounds=5):
+    """Decode GEMMs as the engine runs them: weights streamed from HBM (a pool of copies larger than the
+    256 MB Infinity Cache, cycled), the fused epilogue included. Arms, interleaved per round: native
+    split-K on the natural [N, K] layout, native on fragment-shuffled weights, hipBLASLt + the framework's
+    epilogue kernel. (M, N, K, act, out_dtype, name)."""
+    nat = ops.native()
+    for M, N, K, act, odt, name in shapes:
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        ncopy = max(2, -(-(640 << 20) // (N * K * 2)))
+        ws_ = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(ncopy)]
+        sh_ = [ops.shuffle_fragments(w) for w in ws_] if N % 16 == 0 else None
+        ncol = N // 2 if act == "swiglu" else N
+        out = torch.empty(M, ncol, device="cuda", dtype=odt)
+        wsp = torch.empty(max(1, nat.gemm_splitk_ws_floats(M, N, K)), dtype=torch.float32, device="cuda")
+        epi = ops.EPI[act]
+        it = [0]
+
+        def nxt(pool):
+            it[0] = (it[0] + 1) % ncopy
+            return pool[it[0]]
+        arms = {"native": lambda: nat.gemm_splitk(x, nxt(ws_), out, None, None, epi, wsp, False),
+                "blas": lambda: ops._blas_linear(x, nxt(ws_), None, act, odt)}
+        if sh_ is not None:
+            arms["native_psw"] = lambda: nat.gemm_splitk(x, nxt(sh_), out, None, None, epi, wsp, True)
+        ts = {k: [] for k in arms}
+        for _ in range(rounds):
+            for k, f in arms.items():
+                ts[k].append(timeit(f, iters=30) * 1e3)
+        nat.gemm_splitk(x, ws_[0], out, None, None, epi, wsp, False)
+        ref_ = ops._blas_linear(x, ws_[0], None, act, odt)
+        err = (out.float() - ref_.float()).abs().max().item()
+        by = N * K * 2
+        r = dict(op="dec_hbm", name=name, M=M, N=N, K=K, act=act, max_err_vs_blas=err)
+        for k, v in ts.items():
+            v.sort()
+            r[f"{k}_us"] = v[len(v) // 2]
+            r[f"{k}_tbs"] = by / (v[len(v) // 2] * 1e3)
+        r["native_vs_blas"] = r["blas_us"] / r["native_us"]
+        rows.append(r)
+        print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
+        del ws_, sh_
+
+
 def bench_fp8(rows, shapes):
     """fp8 GEMM (block-scaled MFMA) alone and with the fused per-token quantiser, vs bf16 hipBLASLt and
     (when this torch build has it) hipBLASLt fp8 via torch._scaled_mm."""
@@ -204,6 +247,14 @@ def main():
             sh += [(M, 6144, 4096, f"qkv b{M}"), (M, 4096, 4096, f"o b{M}"), (M, 28672, 4096, f"gate_up b{M}"),
                    (M, 4096, 14336, f"down b{M}")]
         bench_psw(rows, sh)
+    if "dec_hbm" in only:
+        bf, f32 = torch.bfloat16, torch.float32
+        sh = []
+        for M in (64, 1):
+            sh += [(M, 6144, 4096, None, bf, f"qkv b{M}"), (M, 4096, 4096, None, bf, f"o b{M}"),
+                   (M, 28672, 4096, "swiglu", bf, f"gate_up+swiglu b{M}"), (M, 4096, 14336, None, bf, f"down b{M}"),
+                   (M, 128256, 4096, None, f32, f"lm_head b{M}")]
+        bench_dec_hbm(rows, sh)
     if "fp8" in only:
         bench_fp8(rows, [(4096, 6144, 4096, "qkv prefill"), (4096, 28672, 4096, "gate_up prefill"),
                          (4096, 4096, 14336, "down prefill"), (8192, 8192, 8192, "square 8k"),
