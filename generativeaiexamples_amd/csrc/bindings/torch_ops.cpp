@@ -538,6 +538,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8", &gemm_fp8);
   m.def("gemm_splitk", &gemm_splitk, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("R"), pybind11::arg("epi"), pybind11::arg("ws"), pybind11::arg("psw") = false);
+  m.def("gemm_dec2_ok", [](int64_t M, int64_t N, int64_t K, int64_t epi) {
+    return gai_gemm_dec2_ok((int)M, (int)N, (int)K, (int)epi) != 0;
+  });
   m.def("gemm_splitk_ws_floats", [](int64_t M, int64_t N, int64_t K) {
     return (int64_t)(gai_gemm_splitk_ws_bytes(M, N, K) / 4);
   });

@@ -35,6 +35,13 @@ size_t gai_gemm_splitk_ws_bytes(int M, int N, int K);
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                      int ldc, int epi, int out_f32, float* ws, int psw, hipStream_t st);
 
+// gemm_decode.hip (decode M <= 64 on the natural [N, K] weight layout: activations staged once per
+//                  workgroup in LDS, weights streamed through a register ring, epilogue fused; returns false
+//                  when the shape does not fit (caller falls back to gai_gemm_splitk's kernels))
+int gai_gemm_dec2_ok(int M, int N, int K, int epi);
+bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                   int epi, int out_f32, hipStream_t st);
+
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,

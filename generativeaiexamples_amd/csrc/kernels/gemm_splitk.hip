@@ -30,13 +30,13 @@ __device__ __forceinline__ size_t psw_offset(int nt, int kt, int K, int lane) {
   return (((size_t)nt * (K / 32) + kt) * 64 + lane) * 8;
 }
 
-template <int MB, bool PSW>
-__global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                          float* __restrict__ part, int M, int N, int K, int KL) {
+template <int MB, bool PSW, int WPG>
+__global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                               float* __restrict__ part, int M, int N, int K, int KL) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // A slice [16*MB][KL] bf16, swizzled chunks
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int n0 = blockIdx.x * 64;
+  const int n0 = blockIdx.x * 16 * WPG;  // WPG waves x 16 columns share one staged activation slice
   const int ks = blockIdx.y;
   const int k0 = ks * KL;
   const int cpr = KL / 8;  // 16-B chunks per staged row (multiple of 64)
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_kernel(const bf16* __restrict
 
   // ---- stage the activation slice: chunk p -> row p / cpr, physical chunk pc, logical pc ^ (row & 15)
   const int chunks = ROWS * cpr;  // multiple of 256 (cpr % 64 == 0, ROWS % 16 == 0)
-  for (int base = wid * 64; base < chunks; base += 256) {
+  for (int base = wid * 64; base < chunks; base += 64 * WPG) {
     const int p = base + lane;
     const int row = p / cpr, pc = p % cpr, c = pc ^ (row & 15);
     const bf16* src = A + (size_t)min(row, M - 1) * K + k0 + c * 8;
@@ -309,13 +309,20 @@ void launch_reduce(const float* part, int KS, int M, int N, void* C, const void*
 
 namespace {
 
+// Waves per workgroup of the slice-staging kernel: every workgroup stages its activation K-slice once,
+// so 8 waves (128 columns) halve the activation bytes per weight byte of 4 waves (64 columns).
+int splitk_wpg() {
+  static const int v = getenv("GAI_SPLITK_WPG") ? atoi(getenv("GAI_SPLITK_WPG")) : 8;
+  return v == 4 ? 4 : 8;
+}
+
 // Legacy (whole-slice staging) K-split: the grid reaches ~2 workgroups per CU while the slice fits LDS.
 int legacy_ks(int M, int N, int K) {
   if (K % kKAlign) return 0;
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   const int kl_max = (128 * 1024) / (16 * MB * 2);  // LDS bytes / row bytes
   const int units = K / kKAlign;
-  const int tiles = (N + 63) / 64;
+  const int tiles = (N + 16 * splitk_wpg() - 1) / (16 * splitk_wpg());
   int best = units;  // KS = units / d for a divisor d of units
   for (int d = units; d >= 1; --d) {
     if (units % d) continue;
@@ -418,29 +425,37 @@ void launch_partials(const void* A, const void* B, int M, int N, int K, int KS, 
   }
   const int KL = K / KS;
   const size_t lds = (size_t)16 * MB * KL * 2;
-  dim3 grid((N + 63) / 64, KS);
-#define GAI_SK(MBV)                                                                                          \
-  case MBV: {                                                                                                \
-    static bool once = false;                                                                                \
-    if (!once) {                                                                                             \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, false>),                     \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true>),                      \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
-      once = true;                                                                                           \
-    }                                                                                                        \
-    if (psw)                                                                                                 \
-      gemm_splitk_kernel<MBV, true><<<grid, 256, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, KL); \
-    else                                                                                                     \
-      gemm_splitk_kernel<MBV, false><<<grid, 256, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, KL);\
-    GAI_LAUNCH_CHECK();                                                                                      \
-    break;                                                                                                   \
+  const int wpg = splitk_wpg();
+  dim3 grid((N + 16 * wpg - 1) / (16 * wpg), KS);
+#define GAI_SK1(MBV, WPGV)                                                                                       \
+  {                                                                                                              \
+    static bool once = false;                                                                                    \
+    if (!once) {                                                                                                 \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, false, WPGV>),                   \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                               \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true, WPGV>),                    \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                               \
+      once = true;                                                                                               \
+    }                                                                                                            \
+    if (psw)                                                                                                     \
+      gemm_splitk_kernel<MBV, true, WPGV><<<grid, 64 * WPGV, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, \
+                                                                        K, KL);                                  \
+    else                                                                                                         \
+      gemm_splitk_kernel<MBV, false, WPGV><<<grid, 64 * WPGV, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M,   \
+                                                                         N, K, KL);                              \
+    GAI_LAUNCH_CHECK();                                                                                          \
   }
+#define GAI_SK(MBV)                   \
+  case MBV:                           \
+    if (wpg == 4) GAI_SK1(MBV, 4)     \
+    else GAI_SK1(MBV, 8)              \
+    break;
   switch (MB) {
     GAI_SK(1)
     GAI_SK(2)
     GAI_SK(4)
   }
+#undef GAI_SK1
 #undef GAI_SK
 }
 
@@ -513,6 +528,14 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
                                  int M, int N, int K, float eps, float* ws, int psw, hipStream_t st) {
   if (M == 0) return;
   if (!gai_gemm_splitk_fusable_norm(M, N, K)) gai_launch_error(__FILE__, __LINE__, "gemm_splitk_add_rmsnorm: shape");
+  if (!psw && gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) {
+    // decode GEMM on the natural layout into a bf16 scratch h (the workspace), then the residual-add
+    // RMSNorm kernel: res = bf16(h + res), out = rmsnorm(res) * g - the same roundings as the fused tail
+    bf16* h = reinterpret_cast<bf16*>(ws);
+    gai_gemm_dec2(A, B, h, bias, nullptr, M, N, K, N, bias ? EPI_BIAS : EPI_NONE, 0, st);
+    gai_rmsnorm(h, res, res, g, out, M, N, eps, st);
+    return;
+  }
   const int KS = gai_gemm_splitk_ks(M, N, K);
   launch_partials(A, B, M, N, K, KS, ws, psw, st);
   const int nch = (N + 2047) / 2048;
@@ -535,6 +558,8 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
   if (psw && N % 16) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: pre-shuffled weights need N % 16 == 0");
   if (M == 0 || N == 0) return;
   if (M > 64) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: M must be <= 64");
+  // natural weight layout: the LDS-staged decode kernel (gemm_decode.hip) when the shape fits
+  if (!psw && gai_gemm_dec2(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st)) return;
   const int KS = gai_gemm_splitk_ks(M, N, K);
   if (KS == 0) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: K must be a multiple of 512");
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;

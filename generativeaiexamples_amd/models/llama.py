@@ -232,10 +232,11 @@ class LlamaModel:
             self.w["norm_b"] = e(D)
         self.w["lm_head"] = self.w["embed"] if c.tie_embeddings else e(self.vocab_local, D)
 
-    # gate_up stays on the plain layout: at N = 28672 hipBLASLt streams it at 4.9 TB/s (47.6 us, B = 64)
-    # vs 62.7 us for the 448-workgroup fragment-stream kernel (1.75 workgroups per CU: the second
-    # round runs a quarter empty) - profiles/r1/decode_forward_kernel_stats_v3.csv
-    DECODE_PROJECTIONS = ("qkv", "o", "down", "proj")
+    # Only the down projection keeps a fragment-shuffled decode copy (+3.8 GB on Llama-3-8B): its
+    # split-K stream runs 38 vs 45 us at M = 64 from it. QKV / O gain < 1 us from a copy and the wide
+    # gate_up / LM head run on the LDS-staged decode kernel from the natural layout
+    # (profiles/r2/dec2_minwg_sweep.txt).
+    DECODE_PROJECTIONS = ("down",)
 
     def preshuffle_decode_weights(self) -> int:
         """Attach fragment-shuffled copies of the per-layer projection weights for the decode GEMM

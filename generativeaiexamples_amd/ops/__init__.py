@@ -329,18 +329,22 @@ def enable_tuned_blas() -> bool:
 
 
 class GemmTuner:
-    """GEMM backend policy, GAI_GEMM_POLICY = tune (default) | native | hipblaslt.
+    """GEMM backend policy, GAI_GEMM_POLICY = auto (default) | native | hipblaslt | tune.
 
-    native: every projection runs on the hand-written MFMA kernels (ring-pipelined 256x256 kernel for
-    prefill, weight-streaming split-K for decode) with their fused epilogues. tune: per-shape choice
-    between those and hipBLASLt + an elementwise epilogue kernel, decided by timing both on the first
-    call of each (M-bucket, N, K, epilogue) outside graph capture. hipblaslt: library GEMMs only.
-    Headline bench on MI355X (profiles/r2/bench_policy.json): native 13.38 q/s vs tune 14.86 q/s - the
-    ring kernel reaches 0.78-0.85x hipBLASLt at M = 16K and the M = 64 decode gate_up / lm_head still
-    trail it, so tune stays the default until they do."""
+    auto (deterministic, no run-time timing): every decode-sized GEMM (M <= 64) and every fp32-output
+    GEMM runs on the hand-written MFMA kernels - the LDS-staged decode kernel for the wide projections
+    (gate_up + fused SwiGLU, LM head), the weight-streaming split-K kernels for the narrow ones (QKV, O,
+    down) - so the decode graph holds no library GEMM at all; prefill-sized bf16 GEMMs (M > 64) are plain
+    library GEMMs on hipBLASLt (+ the framework's epilogue kernel), where the hand-written 256x256 ring
+    kernel measures 0.78-0.87x hipBLASLt at M = 16K (profiles/r2/gemm_ring.jsonl).
+    native: the hand-written kernels for every shape. hipblaslt: library GEMMs only. tune: per-shape
+    choice between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
+    Decode GEMMs at M = 64 vs hipBLASLt + epilogue kernel, weights streamed from HBM
+    (profiles/r2/dec2_minwg_sweep.txt): gate_up+SwiGLU 54.9 vs 64.1 us, LM head 233 vs 230 us,
+    QKV 24 vs 34 us, O 18 vs 31 us, down 38 vs 54 us."""
 
     def __init__(self):
-        self.mode = os.environ.get("GAI_GEMM_POLICY", "tune")
+        self.mode = os.environ.get("GAI_GEMM_POLICY", "auto")
         self.cache: dict = {}
         self.log: list = []
 
@@ -359,6 +363,8 @@ class GemmTuner:
     def pick(self, M, N, K, act, has_bias, out_dtype, x2, w) -> str:
         if self.mode == "native":
             return "native"
+        if self.mode == "auto":
+            return "native" if (M <= 64 or out_dtype == torch.float32) else "blas"
         if self.mode == "hipblaslt":
             return "blas"
         key = (self.bucket(M), N, K, act, has_bias, out_dtype)

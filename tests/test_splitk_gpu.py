@@ -90,7 +90,7 @@ def test_preshuffled_weights_match(cuda, M, act, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) * 0.02).bfloat16()
-    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if act == "bias" else None
+    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if act in ("bias", "gelu") else None
     r = torch.randn(M, N, device=cuda).bfloat16() if act == "residual" else None
     a = act if act == "swiglu" else None
     want = ops.linear(x, w, bias=b, residual=r, act=a).float()
@@ -121,3 +121,50 @@ def test_tuned_blas_table_loads_and_is_exact(cuda):
     y = torch.mm(x, w.t())
     ref_rows = (x[:64].float() @ w.float().t())
     assert (y[:64].float() - ref_rows).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("K", [4096, 14336])
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("psw", [False, True])
+def test_linear_add_rmsnorm_decode_tail(cuda, M, K, bias, psw):
+    """Decode tail residual += x.W^T (+ b); out = rmsnorm(residual) * g: natural layout (LDS-staged decode
+    GEMM + residual-add norm) and fragment-shuffled layout (split-K + fused reduce/norm) vs fp32 reference
+    with the same bf16 roundings."""
+    N = 4096
+    torch.manual_seed(M + K + bias)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if bias else None
+    res = torch.randn(M, N, device=cuda).bfloat16()
+    g = (1 + 0.1 * torch.randn(N, device=cuda)).bfloat16()
+    if psw:
+        assert ops.preshuffle_weight(w)
+    res_ref = res.clone()
+    h = ref.linear(x.cpu(), w.cpu(), None if b is None else b.cpu(), out_dtype=torch.float32).bfloat16()
+    r_ref = (h.float() + res_ref.cpu().float()).bfloat16()
+    o_ref = r_ref.float() * torch.rsqrt(r_ref.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.cpu().float()
+    out = ops.linear_add_rmsnorm(x, w, res, g, 1e-5, bias=b)
+    torch.testing.assert_close(res.float().cpu(), r_ref.float(), rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(out.float().cpu(), o_ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 16, 31, 64])
+@pytest.mark.parametrize("N,K,act", [(28672, 4096, "swiglu"), (32000, 4096, None), (16384, 14336, "residual"),
+                                     (18432, 4096, "bias"), (16384, 2048, "gelu")])
+def test_decode_gemm_natural_layout(cuda, M, N, K, act):
+    """The LDS-staged decode GEMM (gemm_decode.hip, wide projections) vs the fp32 reference: Llama-3-8B
+    gate_up+SwiGLU, a 32K-vocab LM head (fp32 logits), deep K + residual, bias, bias+GELU."""
+    torch.manual_seed(M * 3 + N)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if act in ("bias", "gelu") else None
+    r = torch.randn(M, N, device=cuda).bfloat16() if act == "residual" else None
+    epi = ops.EPI[act]
+    assert ops.native().gemm_dec2_ok(M, N, K, epi), "shape should take the LDS-staged decode kernel"
+    out_dtype = torch.float32 if act is None else torch.bfloat16
+    y = _run(x, w, b, r, epi, out_dtype)
+    want = ref.linear(x.cpu(), w.cpu(), None if b is None else b.cpu(), None if r is None else r.cpu(),
+                      act if act in ("swiglu", "gelu") else None, torch.float32)
+    tol = 2e-3 if out_dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float().cpu(), want, rtol=tol, atol=tol)
