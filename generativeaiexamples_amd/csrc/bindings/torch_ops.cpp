@@ -95,6 +95,33 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, 
                     (float)k_scale, (float)v_scale, cur_stream());
 }
 
+// Decode QKV projection fused with RoPE + KV write (split-K path). False: nothing launched, the caller
+// runs linear + rope_kv_write.
+bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias, const Tensor& pos,
+                  const Tensor& cos_sin, const Tensor& slots, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
+                  int64_t Hq, int64_t Hkv, int64_t D, double k_scale, double v_scale, Tensor& ws, bool psw) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_i32(pos, "positions");
+  check_f32(cos_sin, "cos_sin");
+  check_i32(slots, "slot_mapping");
+  check_bf16(q_out, "q_out");
+  TORCH_CHECK(A.dim() == 2 && A.is_contiguous() && B.is_contiguous(), "gemm_rope_kv: A [M, K] and B contiguous");
+  const int M = A.size(0), K = A.size(1);
+  TORCH_CHECK(B.size(0) == (Hq + 2 * Hkv) * D && B.size(1) == K, "gemm_rope_kv: weight shape mismatch");
+  TORCH_CHECK(pos.numel() >= M && slots.numel() >= M && q_out.size(0) >= M, "gemm_rope_kv: batch mismatch");
+  TORCH_CHECK(k_cache.size(-2) == 16 && k_cache.size(-1) == D && v_cache.size(-1) == 16, "bad kv cache layout");
+  const int N = B.size(0);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
+              "gemm_rope_kv: workspace too small");
+  if (bias) check_bf16(*bias, "bias");
+  const int f8 = kv_cache_fp8(k_cache, v_cache);
+  return gai_gemm_splitk_rope_kv(A.data_ptr(), B.data_ptr(), opt_ptr(bias), pos.data_ptr<int>(),
+                                 cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
+                                 k_cache.data_ptr(), v_cache.data_ptr(), M, Hq, Hkv, D, f8, (float)k_scale,
+                                 (float)v_scale, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream(), K) != 0;
+}
+
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
           int64_t epi, int64_t force) {
   check_bf16(A, "A");
@@ -538,6 +565,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8", &gemm_fp8);
   m.def("gemm_splitk", &gemm_splitk, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("R"), pybind11::arg("epi"), pybind11::arg("ws"), pybind11::arg("psw") = false);
+  m.def("gemm_rope_kv", &gemm_rope_kv);
   m.def("gemm_dec2_ok", [](int64_t M, int64_t N, int64_t K, int64_t epi) {
     return gai_gemm_dec2_ok((int)M, (int)N, (int)K, (int)epi) != 0;
   });

@@ -39,6 +39,13 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
 //                  workgroup in LDS, weights streamed through a register ring, epilogue fused; returns false
 //                  when the shape does not fit (caller falls back to gai_gemm_splitk's kernels))
 int gai_gemm_dec2_ok(int M, int N, int K, int epi);
+// gemm_splitk.hip fused decode QKV tail: split-K QKV projection, then ONE kernel sums the partials (+ bias),
+// applies RoPE and writes q / the paged K, V^T caches (as gai_rope_kv_write). Returns 0 (nothing launched)
+// when the shape does not take the split-K path; ws as gai_gemm_splitk.
+int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
+                            const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int Hq, int Hkv,
+                            int D, int kv_fp8, float k_scale, float v_scale, float* ws, int psw, hipStream_t st,
+                            int K);
 bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
                    int epi, int out_f32, hipStream_t st);
 

@@ -16,6 +16,7 @@
 #include "gai_common.h"
 #include "gai_epilogue.h"
 #include "gai_kernels.h"
+#include "gai_rope.h"
 
 using namespace gai;
 
@@ -551,6 +552,78 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
   GAI_FN(3)
   GAI_FN(4)
 #undef GAI_FN
+}
+
+namespace {
+
+// Fused decode QKV tail: sum the KS partial slabs of the QKV projection (+ bias), round to bf16 exactly as
+// the unfused GEMM output, then RoPE + q store + paged K / V^T cache write (gai_rope.h) - replaces the
+// split-K reduce launch, the bf16 qkv round trip and the rope_kv launch. Thread mapping as rope_kv_kernel.
+template <int D, typename KV>
+__global__ __launch_bounds__(256) void splitk_rope_kv_kernel(const float* __restrict__ part, int KS, int M, int N,
+                                                             const bf16* __restrict__ bias, const int* __restrict__ pos,
+                                                             const float* __restrict__ cos_sin,
+                                                             const int* __restrict__ slots, bf16* __restrict__ q_out,
+                                                             KV* __restrict__ k_cache, KV* __restrict__ v_cache, int Hq,
+                                                             int Hkv, float inv_ks, float inv_vs) {
+  constexpr int LPH = D / 8;
+  constexpr int HPB = 256 / LPH;
+  const int H = Hq + 2 * Hkv;
+  const long item = (long)blockIdx.x * HPB + threadIdx.x / LPH;
+  if (item >= (long)M * H) return;
+  const int t = (int)(item / H), h = (int)(item % H);
+  const int i0 = (threadIdx.x % LPH) * 4;
+  const int c1 = h * D + i0, c2 = c1 + D / 2;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < KS; ++k) {
+    const float* row = part + ((size_t)k * M + t) * N;
+    const float4 u = *reinterpret_cast<const float4*>(row + c1), v = *reinterpret_cast<const float4*>(row + c2);
+    a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;  // NOLINT
+    b[0] += v.x; b[1] += v.y; b[2] += v.z; b[3] += v.w;  // NOLINT
+  }
+  bf16x4 x1, x2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x1[j] = (bf16)(bias ? a[j] + (float)bias[c1 + j] : a[j]);
+    x2[j] = (bf16)(bias ? b[j] + (float)bias[c2 + j] : b[j]);
+  }
+  rope_kv_store<D>(x1, x2, t, h, i0, pos, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, 1, inv_ks, inv_vs);
+}
+
+}  // namespace
+
+int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
+                            const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int Hq, int Hkv,
+                            int D, int kv_fp8, float k_scale, float v_scale, float* ws, int psw, hipStream_t st,
+                            int K) {
+  const int N = (Hq + 2 * Hkv) * D;
+  if (M < 1 || M > 64 || (D != 64 && D != 128 && D != 256) || N % 16) return 0;
+  if (!psw && gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) return 0;  // single-pass kernel owns it
+  const int KS = gai_gemm_splitk_ks(M, N, K);
+  if (KS <= 1) return 0;
+  launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  const long items = (long)M * (Hq + 2 * Hkv);
+  const float iks = 1.f / k_scale, ivs = 1.f / v_scale;
+#define GAI_SRK(DD)                                                                                               \
+  if (D == DD) {                                                                                                  \
+    constexpr int HPB = 256 / (DD / 8);                                                                           \
+    const unsigned grid = (unsigned)((items + HPB - 1) / HPB);                                                    \
+    if (kv_fp8)                                                                                                   \
+      splitk_rope_kv_kernel<DD, fp8><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin, slots,  \
+                                                           (bf16*)q_out, (fp8*)k_cache, (fp8*)v_cache, Hq, Hkv,     \
+                                                           iks, ivs);                                              \
+    else                                                                                                          \
+      splitk_rope_kv_kernel<DD, bf16><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin, slots, \
+                                                            (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv,  \
+                                                            iks, ivs);                                             \
+    GAI_LAUNCH_CHECK();                                                                                           \
+    return 1;                                                                                                     \
+  }
+  GAI_SRK(64)
+  GAI_SRK(128)
+  GAI_SRK(256)
+#undef GAI_SRK
+  return 0;
 }
 
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,

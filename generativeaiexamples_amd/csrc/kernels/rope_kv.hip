@@ -13,12 +13,11 @@
 // cache option, half the bytes per token for decode attention.
 #include "gai_common.h"
 #include "gai_kernels.h"
+#include "gai_rope.h"
 
 using namespace gai;
 
 namespace {
-
-constexpr int kBS = 16;  // KV block size (tokens per page)
 
 template <int D, typename KV>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restrict__ pos,
@@ -32,63 +31,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   const long item = (long)blockIdx.x * HPB + threadIdx.x / LPH;  // (token, head)
   if (item >= (long)T * H) return;
   const int t = (int)(item / H), h = (int)(item % H);
-  const int l = threadIdx.x % LPH;
-  const int i0 = l * 4;  // pair indices i0..i0+3 and i0+D/2..
+  const int i0 = (threadIdx.x % LPH) * 4;  // pair indices i0..i0+3 and i0+D/2..
   const bf16* src = qkv + ((size_t)t * H + h) * D;
-  bf16x4 x1 = *reinterpret_cast<const bf16x4*>(src + i0);
-  bf16x4 x2 = *reinterpret_cast<const bf16x4*>(src + i0 + D / 2);
-  const bool is_v = h >= Hq + Hkv;
-  if (rope && !is_v) {
-    const int p = pos[t];
-    const float4 c = *reinterpret_cast<const float4*>(cos_sin + (size_t)p * D + i0);
-    const float4 s = *reinterpret_cast<const float4*>(cos_sin + (size_t)p * D + D / 2 + i0);
-    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float a = (float)x1[j], b = (float)x2[j];
-      x1[j] = (bf16)(a * cc[j] - b * ss[j]);
-      x2[j] = (bf16)(b * cc[j] + a * ss[j]);
-    }
-  }
-  if (h < Hq) {
-    bf16* dst = q_out + ((size_t)t * Hq + h) * D;
-    *reinterpret_cast<bf16x4*>(dst + i0) = x1;
-    *reinterpret_cast<bf16x4*>(dst + i0 + D / 2) = x2;
-    return;
-  }
-  const int slot = slots[t];
-  if (slot < 0) return;
-  const int blk = slot / kBS, off = slot % kBS;
-  constexpr bool F8 = sizeof(KV) == 1;
-  if (!is_v) {
-    const int g = h - Hq;
-    KV* dst = k_cache + (((size_t)blk * Hkv + g) * kBS + off) * D;
-    if constexpr (F8) {
-      *reinterpret_cast<uint32_t*>(dst + i0) = f32x4_to_fp8(x1[0], x1[1], x1[2], x1[3], inv_ks);
-      *reinterpret_cast<uint32_t*>(dst + i0 + D / 2) = f32x4_to_fp8(x2[0], x2[1], x2[2], x2[3], inv_ks);
-    } else {
-      *reinterpret_cast<bf16x4*>(dst + i0) = x1;
-      *reinterpret_cast<bf16x4*>(dst + i0 + D / 2) = x2;
-    }
-  } else {
-    const int g = h - Hq - Hkv;
-    KV* dst = v_cache + ((size_t)blk * Hkv + g) * D * kBS + off;
-    if constexpr (F8) {
-      const uint32_t lo = f32x4_to_fp8(x1[0], x1[1], x1[2], x1[3], inv_vs);
-      const uint32_t hi = f32x4_to_fp8(x2[0], x2[1], x2[2], x2[3], inv_vs);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dst[(size_t)(i0 + j) * kBS] = (KV)(lo >> (8 * j));
-        dst[(size_t)(i0 + D / 2 + j) * kBS] = (KV)(hi >> (8 * j));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dst[(size_t)(i0 + j) * kBS] = x1[j];
-        dst[(size_t)(i0 + D / 2 + j) * kBS] = x2[j];
-      }
-    }
-  }
+  const bf16x4 x1 = *reinterpret_cast<const bf16x4*>(src + i0);
+  const bf16x4 x2 = *reinterpret_cast<const bf16x4*>(src + i0 + D / 2);
+  rope_kv_store<D>(x1, x2, t, h, i0, pos, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, rope, inv_ks, inv_vs);
 }
 
 }  // namespace

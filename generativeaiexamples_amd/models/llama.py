@@ -497,6 +497,8 @@ class LlamaModel:
         fuse = (res.is_cuda and ctx.tp_size == 1 and c.norm != "layernorm" and not self.lora_names and T <= 64
                 and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         xn = None
+        fuse_qkv = (res.is_cuda and T <= 64 and not self.lora_names and not c.qk_norm
+                    and os.environ.get("GAI_FUSE_ROPE", "1") == "1")
         # TP: the all-reduce of each row-parallel projection carries the residual add and the next RMSNorm
         tp_norm = (ctx.tp_size > 1 and c.norm != "layernorm" and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         for i in range(c.num_layers):
@@ -505,12 +507,17 @@ class LlamaModel:
                 x, xn = xn, None
             else:
                 x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
-            qkv = self._lora(ops.linear(x, w[p + "qkv"], bias=w.get(p + "qkv_b")), x, i, "qkv", fb)
-            if c.qk_norm:
-                self._qk_norm(qkv, p)
             kc, vc = kv.layer(i)
             ks, vs = kv.scales(i)
-            ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True, ks, vs)
+            if fuse_qkv:  # decode: QKV split-K partials -> RoPE -> q / paged KV in one kernel
+                ops.linear_rope_kv(x, w[p + "qkv"], w.get(p + "qkv_b"), fb.positions, self.cos_sin, fb.slots, q, kc,
+                                   vc, self.hq, self.hkv, hd, ks, vs)
+            else:
+                qkv = self._lora(ops.linear(x, w[p + "qkv"], bias=w.get(p + "qkv_b")), x, i, "qkv", fb)
+                if c.qk_norm:
+                    self._qk_norm(qkv, p)
+                ops.rope_kv_write(qkv, fb.positions, self.cos_sin, fb.slots, q, kc, vc, self.hq, self.hkv, hd, True,
+                                  ks, vs)
             if P > 0:
                 ops.attention_prefill(q[:P], kc, vc, fb.prefill_block_tables, fb.cu_q, fb.prefill_ctx, self.scale,
                                       True, tiles=fb.prefill_tiles, q_lens=fb.prefill_qlen, out=attn[:P], k_scale=ks,

@@ -163,6 +163,25 @@ def linear_add_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
     return rms_norm(linear(x, w, bias), norm_w, eps, residual=residual)
 
 
+def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], positions, cos_sin, slots, q_out,
+                   k_cache, v_cache, Hq: int, Hkv: int, D: int, k_scale=1.0, v_scale=1.0) -> None:
+    """QKV projection + RoPE + paged KV write. For decode-sized M the split-K QKV partials are summed,
+    rotated and scattered into q_out / the K, V^T caches by ONE kernel (no reduce launch, no bf16 qkv
+    round trip, no rope_kv launch); otherwise ``linear`` + ``rope_kv_write``. Same bf16 roundings."""
+    K = x.shape[-1]
+    M = x.numel() // K
+    if (x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and 1 <= M <= 64
+            and TUNER.mode != "hipblaslt"):
+        nat = native()
+        psw = getattr(w, "_gai_psw", None)
+        ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x.device)
+        if nat.gemm_rope_kv(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, positions, cos_sin, slots,
+                            q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None):
+            return
+    qkv = linear(x, w, bias=bias)
+    rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, True, k_scale, v_scale)
+
+
 def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
     """[N, K] -> the same [N, K]-shaped storage in MFMA B-fragment order [N/16][K/32][64 lanes][8]:
     lane l of fragment (nt, kt) holds w[16 nt + (l & 15), 32 kt + 8 (l >> 4) : +8]. A decode GEMM wave

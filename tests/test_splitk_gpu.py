@@ -168,3 +168,48 @@ def test_decode_gemm_natural_layout(cuda, M, N, K, act):
                       act if act in ("swiglu", "gelu") else None, torch.float32)
     tol = 2e-3 if out_dtype == torch.float32 else 2e-2
     torch.testing.assert_close(y.float().cpu(), want, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("kv_fp8", [False, True])
+@pytest.mark.parametrize("psw", [False, True])
+def test_linear_rope_kv_fused_matches_unfused(cuda, M, bias, kv_fp8, psw):
+    """Decode QKV tail fused into the split-K reduce (partials -> bias -> bf16 -> RoPE -> q / paged K, V^T)
+    matches linear + rope_kv_write to the last bit on all but a handful of elements, bf16 and fp8 caches."""
+    Hq, Hkv, D, K = 32, 8, 128, 4096
+    N = (Hq + 2 * Hkv) * D
+    torch.manual_seed(M * 5 + bias + 2 * kv_fp8)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = (torch.randn(N, device=cuda) * 0.1).bfloat16() if bias else None
+    if psw:
+        assert ops.preshuffle_weight(w)
+    cs = ops.rope_cos_sin(4096, D, 500000.0, device=cuda)
+    pos = torch.randint(0, 4000, (M,), device=cuda, dtype=torch.int32)
+    nblk = 64
+    slots = torch.randperm(nblk * 16, device=cuda)[:M].to(torch.int32)
+    slots[0] = -1  # a padded row: no cache write
+    kvd = torch.float8_e4m3fn if kv_fp8 else torch.bfloat16
+    ks, vs = (0.05, 0.04) if kv_fp8 else (1.0, 1.0)
+    outs = []
+    for fused in (True, False):
+        q = torch.zeros(M, Hq, D, device=cuda, dtype=torch.bfloat16)
+        kc = torch.zeros(nblk, Hkv, 16, D, device=cuda, dtype=kvd)
+        vc = torch.zeros(nblk, Hkv, D, 16, device=cuda, dtype=kvd)
+        if fused:
+            ops.linear_rope_kv(x, w, b, pos, cs, slots, q, kc, vc, Hq, Hkv, D, ks, vs)
+        else:
+            qkv = ops.linear(x, w, bias=b)
+            ops.rope_kv_write(qkv, pos, cs, slots, q, kc, vc, Hq, Hkv, D, True, ks, vs)
+        outs.append((q, kc.view(torch.uint8) if kv_fp8 else kc, vc.view(torch.uint8) if kv_fp8 else vc))
+    # same partials, summation order and roundings; hipcc may contract the rotation's mul-sub into an FMA
+    # differently at the two call sites, so a value that cancels to ~0 can differ in its last bit
+    for a, r in zip(outs[0], outs[1]):
+        if a.dtype == torch.uint8:  # fp8 codes: at most a handful one code apart
+            assert (a != r).sum().item() <= max(2, a.numel() // 10000)
+        else:
+            torch.testing.assert_close(a.float(), r.float(), rtol=1e-2, atol=1e-5)
+            assert (a != r).sum().item() <= max(2, a.numel() // 10000)
+    if M > 1:  # row 0 is padded (no cache write)
+        assert outs[0][1].float().abs().sum() > 0  # the cache was written
