@@ -293,8 +293,7 @@ class LLMEngine:
                 b.decode_block_tables, np.asarray(rows, dtype=np.int32)]
         if P > 0:
             rpt = ops.prefill_rows_per_tile(self.model.hq, self.model.hkv)
-            arrs.append(np.asarray([(i, s) for i, n in enumerate(b.prefill_qlen) for s in range(0, n, rpt)],
-                                   dtype=np.int32).reshape(-1, 2))
+            arrs.append(ops.prefill_tile_list(b.prefill_qlen, rpt, b.prefill_ctx))
         plan = dict(op="eager", P=int(P), arr=arrs, qlen=[int(x) for x in b.prefill_qlen],
                     pctx=[int(x) for x in b.prefill_ctx], max_dctx=int(b.decode_ctx.max()) if nd else 0,
                     seq_ids=[int(x) for x in b.prefill_seq_ids] + [int(x) for x in b.decode_seq_ids],

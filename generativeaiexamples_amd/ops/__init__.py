@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import reference as ref
@@ -445,11 +446,23 @@ def prefill_rows_per_tile(Hq: int, Hkv: int) -> int:
     return 32 * (4 // hpw)
 
 
-def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device) -> torch.Tensor:
-    """Host-side varlen tile list [(seq, q_start), ...] for attention_prefill."""
-    rows = prefill_rows_per_tile(Hq, Hkv)
+def prefill_tile_list(q_lens: Sequence[int], rows: int, ctx_lens: Sequence[int] | None = None) -> np.ndarray:
+    """Varlen tile list [(seq, q_start), ...] for attention_prefill, longest first: a causal tile's work
+    grows with its last query position (ctx - qlen + q_start + rows keys), and workgroups are dispatched
+    roughly in tile order, so issuing the long tiles first keeps them off the tail of the grid
+    (longest-processing-time-first scheduling)."""
     t = [(b, s) for b, n in enumerate(q_lens) for s in range(0, n, rows)]
-    return torch.tensor(t, dtype=torch.int32).reshape(-1).to(device, non_blocking=True)
+    if ctx_lens is None:
+        ctx_lens = q_lens
+    t.sort(key=lambda bs: -(int(ctx_lens[bs[0]]) - int(q_lens[bs[0]]) + bs[1]))
+    return np.asarray(t, dtype=np.int32).reshape(-1, 2)
+
+
+def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device,
+                        ctx_lens: Sequence[int] | None = None) -> torch.Tensor:
+    """Host-side varlen tile list [(seq, q_start), ...] for attention_prefill (longest tile first)."""
+    t = prefill_tile_list(q_lens, prefill_rows_per_tile(Hq, Hkv), ctx_lens)
+    return torch.from_numpy(t).reshape(-1).to(device, non_blocking=True)
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, causal=True, tiles=None,
