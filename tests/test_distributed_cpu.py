@@ -39,9 +39,9 @@ def test_expert_parallel_all_to_all(tmp_path):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_ep_padded_dispatch(tmp_path, world):
-    """Fixed-capacity, sync-free EP exchange (the graph-capturable decode path) at 2 and 4 ranks."""
+    """Fixed-capacity, sync-free EP exchange (the graph-capturable decode path) at 2, 4 and 8 ranks."""
     mp.spawn(W.ep_padded_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         d = torch.load(tmp_path / f"ep_padded_{r}.pt", weights_only=True)
