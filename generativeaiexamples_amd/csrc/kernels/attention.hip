@@ -186,32 +186,28 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
     const float m_new = fmaxf(m_run, mt);
     const float alpha = fexp2(m_run - m_new);
-    float rs = 0.f;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(fmaf(s[sub][r], sl2, -m_new));
-        s[sub][r] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
     // lazy rescale: once the running maxima settle (most tiles after the first few) alpha == 1 in
     // every lane and the D/32 x 16 accumulator multiplies are skipped (bit-identical result)
     if (__any(alpha != 1.f)) {
 #pragma unroll
       for (int i = 0; i < D / 32; ++i) acc_o[i] *= alpha;
     }
+    m_run = m_new;
 
-    // O^T[d][q] += V^T[d][key] . P^T[key][q]
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]. The 8 probabilities of each 8-key step are exponentiated
+    // right before that step's MFMAs, so step st's MFMAs run in the matrix pipe while step st+1's
+    // v_exp / cvt issue (the row sum is only needed after the tile).
+    float rs = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int sub = st >> 1, sp = st & 1;
       bf16x8 pf;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pf[j] = (bf16)s[sub][8 * sp + j];
+      for (int j = 0; j < 8; ++j) {
+        const float p = fexp2(fmaf(s[sub][8 * sp + j], sl2, -m_new));
+        rs += p;
+        pf[j] = (bf16)p;
+      }
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
         const int d = 32 * dt + (lane & 31);
@@ -222,6 +218,8 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[dt], 0, 0, 0);
       }
     }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
     if (kt + 1 < ntiles) write_tile(cur ^ 1);
     __syncthreads();
   }

@@ -272,6 +272,40 @@ __global__ __launch_bounds__(256, 2) void gemm_dec_kernel(const bf16* __restrict
   }
 }
 
+// Sum the KS fp32 partial slabs (stride floats apart) of W consecutive values at p, slab 0 first (the
+// same order as a plain loop, so every reduce path rounds identically). A runtime-trip loop waits for
+// each slab's load before issuing the next; here 4 slabs are in flight at a time.
+template <int W>
+__device__ __forceinline__ void sum_slabs(const float* p, size_t stride, int KS, float (&v)[W]) {
+  static_assert(W == 1 || W % 4 == 0, "W: 1 or a multiple of 4");
+  int k = 0;
+  for (; k + 4 <= KS; k += 4) {
+    float x[4][W];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* q = p + (size_t)(k + u) * stride;
+      if constexpr (W == 1) {
+        x[u][0] = q[0];
+      } else {
+#pragma unroll
+        for (int c = 0; c < W; c += 4) {
+          const float4 t = *reinterpret_cast<const float4*>(q + c);
+          x[u][c] = t.x; x[u][c + 1] = t.y; x[u][c + 2] = t.z; x[u][c + 3] = t.w;  // NOLINT
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < W; ++c) v[c] += x[u][c];
+  }
+  for (; k < KS; ++k) {
+    const float* q = p + (size_t)k * stride;
+#pragma unroll
+    for (int c = 0; c < W; ++c) v[c] += q[c];
+  }
+}
+
 // Sum the KS partial slabs and apply the epilogue. One thread per output element.
 template <int EPI, bool OUTF32>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int KS, int M, int N,
@@ -282,17 +316,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int m = (int)(e / ncol), j = (int)(e % ncol);
   if (EPI == EPI_SWIGLU) {
     const int g = (j >> 4) * 32 + (j & 15);  // interleaved per 16: [gate16 | up16]
-    float vg = 0.f, vu = 0.f;
-    for (int s = 0; s < KS; ++s) {
-      const float* p = part + ((size_t)s * M + m) * N;
-      vg += p[g];
-      vu += p[g + 16];
-    }
-    store_out<EPI_NONE, OUTF32>(C, nullptr, nullptr, ldc, m, j, silu(vg) * vu);
+    float vg[1] = {0.f}, vu[1] = {0.f};
+    sum_slabs<1>(part + (size_t)m * N + g, (size_t)M * N, KS, vg);
+    sum_slabs<1>(part + (size_t)m * N + g + 16, (size_t)M * N, KS, vu);
+    store_out<EPI_NONE, OUTF32>(C, nullptr, nullptr, ldc, m, j, silu(vg[0]) * vu[0]);
   } else {
-    float v = 0.f;
-    for (int s = 0; s < KS; ++s) v += part[((size_t)s * M + m) * N + j];
-    store_out<EPI, OUTF32>(C, bias, R, ldc, m, j, v);
+    float v[1] = {0.f};
+    sum_slabs<1>(part + (size_t)m * N + j, (size_t)M * N, KS, v);
+    store_out<EPI, OUTF32>(C, bias, R, ldc, m, j, v[0]);
   }
 }
 
@@ -324,13 +355,14 @@ int legacy_ks(int M, int N, int K) {
   const int kl_max = (128 * 1024) / (16 * MB * 2);  // LDS bytes / row bytes
   const int units = K / kKAlign;
   const int tiles = (N + 16 * splitk_wpg() - 1) / (16 * splitk_wpg());
+  static const int min_wg = getenv("GAI_SPLITK_LEGACY_MINWG") ? atoi(getenv("GAI_SPLITK_LEGACY_MINWG")) : 512;
   int best = units;  // KS = units / d for a divisor d of units
   for (int d = units; d >= 1; --d) {
     if (units % d) continue;
     const int KS = units / d, KL = d * kKAlign;
     if (KL > kl_max) continue;
     best = KS;
-    if ((long)tiles * KS >= 512) break;  // largest slice that still fills the chip
+    if ((long)tiles * KS >= min_wg) break;  // largest slice that still fills the chip
   }
   return best;
 }
@@ -481,12 +513,7 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(const float* __
       gg[c] = load8(g + idx);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
-      for (int k = 0; k < KS; ++k) {
-        const float4* p = reinterpret_cast<const float4*>(part + ((size_t)k * M + m) * N + idx);
-        const float4 a = p[0], b = p[1];
-        v[c][0] += a.x; v[c][1] += a.y; v[c][2] += a.z; v[c][3] += a.w;  // NOLINT
-        v[c][4] += b.x; v[c][5] += b.y; v[c][6] += b.z; v[c][7] += b.w;  // NOLINT
-      }
+      sum_slabs<8>(part + (size_t)m * N + idx, (size_t)M * N, KS, v[c]);
     }
   }
   float ss = 0.f;
@@ -575,12 +602,8 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(const float* __rest
   const int i0 = (threadIdx.x % LPH) * 4;
   const int c1 = h * D + i0, c2 = c1 + D / 2;
   float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < KS; ++k) {
-    const float* row = part + ((size_t)k * M + t) * N;
-    const float4 u = *reinterpret_cast<const float4*>(row + c1), v = *reinterpret_cast<const float4*>(row + c2);
-    a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;  // NOLINT
-    b[0] += v.x; b[1] += v.y; b[2] += v.z; b[3] += v.w;  // NOLINT
-  }
+  sum_slabs<4>(part + (size_t)t * N + c1, (size_t)M * N, KS, a);
+  sum_slabs<4>(part + (size_t)t * N + c2, (size_t)M * N, KS, b);
   bf16x4 x1, x2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
