@@ -499,6 +499,9 @@ class LlamaModel:
         xn = None
         fuse_qkv = (res.is_cuda and T <= 64 and not self.lora_names and not c.qk_norm
                     and os.environ.get("GAI_FUSE_ROPE", "1") == "1")
+        # TP prefill: row-parallel projections pipelined with their all-reduce (DistContext.tp_linear_all_reduce)
+        overlap = (ctx.tp_size > 1 and not self.lora_names and os.environ.get("GAI_TP_OVERLAP", "1") == "1"
+                   and T >= 2 * int(os.environ.get("GAI_TP_OVERLAP_CHUNK_ROWS", "1024")))
         # TP: the all-reduce of each row-parallel projection carries the residual add and the next RMSNorm
         tp_norm = (ctx.tp_size > 1 and c.norm != "layernorm" and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         for i in range(c.num_layers):
@@ -528,6 +531,9 @@ class LlamaModel:
             a2 = attn.view(T, -1)
             if fuse:
                 x = ops.linear_add_rmsnorm(a2, w[p + "o"], res, w[p + "mlp_norm"], c.rms_eps, bias=w.get(p + "o_b"))
+            elif overlap:  # TP prefill: each row chunk's all-reduce overlaps the next chunk's GEMM
+                h = ctx.tp_linear_all_reduce(a2, w[p + "o"], self._row_bias(p + "o_b"))
+                x = self._norm(h, p + "mlp_norm", residual=res)
             else:
                 h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
                 if tp_norm:  # all-reduce + residual add + RMSNorm in one peer-memory kernel
@@ -544,6 +550,8 @@ class LlamaModel:
                 nxt = "norm" if last else f"l{i + 1}.attn_norm"
                 xn = ops.linear_add_rmsnorm(g, w[p + "down"], res, w[nxt], c.rms_eps, bias=w.get(p + "down_b"))
                 h = None
+            elif overlap:
+                h = ctx.tp_linear_all_reduce(g, w[p + "down"], self._row_bias(p + "down_b"))
             else:
                 h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
                 if tp_norm and not (last and fb.sample_rows is not None):

@@ -133,8 +133,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x2.device)
         nat.gemm_splitk(x2, psw, out, bias, residual, epi, ws, True)
         return out
-    if residual is None and out is None and TUNER.pick(M, N, K, act, bias is not None, out_dtype, x2, w) == "blas":
-        return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
+    if residual is None and TUNER.pick(M, N, K, act, bias is not None, out_dtype, x2, w) == "blas":
+        if out is None:
+            return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
+        if act is None and out_dtype == x.dtype and out.is_contiguous():  # library GEMM straight into `out`
+            o2 = out.view(M, N)
+            torch.addmm(bias, x2, w.t(), out=o2) if bias is not None else torch.mm(x2, w.t(), out=o2)
+            return out
     if out is None:
         out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
     _native_gemm(x2, w, out, bias, residual, epi)

@@ -3,8 +3,8 @@
 MI355X topology: 8 GPUs, fully connected by xGMI, 7 point-to-point links of
 ~153 GB/s per GPU. One process per GPU; ``torch.distributed`` with backend ``nccl`` is RCCL on
 ROCm. Sub-groups: ``tp`` (generator tensor parallel), ``dp`` (embedder / index shards) and ``ep``
-(MoE experts). Collectives are issued on the current stream; the engine places them on a
-separate high-priority stream when it overlaps communication with compute.
+(MoE experts). The TP group's RCCL collectives run on a high-priority stream; prefill row-parallel
+projections overlap their all-reduce with the next row chunk's GEMM (``tp_linear_all_reduce``).
 
 On the CPU test tier the same code runs over ``gloo`` (world_size 2, 127.0.0.1 rendezvous).
 """
@@ -68,6 +68,37 @@ class DistContext:
                     dist.all_reduce(f, group=self.tp_group)
                     t.copy_(f)
         return t
+
+    def tp_linear_all_reduce(self, x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                             chunks: Optional[int] = None) -> torch.Tensor:
+        """Row-parallel projection ``x @ w^T (+ bias)`` followed by its TP all-reduce, pipelined over row
+        chunks for prefill-sized inputs: chunk i's all-reduce is issued asynchronously (RCCL runs it on
+        its own high-priority stream, see ``init_distributed``) as soon as chunk i's GEMM is enqueued, so
+        it overlaps chunk i+1's GEMM on the compute stream; the compute stream waits for every chunk's
+        all-reduce before the result is used. Decode-sized inputs (and TP = 1) take the plain path.
+        Same math as ``linear`` + ``tp_all_reduce`` (rows are independent)."""
+        from .. import ops
+
+        M = x.shape[0]
+        if chunks is None:
+            chunks = min(4, M // int(os.environ.get("GAI_TP_OVERLAP_CHUNK_ROWS", "1024")))
+        if self.tp_size == 1 or chunks <= 1:
+            return self.tp_all_reduce(ops.linear(x, w, bias=bias))
+        out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+        step = -(-M // chunks)
+        asynchronous = x.is_cuda or x.dtype in (torch.float32, torch.float64)
+        works = []
+        with guard("tp_linear_all_reduce", self.rank):
+            for a in range(0, M, step):
+                part = out[a:a + step]
+                ops.linear(x[a:a + step], w, bias=bias, out=part)
+                if asynchronous:
+                    works.append(dist.all_reduce(part, group=self.tp_group, async_op=True))
+                else:  # gloo with reduced precision (CPU test tier): synchronous fp32 reduce per chunk
+                    self.tp_all_reduce(part)
+            for wk in works:
+                wk.wait()
+        return out
 
     def tp_all_reduce_rmsnorm(self, h: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float
                               ) -> torch.Tensor:
@@ -201,9 +232,19 @@ def init_distributed(tp_size: int = 1, backend: str | None = None, timeout_s: in
         ctx.tp_size, ctx.dp_size = tp_size, world // tp_size
         ctx.world_group = dist.group.WORLD
         # every rank must create every group in the same order
+        # RCCL runs the TP group's collectives on a high-priority stream, so an all-reduce issued
+        # asynchronously beside a GEMM (tp_linear_all_reduce) is scheduled ahead of the compute kernels
+        tp_opts = None
+        if backend == "nccl":
+            try:
+                tp_opts = dist.ProcessGroupNCCL.Options()
+                tp_opts.is_high_priority_stream = True
+            except (AttributeError, RuntimeError):
+                tp_opts = None
         for d in range(ctx.dp_size):
             ranks = list(range(d * tp_size, (d + 1) * tp_size))
-            g = dist.new_group(ranks) if tp_size > 1 else None
+            g = (dist.new_group(ranks, pg_options=tp_opts) if tp_opts is not None else dist.new_group(ranks)) \
+                if tp_size > 1 else None
             if rank in ranks:
                 ctx.tp_group = g
         for t in range(tp_size):

@@ -13,7 +13,9 @@ def _init(rank, world, port, tp):
     return gdist.init_distributed(tp_size=tp, backend="gloo")
 
 
-def tp_llama_worker(rank, world, port, out_dir):
+def tp_llama_worker(rank, world, port, out_dir, overlap_rows=None):
+    if overlap_rows:  # exercise the row-chunked overlapped all-reduce path on these short prompts
+        os.environ["GAI_TP_OVERLAP_CHUNK_ROWS"] = str(overlap_rows)
     ctx = _init(rank, world, port, world)
     from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
@@ -635,5 +637,25 @@ def full_sft_worker(rank, world, tp, port, out_dir):
     err = max(float((m.w[k].detach() - mine.w[k]).abs().max()) for k in m.w)
     with open(os.path.join(out_dir, f"full_sft_{rank}.json"), "w") as f:
         json.dump({"loss": hist, "ref_loss": ref_hist, "max_err": err}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def tp_linear_overlap_worker(rank, world, port, out_dir):
+    """tp_linear_all_reduce (row-chunked GEMM + async all-reduce) == linear + all-reduce, and the TP Llama
+    prefill with the overlapped path == the plain TP path."""
+    ctx = _init(rank, world, port, world)
+    from generativeaiexamples_amd import ops
+
+    g = torch.Generator().manual_seed(1)
+    res = {}
+    for dt in (torch.float32, torch.bfloat16):
+        x = torch.randn(300, 64, generator=g).to(dt)  # this rank's K-shard of the activations
+        w = torch.randn(48, 64, generator=g).to(dt)
+        b = torch.randn(48, generator=g).to(dt) if rank == 0 else None
+        got = ctx.tp_linear_all_reduce(x + rank, w * (rank + 1), b, chunks=3)
+        want = ctx.tp_all_reduce(ops.linear(x + rank, w * (rank + 1), bias=b))
+        res[str(dt)] = (got.float() - want.float()).abs().max().item()
+    torch.save(res, os.path.join(out_dir, f"ovl_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

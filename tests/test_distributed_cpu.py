@@ -22,8 +22,11 @@ def _port():
 
 
 @pytest.mark.timeout(300)
-def test_tp2_llama_matches_tp1(tmp_path):
-    mp.spawn(W.tp_llama_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("overlap_rows", [None, 8])
+def test_tp2_llama_matches_tp1(tmp_path, overlap_rows):
+    """TP=2 logits == TP=1; with overlap_rows the O / down projections take the row-chunked GEMM +
+    asynchronous all-reduce path of TP prefill (chunks of 8 rows on these short prompts)."""
+    mp.spawn(W.tp_llama_worker, args=(2, _port(), str(tmp_path), overlap_rows), nprocs=2, join=True)
     for r in range(2):
         d = torch.load(tmp_path / f"tp_{r}.pt", weights_only=True)
         err = (d["tp"] - d["ref"]).abs().max().item()
@@ -97,3 +100,14 @@ def test_tp_serving_hub(tmp_path, world):
     d = json.loads((tmp_path / "tp_serving.json").read_text())
     assert d["api"] == d["ref"], (d["api"], d["ref"])
     assert d["after_abort"] == d["ref"][1]
+
+
+@pytest.mark.timeout(300)
+def test_tp_linear_all_reduce_overlap(tmp_path):
+    """Row-chunked row-parallel GEMM with asynchronous per-chunk all-reduces (the TP prefill overlap path)
+    matches the plain GEMM + all-reduce, fp32 and bf16, 2 ranks."""
+    mp.spawn(W.tp_linear_overlap_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"ovl_{r}.pt", weights_only=True)
+        assert d["torch.float32"] < 1e-4
+        assert d["torch.bfloat16"] < 1e-2
