@@ -56,8 +56,14 @@ __device__ __forceinline__ int k_lds_off(int key, int u) {
   constexpr int MASK = KU >= 16 ? 15 : KU - 1;
   return key * D * 2 + ((u ^ (key & MASK)) << 4);
 }
-// V^T image: row = d (64 keys = 128 B), 8-B unit u (0..15) stored at u ^ ((d >> 1) & 15)
-__device__ __forceinline__ int v_lds_off(int d, int u) { return d * 128 + ((u ^ ((d >> 1) & 15)) << 3); }
+// V^T image: row = d (64 keys = 128 B) of 8-B units u (4 keys each). Unit u = 4st + 2b1 + b0 is stored at
+// position 4st + 2b0 + b1, so the two units one P.V MFMA operand takes (u = 4st + h and 4st + 2 + h) are
+// one aligned 16-B pair read by a single ds_read_b128 (no register shuffles); 16-B pairs are XOR-swizzled
+// by (d >> 1) & 7, conflict-free for the read lane groups.
+__device__ __forceinline__ int v_lds_off(int d, int u) {
+  const int p = (u & ~3) | ((u & 1) << 1) | ((u >> 1) & 1);
+  return d * 128 + (((p >> 1) ^ ((d >> 1) & 7)) << 4) + ((p & 1) << 3);
+}
 
 __device__ __forceinline__ bf16x8 kv_to_bf16(bf16x8 v, float) { return v; }
 __device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to_bf16(v, s); }
@@ -210,11 +216,8 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
       }
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
-        const int d = 32 * dt + (lane & 31);
-        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(sv + v_lds_off(d, 4 * st + h));
-        const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(sv + v_lds_off(d, 4 * st + 2 + h));
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        // units 4st + h (lo) and 4st + 2 + h (hi) of row d: one 16-B pair in the image
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off(32 * dt + (lane & 31), 4 * st + h));
         acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[dt], 0, 0, 0);
       }
     }
