@@ -5,8 +5,8 @@
 //
 // attn_prefill: varlen, causal or bidirectional, GQA. Workgroup = 4 waves; each
 // wave owns 32 query rows of one q-head, the workgroup shares 64-key K / V^T tiles
-// in LDS (register-staged, issue-early / write-late, one barrier per tile, XOR
-// swizzled images). S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts a full query row
+// in LDS (register-staged, issue-early / write-late, one barrier per tile, row-padded
+// images). S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts a full query row
 // in one lane (swapped QK^T), so the online softmax is in-register; P^T is fed to
 // the P.V MFMA straight from the S accumulator (k-order permuted on the V side,
 // cdna_hip_programming §3 "accumulator tile as the next MFMA's operand"). exp2
@@ -39,30 +39,34 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 // ----------------------------------------------------------------------------------------------
 // Prefill
 // ----------------------------------------------------------------------------------------------
+// LDS images are padded by 16 B per row instead of XOR-swizzled: the 16 rows one ds_read_b128 lane group
+// reads at the same column then fall on 16 distinct 4-bank slots (row strides of 4 mod 64 or 36 mod 64
+// banks), and every fragment address is one per-lane base plus a compile-time offset (no per-read
+// address VALU in the loop).
 template <int D>
 struct PrefillCfg {
   static constexpr int KT = 64;                  // keys per tile
-  static constexpr int KBYTES = KT * D * 2;      // K tile image
-  static constexpr int VBYTES = D * KT * 2;      // V^T tile image
+  static constexpr int KRS = D * 2 + 16;         // K image row stride (bytes)
+  static constexpr int VRS = KT * 2 + 16;        // V^T image row stride (bytes)
+  static constexpr int KBYTES = KT * KRS;        // K tile image
+  static constexpr int VBYTES = D * VRS;         // V^T tile image
   static constexpr int BUF = KBYTES + VBYTES;
   static constexpr int CH = D / 32;              // 16-B chunks per thread per operand
   static constexpr int KU = D / 8;               // 16-B units per K row
 };
 
-// K image: row = key (D*2 bytes), unit u (16 B) stored at u ^ (key & (KU-1) & 15)
+// K image: row = key, 16-B unit u at 16u
 template <int D>
 __device__ __forceinline__ int k_lds_off(int key, int u) {
-  constexpr int KU = D / 8;
-  constexpr int MASK = KU >= 16 ? 15 : KU - 1;
-  return key * D * 2 + ((u ^ (key & MASK)) << 4);
+  return key * PrefillCfg<D>::KRS + (u << 4);
 }
-// V^T image: row = d (64 keys = 128 B) of 8-B units u (4 keys each). Unit u = 4st + 2b1 + b0 is stored at
-// position 4st + 2b0 + b1, so the two units one P.V MFMA operand takes (u = 4st + h and 4st + 2 + h) are
-// one aligned 16-B pair read by a single ds_read_b128 (no register shuffles); 16-B pairs are XOR-swizzled
-// by (d >> 1) & 7, conflict-free for the read lane groups.
+// V^T image: row = d (64 keys) of 8-B units u (4 keys each). Unit u = 4st + 2b1 + b0 is stored at position
+// 4st + 2b0 + b1, so the two units one P.V MFMA operand takes (u = 4st + h and 4st + 2 + h) are one
+// aligned 16-B pair read by a single ds_read_b128 (no register shuffles).
+template <int D>
 __device__ __forceinline__ int v_lds_off(int d, int u) {
   const int p = (u & ~3) | ((u & 1) << 1) | ((u >> 1) & 1);
-  return d * 128 + (((p >> 1) ^ ((d >> 1) & 7)) << 4) + ((p & 1) << 3);
+  return d * PrefillCfg<D>::VRS + (p << 3);
 }
 
 __device__ __forceinline__ bf16x8 kv_to_bf16(bf16x8 v, float) { return v; }
@@ -132,8 +136,8 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
       const bf16x8 vv = kv_to_bf16(vst[c], v_scale);
       const bf16x4_t lo = {vv[0], vv[1], vv[2], vv[3]};
       const bf16x4_t hi = {vv[4], vv[5], vv[6], vv[7]};
-      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8)) = lo;
-      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off(d, u8 + 1)) = hi;
+      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off<D>(d, u8)) = lo;
+      *reinterpret_cast<bf16x4_t*>(sv + v_lds_off<D>(d, u8 + 1)) = hi;
     }
   };
 
@@ -217,7 +221,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
         // units 4st + h (lo) and 4st + 2 + h (hi) of row d: one 16-B pair in the image
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off(32 * dt + (lane & 31), 4 * st + h));
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off<D>(32 * dt + (lane & 31), 4 * st + h));
         acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[dt], 0, 0, 0);
       }
     }
