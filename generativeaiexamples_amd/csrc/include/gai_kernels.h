@@ -48,6 +48,9 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
                             int K);
 bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
                    int epi, int out_f32, hipStream_t st);
+// deep-K decode projections: K split over workgroups into fp32 slabs ws[KS][M][N]; returns KS (0: not handled)
+int gai_gemm_dec2_partials_ks(int M, int N, int K);
+int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st);
 
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,

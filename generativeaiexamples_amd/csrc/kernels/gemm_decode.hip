@@ -78,10 +78,12 @@ __device__ __forceinline__ void dec_store8(void* C, size_t off, const float (&v)
   }
 }
 
-template <int MB, int NT, int EPI, bool OUTF32>
+// PART: K is also split over gridDim.y workgroups (deep-K projections: down); each writes its fp32 partial
+// slab [ks][M][N] instead of the epilogue, reduced by the split-K tail kernels (gemm_splitk.hip).
+template <int MB, int NT, int EPI, bool OUTF32, bool PART = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                                 void* C, const bf16* __restrict__ bias, const bf16* R,
-                                                                int M, int N, int K, int ldc) {
+                                                                int M, int N, int K, int ldc, float* __restrict__ part) {
   constexpr int KQ = 8 / NT;
   using Cf = DecCfg<MB, KQ>;
   constexpr int ROWS = Cf::ROWS, SPS = Cf::SPS, RB = Cf::RB, CPR = Cf::CPR, L = Cf::L, BKS = Cf::BKS;
@@ -91,12 +93,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntl = wid % NT, kq = wid / NT;
   const int nb = blockIdx.x * BN;
-  const int KW = K / KQ;
+  const int ks = blockIdx.y, KR = K / gridDim.y, kbase = ks * KR;  // this workgroup's K range
+  const int KW = KR / KQ;
   const int nsteps = KW / 32;  // host: multiple of L
   const int nstages = nsteps / SPS;
 
   // ---- weight stream: rows nb + 16 ntl + (lane & 15), k = kq KW + 32 s + 8 (lane >> 4)
-  const bf16* wp = W + (size_t)min(nb + 16 * ntl + (lane & 15), N - 1) * K + (size_t)kq * KW + 8 * (lane >> 4);
+  const bf16* wp = W + (size_t)min(nb + 16 * ntl + (lane & 15), N - 1) * K + kbase + (size_t)kq * KW + 8 * (lane >> 4);
 
   // ---- activation staging: chunk p = (4 wid + j) 64 + lane of a stage's [KQ][ROWS][CPR] chunks
   const bf16* asrc[4];
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
   for (int j = 0; j < 4; ++j) {
     const int p = (wid * 4 + j) * 64 + lane;
     const int strip = p / (ROWS * CPR), rem = p % (ROWS * CPR), r = rem / CPR, c = rem % CPR;
-    asrc[j] = A + (size_t)min(r, M - 1) * K + (size_t)strip * KW + 8 * c;
+    asrc[j] = A + (size_t)min(r, M - 1) * K + kbase + (size_t)strip * KW + 8 * c;
     adst[j] = strip * ROWS * RB + r * RB + 16 * (c ^ dec_swz<MB, KQ>(r));
   }
   bf16x8 ast[2][4];
@@ -173,7 +176,23 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(kq * ROWS + 16 * i + 4 * cq + r) * RS + 16 * ntl + (lane & 15)] = acc[i][r];
   __syncthreads();
-  if (EPI == EPI_SWIGLU) {
+  if constexpr (PART) {
+    constexpr int ITEMS = ROWS * BN / 8;
+    for (int e = tid; e < ITEMS; e += kThreads) {
+      const int m = e / (BN / 8), c0 = 8 * (e % (BN / 8));
+      const int n = nb + c0;
+      if (m >= M || n >= N) continue;
+      float v[8];
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) t += red[(q * ROWS + m) * RS + c0 + x];
+        v[x] = t;
+      }
+      dec_store8<true>(part, ((size_t)ks * M + m) * N + n, v);
+    }
+  } else if (EPI == EPI_SWIGLU) {
     // 16-column tiles (2j, 2j + 1) are (gate, up); output columns nb / 2 + 16 j + 8 h .. + 7
     constexpr int ITEMS = ROWS * NT;  // (m, j, h)
     for (int e = tid; e < ITEMS; e += kThreads) {
@@ -220,10 +239,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
 template <int MB, int NT>
 constexpr int dec2_steps_multiple() { return DecCfg<MB, 8 / NT>::L; }
 
-template <int MB, int NT, int EPI, bool OUTF32>
+template <int MB, int NT, int EPI, bool OUTF32, bool PART = false>
 void dec2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                 hipStream_t st) {
-  auto kern = gemm_dec2_kernel<MB, NT, EPI, OUTF32>;
+                 hipStream_t st, int KS = 1, float* part = nullptr) {
+  auto kern = gemm_dec2_kernel<MB, NT, EPI, OUTF32, PART>;
   constexpr int lds = 2 * kStage;
   static bool once = false;
   if (!once) {
@@ -231,8 +250,8 @@ void dec2_launch(const void* A, const void* W, void* C, const void* bias, const 
     once = true;
   }
   const int blocks = (N + 16 * NT - 1) / (16 * NT);
-  kern<<<blocks, kThreads, lds, st>>>((const bf16*)A, (const bf16*)W, C, (const bf16*)bias, (const bf16*)R, M, N, K,
-                                      ldc);
+  kern<<<dim3(blocks, KS), kThreads, lds, st>>>((const bf16*)A, (const bf16*)W, C, (const bf16*)bias, (const bf16*)R,
+                                                M, N, K, ldc, part);
   GAI_LAUNCH_CHECK();
 }
 
@@ -333,4 +352,43 @@ bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, cons
   if (M <= 16) return dec2_run<1>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
   if (M <= 32) return dec2_run<2>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
   return dec2_run<4>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+}
+
+namespace {
+
+// K split for the partial-slab mode: the smallest KS (2..16) whose per-workgroup K range fits the
+// unrolled loop and that gives >= 192 workgroups (a K range per CU long enough to stream, few slabs).
+template <int MB>
+int dec2_part_ks(int N, int K, int NT) {
+  const int blocks = (N + 16 * NT - 1) / (16 * NT);
+  for (int KS = 2; KS <= 16; ++KS)
+    if (K % KS == 0 && (K / KS) % 32 == 0 && dec2_shape_ok<MB>(NT, K / KS) && blocks * KS >= 192) return KS;
+  return 0;
+}
+
+template <int MB>
+int dec2_part_run(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
+  constexpr int NT = MB == 1 ? 4 : 8;
+  const int KS = dec2_part_ks<MB>(N, K, NT);
+  if (KS && launch) dec2_launch<MB, NT, EPI_NONE, true, true>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS, ws);
+  return KS;
+}
+
+int dec2_part_dispatch(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
+  static const int min_k = getenv("GAI_DEC2_PART_MINK") ? atoi(getenv("GAI_DEC2_PART_MINK")) : 8192;
+  static const bool off = getenv("GAI_DEC2") && atoi(getenv("GAI_DEC2")) == 0;
+  // M <= 16: the register-streamed split-K kernel is faster (down at M = 1: 30 vs 34 us)
+  if (off || M <= 16 || M > 64 || N % 16 || K < min_k) return 0;
+  if (M <= 32) return dec2_part_run<2>(A, W, M, N, K, ws, st, launch);
+  return dec2_part_run<4>(A, W, M, N, K, ws, st, launch);
+}
+
+}  // namespace
+
+// Deep-K decode projections (down: K = 14336) on the natural layout: LDS-staged activations, K split over
+// KS workgroups writing fp32 slabs ws[KS][M][N] for the split-K tail kernels. Returns KS (0: shape not
+// handled, nothing launched).
+int gai_gemm_dec2_partials_ks(int M, int N, int K) { return dec2_part_dispatch(nullptr, nullptr, M, N, K, nullptr, 0, false); }
+int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st) {
+  return dec2_part_dispatch(A, W, M, N, K, ws, st, true);
 }

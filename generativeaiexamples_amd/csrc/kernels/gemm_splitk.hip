@@ -396,7 +396,7 @@ int stream_ks(int N, int K) {
 int gai_gemm_splitk_ks(int M, int N, int K) { return use_legacy(N, K) ? legacy_ks(M, N, K) : stream_ks(N, K); }
 
 size_t gai_gemm_splitk_ws_bytes(int M, int N, int K) {
-  const int KS = gai_gemm_splitk_ks(M, N, K);
+  const int KS = max(gai_gemm_splitk_ks(M, N, K), gai_gemm_dec2_partials_ks(M, N, K));
   return (size_t)(KS > 1 ? KS : 1) * M * N * sizeof(float);
 }
 
@@ -564,8 +564,10 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
     gai_rmsnorm(h, res, res, g, out, M, N, eps, st);
     return;
   }
-  const int KS = gai_gemm_splitk_ks(M, N, K);
-  launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  // deep K (down): LDS-staged decode kernel writing K-split slabs on the natural layout
+  const int ks2 = psw ? 0 : gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+  const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
+  if (!ks2) launch_partials(A, B, M, N, K, KS, ws, psw, st);
   const int nch = (N + 2047) / 2048;
 #define GAI_FN(NC)                                                                                          \
   if (nch == NC) {                                                                                          \
@@ -654,9 +656,11 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
   if (psw && N % 16) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: pre-shuffled weights need N % 16 == 0");
   if (M == 0 || N == 0) return;
   if (M > 64) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: M must be <= 64");
-  // natural weight layout: the LDS-staged decode kernel (gemm_decode.hip) when the shape fits
+  // natural weight layout: the LDS-staged decode kernel (gemm_decode.hip) when the shape fits - single
+  // pass for the wide projections, K-split slabs for the deep ones
   if (!psw && gai_gemm_dec2(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st)) return;
-  const int KS = gai_gemm_splitk_ks(M, N, K);
+  const int ks2 = psw ? 0 : gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+  const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (KS == 0) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: K must be a multiple of 512");
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   if (!use_legacy(N, K) && KS == 1) {
@@ -665,7 +669,7 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
     else dispatch_stream_ks1<4>(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, psw, st);
     return;
   }
-  launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  if (!ks2) launch_partials(A, B, M, N, K, KS, ws, psw, st);
 #define GAI_SKR(E)                                                         \
   case E:                                                                  \
     if (out_f32)                                                           \

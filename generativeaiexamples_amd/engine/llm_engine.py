@@ -57,9 +57,10 @@ class EngineConfig:
     kv_memory_bytes: Optional[int] = None
     prefix_cache: bool = True
     use_graphs: bool = True
-    # keep an MFMA-fragment-shuffled copy of the down projection (ops.preshuffle_weight, see
-    # LlamaModel.DECODE_PROJECTIONS): +3.8 GB on Llama-3-8B for a 1.2x faster decode down GEMM
-    decode_preshuffle: bool = True
+    # keep MFMA-fragment-shuffled copies of the decode projections (ops.preshuffle_weight, see
+    # LlamaModel.DECODE_PROJECTIONS): a second copy of those weights in HBM for <= 4 % faster decode
+    # GEMMs; off by default (one weight layout, all HBM beyond the weights goes to the KV cache)
+    decode_preshuffle: bool = False
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     # multi-step decode: when every running sequence is decoding (nothing waiting), run this many
     # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)

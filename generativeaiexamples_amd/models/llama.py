@@ -232,11 +232,11 @@ class LlamaModel:
             self.w["norm_b"] = e(D)
         self.w["lm_head"] = self.w["embed"] if c.tie_embeddings else e(self.vocab_local, D)
 
-    # Only the down projection keeps a fragment-shuffled decode copy (+3.8 GB on Llama-3-8B): its
-    # split-K stream runs 38 vs 45 us at M = 64 from it. QKV / O gain < 1 us from a copy and the wide
-    # gate_up / LM head run on the LDS-staged decode kernel from the natural layout
-    # (profiles/r2/dec2_minwg_sweep.txt).
-    DECODE_PROJECTIONS = ("down",)
+    # Projections that may keep a fragment-shuffled decode copy (ops.preshuffle_weight, opt-in through
+    # EngineConfig.decode_preshuffle). Off by default: every decode GEMM runs from the single natural
+    # layout - the down projection on the LDS-staged K-split kernel at 38.9 us vs 37.5 us from a 3.8 GB
+    # copy at M = 64 (profiles/r2/dec_gemm_hbm_part.jsonl), QKV / O within 1 us.
+    DECODE_PROJECTIONS = ("qkv", "o", "down", "proj")
 
     def preshuffle_decode_weights(self) -> int:
         """Attach fragment-shuffled copies of the per-layer projection weights for the decode GEMM
