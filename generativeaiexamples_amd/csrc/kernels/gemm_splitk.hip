@@ -624,9 +624,13 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
   const int N = (Hq + 2 * Hkv) * D;
   if (M < 1 || M > 64 || (D != 64 && D != 128 && D != 256) || N % 16) return 0;
   if (!psw && gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) return 0;  // single-pass kernel owns it
-  const int KS = gai_gemm_splitk_ks(M, N, K);
+  const int ks2 = psw ? 0 : gai_gemm_dec2_partials_ks(M, N, K);
+  const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (KS <= 1) return 0;
-  launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  if (ks2)
+    gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+  else
+    launch_partials(A, B, M, N, K, KS, ws, psw, st);
   const long items = (long)M * (Hq + 2 * Hkv);
   const float iks = 1.f / k_scale, ivs = 1.f / v_scale;
 #define GAI_SRK(DD)                                                                                               \
