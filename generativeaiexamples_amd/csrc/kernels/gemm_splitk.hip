@@ -546,6 +546,45 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(const float* __
   }
 }
 
+// The same tail with 1024 threads x 4 columns (N <= 4096): one workgroup per row is all the parallelism
+// a batch-64 decode step has, so the row's slab loads are spread over 4x the waves to keep more of them
+// in flight per CU.
+__global__ __launch_bounds__(1024) void splitk_add_rmsnorm_w4_kernel(const float* __restrict__ part, int KS, int M,
+                                                                     int N, const bf16* __restrict__ bias, bf16* res,
+                                                                     const bf16* __restrict__ g, float eps,
+                                                                     bf16* __restrict__ out) {
+  __shared__ float scratch[16];
+  const int m = blockIdx.x, idx = threadIdx.x * 4;
+  const bool live = idx < N;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  bf16x4 rr, gg;
+  if (live) {
+    rr = *reinterpret_cast<const bf16x4*>(res + (size_t)m * N + idx);
+    gg = *reinterpret_cast<const bf16x4*>(g + idx);
+    sum_slabs<4>(part + (size_t)m * N + idx, (size_t)M * N, KS, v);
+  }
+  float ss = 0.f;
+  if (live) {
+    bf16x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float h = v[j];
+      if (bias) h += (float)bias[idx + j];
+      r[j] = (bf16)((float)(bf16)h + (float)rr[j]);
+      v[j] = (float)r[j];
+      ss += v[j] * v[j];
+    }
+    *reinterpret_cast<bf16x4*>(res + (size_t)m * N + idx) = r;
+  }
+  const float inv = rsqrtf(block_sum(ss, scratch) / N + eps);
+  if (live) {
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] * inv * (float)gg[j]);
+    *reinterpret_cast<bf16x4*>(out + (size_t)m * N + idx) = o;
+  }
+}
+
 }  // namespace
 
 int gai_gemm_splitk_fusable_norm(int M, int N, int K) {
@@ -568,6 +607,12 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
   const int ks2 = psw ? 0 : gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (!ks2) launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  if (N <= 4096 && N % 4 == 0 && getenv("GAI_NORM_TAIL_256") == nullptr) {
+    splitk_add_rmsnorm_w4_kernel<<<M, 1024, 0, st>>>(ws, KS, M, N, (const bf16*)bias, (bf16*)res, (const bf16*)g,
+                                                     eps, (bf16*)out);
+    GAI_LAUNCH_CHECK();
+    return;
+  }
   const int nch = (N + 2047) / 2048;
 #define GAI_FN(NC)                                                                                          \
   if (nch == NC) {                                                                                          \
