@@ -5,8 +5,8 @@
 //
 // attn_prefill: varlen, causal or bidirectional, GQA. Workgroup = 4 waves; each
 // wave owns 32 query rows of one q-head, the workgroup shares 64-key K / V^T tiles
-// in LDS (register-staged, issue-early / write-late, one barrier per tile, row-padded
-// images). S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts a full query row
+// in LDS (register-staged, issue-early / write-late: K then V^T through one register set,
+// one barrier per tile, row-padded images). S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts a full query row
 // in one lane (swapped QK^T), so the online softmax is in-register; P^T is fed to
 // the P.V MFMA straight from the S accumulator (k-order permuted on the V side,
 // cdna_hip_programming §3 "accumulator tile as the next MFMA's operand"). exp2
@@ -106,10 +106,12 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     for (int t = 0; t < D / 16; ++t) qf[t] = load8(qp + 16 * t);
   }
 
-  // staging registers (raw cache bytes: the fp8 conversion happens at the LDS write, after the prefetch)
+  // One set of staging registers (raw cache bytes: the fp8 conversion happens at the LDS write), used
+  // twice per tile: the next tile's K is loaded at the top and written to the free buffer after QK^T,
+  // then its V^T is loaded into the same registers and written before the barrier.
   using Stage = typename std::conditional<sizeof(KV) == 1, uint2, bf16x8>::type;
-  Stage kst[Cfg::CH], vst[Cfg::CH];
-  auto load_tile = [&](int kt) {
+  Stage stg[Cfg::CH];
+  auto load_half = [&](int kt, const KV* base) {
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
       const int id = c * 256 + tid;
@@ -117,23 +119,30 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
       const int pidx = kt * 4 + page;
       const int blk = (pidx * kBS < ctx) ? bt[pidx] : bt[0];
       const size_t pbase = ((size_t)blk * Hkv + g) * kBS * D;
-      kst[c] = *reinterpret_cast<const Stage*>(kc + pbase + (size_t)w * 8);  // K page is [16][D] contiguous
-      vst[c] = *reinterpret_cast<const Stage*>(vc + pbase + (size_t)w * 8);  // V^T page is [D][16] contiguous
+      // K page is [16][D] contiguous, V^T page [D][16]
+      stg[c] = *reinterpret_cast<const Stage*>(base + pbase + (size_t)w * 8);
     }
   };
-  auto write_tile = [&](int buf) {
+  auto write_k = [&](int buf) {
     char* sk = smem + buf * Cfg::BUF;
-    char* sv = sk + Cfg::KBYTES;
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
       const int id = c * 256 + tid;
       const int page = id / (2 * D), w = id % (2 * D);
       const int key = page * 16 + w / Cfg::KU, u = w % Cfg::KU;
-      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(kst[c], k_scale);
+      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(stg[c], k_scale);
+    }
+  };
+  auto write_v = [&](int buf) {
+    char* sv = smem + buf * Cfg::BUF + Cfg::KBYTES;
+#pragma unroll
+    for (int c = 0; c < Cfg::CH; ++c) {
+      const int id = c * 256 + tid;
+      const int page = id / (2 * D), w = id % (2 * D);
       const int d = w >> 1, half = w & 1;
       const int u8 = 4 * page + 2 * half;
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      const bf16x8 vv = kv_to_bf16(vst[c], v_scale);
+      const bf16x8 vv = kv_to_bf16(stg[c], v_scale);
       const bf16x4_t lo = {vv[0], vv[1], vv[2], vv[3]};
       const bf16x4_t hi = {vv[4], vv[5], vv[6], vv[7]};
       *reinterpret_cast<bf16x4_t*>(sv + v_lds_off<D>(d, u8)) = lo;
@@ -148,13 +157,16 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
   const float sl2 = scale * kLog2e;
 
   if (ntiles > 0) {
-    load_tile(0);
-    write_tile(0);
+    load_half(0, kc);
+    write_k(0);
+    load_half(0, vc);
+    write_v(0);
   }
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < ntiles) load_tile(kt + 1);
+    const bool more = kt + 1 < ntiles;
+    if (more) load_half(kt + 1, kc);
     const char* sk = smem + cur * Cfg::BUF;
     const char* sv = sk + Cfg::KBYTES;
 
@@ -169,6 +181,10 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
         s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], s[sub], 0, 0, 0);
       }
+    }
+    if (more) {  // buffer cur ^ 1 was released by the previous barrier
+      write_k(cur ^ 1);
+      load_half(kt + 1, vc);
     }
     // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves.
     // Interior tiles (every key < ctx and, causal, <= the wave's first query position) skip the
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     }
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
-    if (kt + 1 < ntiles) write_tile(cur ^ 1);
+    if (more) write_v(cur ^ 1);
     __syncthreads();
   }
 

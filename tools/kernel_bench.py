@@ -262,6 +262,7 @@ def main():
     if "prefill" in only:
         bench_prefill(rows, 4, 2048, 32, 8, 128)
         bench_prefill(rows, 64, 512, 16, 16, 64)
+        bench_prefill(rows, 4, 2048, 16, 16, 256)  # Gemma-7B attention shape
     if "decode_sweep" in only:
         for sp in (128, 256, 512, 1024, 2048):
             bench_decode(rows, 64, 2600, 32, 8, 128, sp)
