@@ -69,6 +69,19 @@ __device__ __forceinline__ int v_lds_off(int d, int u) {
   return d * PrefillCfg<D>::VRS + (p << 3);
 }
 
+// 16 (bf16 cache) or 8 (fp8 cache) bytes at base + off through a buffer resource built from the wave-uniform
+// page base: the load's only VGPR operand is the loop-invariant lane offset, so no per-tile 64-bit address
+// registers exist for the compiler to recycle (and then wait on) while the load is in flight.
+template <typename T>
+__device__ __forceinline__ T buf_load(const void* base, unsigned off) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  if constexpr (sizeof(T) == 16) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+}
+
 __device__ __forceinline__ bf16x8 kv_to_bf16(bf16x8 v, float) { return v; }
 __device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to_bf16(v, s); }
 
@@ -109,18 +122,29 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
   // One set of staging registers (raw cache bytes: the fp8 conversion happens at the LDS write), used
   // twice per tile: the next tile's K is loaded at the top and written to the free buffer after QK^T,
   // then its V^T is loaded into the same registers and written before the barrier.
+  // Piece c of thread tid (16 B of a tile half) lies in page (c*256 + tid) / 2D of the tile, which is
+  // wave-uniform (a wave's 64 pieces never straddle a page): the page's physical block is looked up with a
+  // scalar load one tile ahead (nblk), and each load is a buffer load from that block's scalar base at a
+  // loop-invariant 32-bit per-lane offset (no per-lane block-table round trip or 64-bit address math in the loop).
   using Stage = typename std::conditional<sizeof(KV) == 1, uint2, bf16x8>::type;
   Stage stg[Cfg::CH];
-  auto load_half = [&](int kt, const KV* base) {
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  unsigned voff[Cfg::CH];
+#pragma unroll
+  for (int c = 0; c < Cfg::CH; ++c) voff[c] = (unsigned)(((c * 256 + tid) % (2 * D)) * 8 * sizeof(KV));
+  int nblk[Cfg::CH];
+  auto lookup = [&](int kt) {
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
-      const int id = c * 256 + tid;
-      const int page = id / (2 * D), w = id % (2 * D);
-      const int pidx = kt * 4 + page;
-      const int blk = (pidx * kBS < ctx) ? bt[pidx] : bt[0];
-      const size_t pbase = ((size_t)blk * Hkv + g) * kBS * D;
+      const int pidx = kt * 4 + (c * 256 + wid_u * 64) / (2 * D);
+      nblk[c] = bt[pidx * kBS < ctx ? pidx : 0];
+    }
+  };
+  auto load_half = [&](const KV* base) {
+#pragma unroll
+    for (int c = 0; c < Cfg::CH; ++c) {
       // K page is [16][D] contiguous, V^T page [D][16]
-      stg[c] = *reinterpret_cast<const Stage*>(base + pbase + (size_t)w * 8);
+      stg[c] = buf_load<Stage>(base + ((size_t)nblk[c] * Hkv + g) * (kBS * D), voff[c]);
     }
   };
   auto write_k = [&](int buf) {
@@ -157,16 +181,22 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
   const float sl2 = scale * kLog2e;
 
   if (ntiles > 0) {
-    load_half(0, kc);
+    lookup(0);
+    load_half(kc);
     write_k(0);
-    load_half(0, vc);
+    load_half(vc);
     write_v(0);
+    lookup(1);
   }
+  // Q fragments landed: without this wait the ntiles == 0 path reaches the loop header with the Q loads
+  // pending, and hipcc's waitcnt pass then keeps vmcnt(7..0) in front of every tile's QK^T MFMAs, which
+  // (counters are in order) waits for the next tile's K loads issued just above them.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < ntiles;
-    if (more) load_half(kt + 1, kc);
+    if (more) load_half(kc);
     const char* sk = smem + cur * Cfg::BUF;
     const char* sv = sk + Cfg::KBYTES;
 
@@ -184,8 +214,9 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     }
     if (more) {  // buffer cur ^ 1 was released by the previous barrier
       write_k(cur ^ 1);
-      load_half(kt + 1, vc);
+      load_half(vc);
     }
+    lookup(kt + 2);  // pages past the context resolve to entry 0 (never read unmasked)
     // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves.
     // Interior tiles (every key < ctx and, causal, <= the wave's first query position) skip the
     // per-element mask: wave-uniform test, so only the diagonal / tail tiles pay for it.

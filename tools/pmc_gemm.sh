@@ -1,10 +1,14 @@
+# rocprofv3 counter passes of one prefill GEMM shape: hand-written ring / w4 kernels vs hipBLASLt.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r2e
+export PYTHONPATH=$R
+O=$R/gpurun_out/pmc_gemm
 mkdir -p $O
-timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
-for arm in ring blas; do
+for arm in ring w4 blas; do
+  timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d $O/t_$arm -o t --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/t_$arm.log 2>&1 || exit 2
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES -d $O/p1_$arm -o p1 --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/p1_$arm.log 2>&1 || exit 3
   timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM -d $O/p2_$arm -o p2 --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/p2_$arm.log 2>&1 || exit 4
+  timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d $O/p3_$arm -o p3 --output-format csv -- python3 $R/tools/gemm_one.py $arm 4096 4096 > $O/p3_$arm.log 2>&1 || exit 5
 done
+echo ok
