@@ -772,6 +772,153 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 }
 
 // ----------------------------------------------------------------------------------------------
+// Persistent 4-wave ring kernel: gemm_w4_kernel's tile, waves and phase, but one workgroup per CU
+// walking tiles blockIdx.x, +G, +2G, ... with ONE unit ring running across its tiles. The last six
+// phases of a tile prefetch units 0..4 of the workgroup's next tile, and the last one reads unit 0's
+// fragments, so a tile's epilogue (AGPR reads + 16-B stores) runs while the next tile's operands are
+// landing and its first MFMAs start right after it: no per-tile ring fill (the non-persistent kernel
+// idles the matrix pipe ~4 phases per tile while units 0..4 load) and no launch tail between
+// workgroup waves. Tile v of the walk goes through the same XCD remap (G % 8 == 0, so v % 8 is the
+// XCD) and grouped raster: the 32 CUs of an XCD work on 32 neighbouring tiles at a time.
+// ----------------------------------------------------------------------------------------------
+template <int EPI, bool OUTF32>
+__global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          void* C, const bf16* bias, const bf16* R, int M, int N,
+                                                          int K, int ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // RNS slots x [A 16K | B 16K]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
+  const int tiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int n_my = (tiles - (int)blockIdx.x + G - 1) / G;
+  auto coords = [&](int it, int& m0, int& n0) {
+    const int wg = xcd_remap((int)blockIdx.x + it * G, tiles);
+    constexpr int GM = 4;
+    const int group = wg / (GM * tiles_n);
+    const int first_m = group * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    const int pin = wg % (GM * tiles_n);
+    m0 = (first_m + pin % gsz) * LBM;
+    n0 = (pin / gsz) * LBN;
+  };
+  auto sources = [&](int m0, int n0, const bf16** as, const bf16** bs) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (wid * 4 + j) * 16 + (lane >> 2);
+      const int cg = (lane & 3) ^ lswz(row);
+      as[j] = A + (size_t)min(m0 + row, M - 1) * K + cg * 8;
+      bs[j] = B + (size_t)min(n0 + row, N - 1) * K + cg * 8;
+    }
+  };
+  const int wm = wid >> 1, wn = wid & 1;
+  const int rsw = (((lane >> 4) ^ lswz(lane & 15)) << 4);
+  const int a_rd = (wm * 128 + (lane & 15)) * 64 + rsw;
+  const int b_rd = kUnitHalf + (wn * 128 + (lane & 15)) * 64 + rsw;
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto phase_end = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): next unit's fragments in registers
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // unit u+2 landed (u+3..u+5 in flight)
+    barrier();
+  };
+  // 64 MFMAs on (af, bfr); spread between them: the 8 glds of k-unit ks of (as, bs) into ring slot
+  // g_slot and the 16 ds_reads of ring unit g_rd into (naf, nbf). g_* are walk-global unit numbers.
+  auto phase = [&](const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int g_rd, int g_slot,
+                   const bf16* const* as, const bf16* const* bs, int ks) {
+    char* d = smem + (g_slot % RNS) * kUnitBytes + wid * 4096;
+    const char* sr = smem + (g_rd % RNS) * kUnitBytes;
+    for_each_const<64>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int i = t >> 3, j = t & 7;
+      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                   :
+                   : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
+                   : GAI_AGPR_CLOBBERS);
+      constexpr int g = (t - 5) / 8, r = t / 2;
+      if constexpr (t % 8 == 5 && g < 4) glds16(as[g] + ks * 32, d + g * 1024);
+      else if constexpr (t % 8 == 5) glds16(bs[g - 4] + ks * 32, d + kUnitHalf + (g - 4) * 1024);
+      else if constexpr (t % 2 == 0 && t < 32 && r < 8) naf[r] = *reinterpret_cast<const bf16x8*>(sr + a_rd + r * 1024);
+      else if constexpr (t % 2 == 0 && t < 32) nbf[r - 8] = *reinterpret_cast<const bf16x8*>(sr + b_rd + (r - 8) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  const int nu = K / 32;  // host guarantees nu even and nu >= 6
+  int m0, n0;
+  coords(0, m0, n0);
+  const bf16 *ca[4], *cb[4], *xa[4], *xb[4];
+  sources(m0, n0, ca, cb);
+  asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+#pragma unroll
+  for (int u = 0; u < RNS; ++u) {
+    char* dd = smem + u * kUnitBytes + wid * 4096;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(ca[j] + u * 32, dd + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(cb[j] + u * 32, dd + kUnitHalf + j * 1024);
+  }
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // units 0 and 1 landed
+  barrier();
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + a_rd + i * 1024);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + b_rd + j * 1024);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  barrier();  // every wave has slot 0 in registers before phase 0 restages it
+
+  for (int it = 0, gb = 0; it < n_my; ++it, gb += nu) {
+    // the next tile's operand sources; past the last tile, dummy re-reads of this tile's first units
+    // into slots no later phase reads (keeps every phase's glds / vmcnt count uniform)
+    int nm0 = m0, nn0 = n0;
+    if (it + 1 < n_my) coords(it + 1, nm0, nn0);
+    sources(nm0, nn0, xa, xb);
+    int u = 0;
+    for (; u < nu - 6; u += 2) {
+      phase(a0, b0, a1, b1, gb + u + 1, gb + u + RNS, ca, cb, u + RNS);
+      phase_end();
+      phase(a1, b1, a0, b0, gb + u + 2, gb + u + 1 + RNS, ca, cb, u + 1 + RNS);
+      phase_end();
+    }
+    // u = nu - 6: the ring crosses into the next tile (this tile's unit nu-1, then next units 0..4)
+    phase(a0, b0, a1, b1, gb + u + 1, gb + u + RNS, ca, cb, nu - 1);
+    phase_end();
+    phase(a1, b1, a0, b0, gb + u + 2, gb + u + 1 + RNS, xa, xb, 0);
+    phase_end();
+#pragma unroll
+    for (int s = 1; s < 5; s += 2) {
+      u += 2;
+      phase(a0, b0, a1, b1, gb + u + 1, gb + u + RNS, xa, xb, s);
+      phase_end();
+      phase(a1, b1, a0, b0, gb + u + 2, gb + u + 1 + RNS, xa, xb, s + 1);
+      phase_end();
+    }
+    // (a0, b0) now hold the next tile's unit-0 fragments; this tile's accumulators are complete
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
+    for_each_const<8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      f32x4 row[8];
+      read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
+      epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+    });
+    asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+    m0 = nm0;
+    n0 = nn0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ca[j] = xa[j];
+      cb[j] = xb[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+// ----------------------------------------------------------------------------------------------
 // Skinny kernel (decode): 8 waves split K inside the workgroup
 // ----------------------------------------------------------------------------------------------
 template <int MT, int NF, int EPI, bool OUTF32>
@@ -912,6 +1059,25 @@ void launch_w4(const void* A, const void* B, void* C, const void* bias, const vo
   GAI_LAUNCH_CHECK();
 }
 
+template <int EPI, bool OUTF32>
+void launch_w4p(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                hipStream_t st) {
+  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      gai_launch_error(__FILE__, __LINE__, "gemm_w4p: cannot query the CU count");
+    set_max_lds(gemm_w4p_kernel<EPI, OUTF32>);
+  }
+  // one workgroup per CU (160 KiB LDS each), a multiple of 8 so that walk index % 8 stays the XCD
+  const int grid = tiles <= ncu ? tiles : (ncu & ~7);
+  gemm_w4p_kernel<EPI, OUTF32><<<grid, 256, RNS * kUnitBytes, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                    (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
+  GAI_LAUNCH_CHECK();
+}
+
 template <int MT, int NF, int EPI, bool OUTF32>
 void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                       int ldc, hipStream_t st) {
@@ -952,8 +1118,9 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force == 4 || force == 7 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force == 4 || force == 7 || force == 8 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
+    if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if (force == 7) return launch_w4<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   }

@@ -11,10 +11,11 @@ from generativeaiexamples_amd import ops
 from generativeaiexamples_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
-KERNELS = {"ring8": 4, "w4": 7}  # force codes in gai_gemm: 8-wave ring, 4-wave asm-MFMA ring
+# force codes in gai_gemm: 8-wave ring, 4-wave asm-MFMA ring, persistent 4-wave ring (tile walk per CU)
+KERNELS = {"ring8": 4, "w4": 7, "w4p": 8}
 
 SHAPES = [(1024, 256, 192), (1280, 1040, 256), (2048, 2304, 1024), (1100, 4096, 4096), (4096, 6144, 320),
-          (1536, 512, 14336)]
+          (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256)]  # last two: > 256 tiles, multi-tile walks
 
 
 def _run(x, w, bias, res, act, out_dtype=torch.bfloat16, force=4):
@@ -65,11 +66,12 @@ def test_ring_gemm_fp32_out(cuda, M, N, K, kern):
 
 
 @pytest.mark.parametrize("kern", list(KERNELS))
-def test_ring_gemm_exact_layout(cuda, kern):
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 256), (8192, 4352, 448)])
+def test_ring_gemm_exact_layout(cuda, kern, M, N, K):
     """Small-integer operands make every product exact in fp32: any row/column mix-up in the swapped
-    operand order or the permlane16 epilogue shows as a wrong integer."""
+    operand order or the permlane16 epilogue shows as a wrong integer (the second shape walks 2-3 tiles
+    per CU in the persistent kernel, so a ring hand-over between tiles is checked exactly too)."""
     torch.manual_seed(9)
-    M, N, K = 1024, 512, 256
     x = torch.randint(-3, 4, (M, K), device=cuda).to(torch.bfloat16)
     w = torch.randint(-3, 4, (N, K), device=cuda).to(torch.bfloat16)
     y = _run(x, w, None, None, None, torch.float32, KERNELS[kern])

@@ -47,6 +47,7 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         arms = {"ring": lambda: nat.gemm(x, w, out, None, None, 0, 4),
                 "w4": lambda: nat.gemm(x, w, out, None, None, 0, 7),
+                "w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
                 "large": lambda: nat.gemm(x, w, out, None, None, 0, 3),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
@@ -61,6 +62,7 @@ def main():
             r[f"{k}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
         r["ring_vs_blas"] = round(r["hipblaslt_ms"] / r["ring_ms"], 3)
         r["w4_vs_blas"] = round(r["hipblaslt_ms"] / r["w4_ms"], 3)
+        r["w4p_vs_blas"] = round(r["hipblaslt_ms"] / r["w4p_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if ops.enable_tuned_blas():
