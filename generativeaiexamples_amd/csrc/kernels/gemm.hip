@@ -337,7 +337,7 @@ __global__ __launch_bounds__(512, 1) void gemm_large_kernel(const bf16* __restri
 }
 
 // ----------------------------------------------------------------------------------------------
-// Ring kernel (prefill, the default for M >= 1024): 256x256 block tile, 8 waves as 2(M) x 4(N),
+// Ring kernel (prefill, force 4; superseded by gemm_w4d_kernel): 256x256 block tile, 8 waves as 2(M) x 4(N),
 // each wave 128x64 = 8x4 MFMA 16x16x32 tiles. K is staged in 32-deep *units* (A 256x32 | B 256x32
 // = 32 KiB) through a ring of RNS = 5 LDS slots (160 KiB) by global_load_lds, 3-4 units ahead of
 // their use. Each unit runs two phases (wave rows 0-63 / 64-127, 16 MFMAs each) and ONE barrier:
@@ -781,7 +781,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 // workgroup waves. Tile v of the walk goes through the same XCD remap (G % 8 == 0, so v % 8 is the
 // XCD) and grouped raster: the 32 CUs of an XCD work on 32 neighbouring tiles at a time.
 // ----------------------------------------------------------------------------------------------
-template <int EPI, bool OUTF32>
+// VAR (tools/microbench/gemm_w4p_ab.hip ablations only; 0 in the framework): bit 0 = no glds / vmcnt
+// waits in the main loop, bit 1 = no barrier at phase ends, bit 2 = no fragment ds_reads in the loop,
+// bit 3 = each glds covers 8 rows x 128 B (full lines; even units rows 0-127, odd 128-255: the request
+// count of a k64 double-unit layout, wrong data)
+template <int EPI, bool OUTF32, int VAR = 0>
 __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
                                                           int K, int ldc) {
@@ -805,11 +809,15 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
   auto sources = [&](int m0, int n0, const bf16** as, const bf16** bs) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int row = (wid * 4 + j) * 16 + (lane >> 2);
-      const int cg = (lane & 3) ^ lswz(row);
+      const int row = VAR & 8 ? (wid * 4 + j) * 8 + (lane >> 3) : (wid * 4 + j) * 16 + (lane >> 2);
+      const int cg = VAR & 8 ? (lane & 7) : (lane & 3) ^ lswz(row);
       as[j] = A + (size_t)min(m0 + row, M - 1) * K + cg * 8;
       bs[j] = B + (size_t)min(n0 + row, N - 1) * K + cg * 8;
     }
+  };
+  // source offset (elements) of k-unit ks
+  auto koff = [&](int ks, int ld) -> size_t {
+    return VAR & 8 ? (size_t)(ks & 1) * 128 * ld + (ks >> 1) * 64 : (size_t)ks * 32;
   };
   const int wm = wid >> 1, wn = wid & 1;
   const int rsw = (((lane >> 4) ^ lswz(lane & 15)) << 4);
@@ -823,8 +831,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
   auto phase_end = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): next unit's fragments in registers
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // unit u+2 landed (u+3..u+5 in flight)
-    barrier();
+    if constexpr (!(VAR & 1)) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // unit u+2 landed
+    if constexpr (!(VAR & 2)) barrier();
+    else __builtin_amdgcn_sched_barrier(0);
   };
   // 64 MFMAs on (af, bfr); spread between them: the 8 glds of k-unit ks of (as, bs) into ring slot
   // g_slot and the 16 ds_reads of ring unit g_rd into (naf, nbf). g_* are walk-global unit numbers.
@@ -840,10 +849,15 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
                    : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
                    : GAI_AGPR_CLOBBERS);
       constexpr int g = (t - 5) / 8, r = t / 2;
-      if constexpr (t % 8 == 5 && g < 4) glds16(as[g] + ks * 32, d + g * 1024);
-      else if constexpr (t % 8 == 5) glds16(bs[g - 4] + ks * 32, d + kUnitHalf + (g - 4) * 1024);
-      else if constexpr (t % 2 == 0 && t < 32 && r < 8) naf[r] = *reinterpret_cast<const bf16x8*>(sr + a_rd + r * 1024);
-      else if constexpr (t % 2 == 0 && t < 32) nbf[r - 8] = *reinterpret_cast<const bf16x8*>(sr + b_rd + (r - 8) * 1024);
+      if constexpr (t % 8 == 5 && g < 4) {
+        if constexpr (!(VAR & 1)) glds16(as[g] + koff(ks, K), d + g * 1024);
+      } else if constexpr (t % 8 == 5) {
+        if constexpr (!(VAR & 1)) glds16(bs[g - 4] + koff(ks, K), d + kUnitHalf + (g - 4) * 1024);
+      } else if constexpr (t % 2 == 0 && t < 32 && r < 8) {
+        if constexpr (!(VAR & 4)) naf[r] = *reinterpret_cast<const bf16x8*>(sr + a_rd + r * 1024);
+      } else if constexpr (t % 2 == 0 && t < 32) {
+        if constexpr (!(VAR & 4)) nbf[r - 8] = *reinterpret_cast<const bf16x8*>(sr + b_rd + (r - 8) * 1024);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -911,6 +925,179 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
     n0 = nn0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      ca[j] = xa[j];
+      cb[j] = xb[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+// ----------------------------------------------------------------------------------------------
+// Persistent 4-wave kernel with full-line operand loads (the default prefill GEMM): gemm_w4p_kernel's
+// walk, waves and AGPR accumulators, but operands are staged in 64-deep *double units* (A 256 x 128 B |
+// B 256 x 128 B = 64 KiB, two slots = 128 KiB LDS) so that each LDS-DMA load covers 8 whole 128-B rows:
+// 8 lanes per line, one full-line L2 request per 8 lanes instead of two 64-B half-line requests. The
+// ablation tools/microbench/gemm_w4p_ab.hip measured that request count as the limiter of the 32-deep
+// ring (profiles/r2/gemm_w4p_ab.jsonl: same bytes in full-line requests +11-20 %, no operand loads at
+// all +20-50 %). Loads are buffer_load ... lds at per-lane row offsets fixed per tile plus a scalar k
+// offset (no 64-bit address arithmetic in the loop). LDS rows are 128 B; 16-B chunk c of row r is
+// stored at position c ^ ((r >> 1) & 7), so each 16-lane ds_read_b128 group (16 rows, one chunk) hits
+// 16 distinct bank groups.
+// Schedule per double unit D (k32 units 2D, 2D+1; slot D & 1), fragments double-buffered in registers:
+//   even phase (MFMA unit 2D, ds_read unit 2D+1), then vmcnt(0) + the one barrier: double D+1 landed,
+//     every wave is done reading slot D;
+//   odd phase (MFMA unit 2D+1, ds_read unit 2D+2 from slot D+1, and the 16 loads of double D+2 into
+//     slot D, one after every 4th MFMA: a burst of LDS-DMA issues stalls the wave): 1-2 phases of
+//     load latency cover.
+// The last two odd phases of a tile load the next tile's doubles 0 and 1, so its epilogue overlaps them.
+// ----------------------------------------------------------------------------------------------
+constexpr int kDblBytes = 2 * 256 * 64 * 2;  // A + B, 64 k
+constexpr int kDblHalf = 256 * 64 * 2;
+
+// VAR (microbench ablations only; 0 in the framework): bit 0 = the 16 loads issued in a burst over the
+// odd phase's first 32 MFMAs (measured 3-9 % slower than 1 per 4 MFMAs: an LDS-DMA issue stalls the
+// wave), bit 1 = no vmcnt wait at even phase ends (timing only)
+template <int EPI, bool OUTF32, int VAR = 0>
+__global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          void* C, const bf16* bias, const bf16* R, int M, int N,
+                                                          int K, int ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 slots x [A 32K | B 32K]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
+  const int tiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int n_my = (tiles - (int)blockIdx.x + G - 1) / G;
+  auto coords = [&](int it, int& m0, int& n0) {
+    const int wg = xcd_remap((int)blockIdx.x + it * G, tiles);
+    constexpr int GM = 4;
+    const int group = wg / (GM * tiles_n);
+    const int first_m = group * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    const int pin = wg % (GM * tiles_n);
+    m0 = (first_m + pin % gsz) * LBM;
+    n0 = (pin / gsz) * LBN;
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
+  // load j (0..7) of wave w, per operand: rows (8w + j) * 8 + lane / 8, 16-B chunk (lane & 7) of the LDS
+  // row <- global chunk (lane & 7) ^ f(row); byte offsets (rows clamped to the matrix: partial tiles)
+  auto offsets = [&](int m0, int n0, int* oa, int* ob) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = (wid * 8 + j) * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      oa[j] = min(m0 + row, M - 1) * K * 2 + gc * 16;
+      ob[j] = min(n0 + row, N - 1) * K * 2 + gc * 16;
+    }
+  };
+  const int wm = wid >> 1, wn = wid & 1;
+  // fragment reads: row wm*128 + 16i + (lane & 15) (f depends on lane & 15 only), chunk 4h + lane / 16
+  const int fr = (lane & 15) >> 1;
+  const int a_rd0 = (wm * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int a_rd1 = (wm * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  const int b_rd0 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int b_rd1 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one k32 phase: 64 MFMAs on (af, bfr); the 16 ds_reads of the next unit (half 1 of slot `rslot` in
+  // an even phase, half 0 in an odd one) interleaved in the first 32 MFMAs and, in an odd phase, the 16
+  // loads of k-double `kd` from (oa, ob) into slot `wslot` spread over all 64
+  auto phase = [&](auto odd_c, const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int rslot,
+                   int wslot, const int* oa, const int* ob, int kd) {
+    constexpr bool ODD = decltype(odd_c)::value;
+    const char* sr = smem + rslot * kDblBytes;
+    char* d = smem + wslot * kDblBytes + wid * 8192;
+    const int ar = ODD ? a_rd0 : a_rd1, br = ODD ? b_rd0 : b_rd1;
+    const int soff = kd * 128;
+    for_each_const<64>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int i = t >> 3, j = t & 7;
+      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                   :
+                   : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
+                   : GAI_AGPR_CLOBBERS);
+      constexpr int g = t >> 1;
+      constexpr bool LD = (VAR & 1) ? (t % 2 == 1 && t < 32) : (t % 4 == 1);  // load issue slots
+      constexpr int gl = (VAR & 1) ? g : (t >> 2);                               // load number 0..15
+      if constexpr (ODD && LD && gl < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(d + gl * 1024), 16, oa[gl], soff, 0, 0);
+      else if constexpr (ODD && LD)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(d + kDblHalf + (gl - 8) * 1024), 16, ob[gl - 8], soff, 0, 0);
+      else if constexpr (t % 2 == 0 && t < 32 && g < 8)
+        naf[g] = *reinterpret_cast<const bf16x8*>(sr + ar + g * 2048);
+      else if constexpr (t % 2 == 0 && t < 32)
+        nbf[g - 8] = *reinterpret_cast<const bf16x8*>(sr + br + (g - 8) * 2048);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): next unit's fragments in registers
+    if constexpr (!ODD) {
+      if constexpr (!(VAR & 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // double D+1 landed (this wave's share)
+      barrier();                                         // ... and every wave's; slot D free
+    }
+  };
+  using EvenT = std::integral_constant<bool, false>;
+  using OddT = std::integral_constant<bool, true>;
+
+  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2
+  int m0, n0;
+  coords(0, m0, n0);
+  int ca[8], cb[8], xa[8], xb[8];
+  offsets(m0, n0, ca, cb);
+  asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd) {
+    char* dst = smem + dd * kDblBytes + wid * 8192;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(dst + j * 1024), 16, ca[j], dd * 128, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(dst + kDblHalf + j * 1024), 16, cb[j], dd * 128, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
+  barrier();
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + a_rd0 + i * 2048);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + b_rd0 + j * 2048);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  for (int it = 0, gd = 0; it < n_my; ++it, gd += nd) {
+    // next tile's sources; past the last tile, dummy re-loads of this tile's doubles 0 / 1 into a slot
+    // no later phase reads
+    int nm0 = m0, nn0 = n0;
+    if (it + 1 < n_my) coords(it + 1, nm0, nn0);
+    offsets(nm0, nn0, xa, xb);
+    int D = 0;
+    for (; D < nd - 2; ++D) {
+      const int s = (gd + D) & 1;
+      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0);
+      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, ca, cb, D + 2);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e, ++D) {
+      const int s = (gd + D) & 1;
+      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0);
+      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, xa, xb, e);
+    }
+    // (a0, b0) hold the next tile's unit-0 fragments; this tile's accumulators are complete
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
+    for_each_const<8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      f32x4 row[8];
+      read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
+      epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+    });
+    asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+    m0 = nm0;
+    n0 = nn0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
       ca[j] = xa[j];
       cb[j] = xb[j];
     }
@@ -1078,6 +1265,24 @@ void launch_w4p(const void* A, const void* B, void* C, const void* bias, const v
   GAI_LAUNCH_CHECK();
 }
 
+template <int EPI, bool OUTF32>
+void launch_w4d(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                hipStream_t st) {
+  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      gai_launch_error(__FILE__, __LINE__, "gemm_w4d: cannot query the CU count");
+    set_max_lds(gemm_w4d_kernel<EPI, OUTF32>);
+  }
+  const int grid = tiles <= ncu ? tiles : (ncu & ~7);
+  gemm_w4d_kernel<EPI, OUTF32><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                 (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
+  GAI_LAUNCH_CHECK();
+}
+
 template <int MT, int NF, int EPI, bool OUTF32>
 void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                       int ldc, hipStream_t st) {
@@ -1118,11 +1323,14 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force == 4 || force == 7 || force == 8 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force == 4 || force == 7 || force == 8 || force == 9 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
     if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if (force == 7) return launch_w4<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    if (force == 4) return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
+      return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   }
   const bool large_ok = M >= 1024 && N >= 256;
   if (force == 3 || (force == 0 && large_ok)) return launch_large<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
@@ -1131,6 +1339,7 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
 
 }  // namespace
 
+#ifndef GAI_GEMM_KERNELS_ONLY
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
               int epi, int out_f32, int force, hipStream_t st) {
   if (M == 0 || N == 0) return;
@@ -1155,3 +1364,4 @@ void gai_gemm(const void* A, const void* B, void* C, const void* bias, const voi
   }
 #undef GAI_GEMM_EPI
 }
+#endif  // GAI_GEMM_KERNELS_ONLY
