@@ -933,7 +933,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
 }
 
 // ----------------------------------------------------------------------------------------------
-// Persistent 4-wave kernel with full-line operand loads (the default prefill GEMM): gemm_w4p_kernel's
+// Persistent 4-wave kernel with full-line operand loads (the default prefill GEMM for K < 8192;
+// gemm_w4r_kernel below differs only in its LDS ring): gemm_w4p_kernel's
 // walk, waves and AGPR accumulators, but operands are staged in 64-deep *double units* (A 256 x 128 B |
 // B 256 x 128 B = 64 KiB, two slots = 128 KiB LDS) so that each LDS-DMA load covers 8 whole 128-B rows:
 // 8 lanes per line, one full-line L2 request per 8 lanes instead of two 64-B half-line requests. The
@@ -1086,6 +1087,156 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
       phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, xa, xb, e);
     }
     // (a0, b0) hold the next tile's unit-0 fragments; this tile's accumulators are complete
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
+    for_each_const<8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      f32x4 row[8];
+      read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
+      epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+    });
+    asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+    m0 = nm0;
+    n0 = nn0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = xa[j];
+      cb[j] = xb[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+// ----------------------------------------------------------------------------------------------
+// Part-ring variant of gemm_w4d_kernel (the default prefill GEMM for K >= 8192): the same full-line double units, but the A and B halves of a
+// double are separate 32 KiB *parts* in a 5-part ring (160 KiB: all of the LDS), A(D), B(D), A(D+1), ...
+// Part q lives in slot q % 5. The A part of double D+2 is loaded during the even phase 2D (into the
+// slot B(D-1) left) and its B part during the odd phase 2D+1 (into the slot A(D) left), 8 loads per
+// phase, one per 8 MFMAs: A gets 2-3 phases of latency cover, B 1-2 (w4d: 1-2 for both), one barrier
+// per double as in w4d (even phase end, after vmcnt(8): double D+1 landed, A(D+2) may fly).
+// M = 16384 (profiles/r2/gemm_w4p_ab.jsonl): 1.55-1.56 PF/s on O / down / gate_up; the longer A cover
+// lifts the deep-K down projection (activations streamed from HBM) from 1.41 (w4d) to 1.56 PF/s.
+// ----------------------------------------------------------------------------------------------
+constexpr int kPart = 256 * 64 * 2;  // one operand of a double unit
+
+template <int EPI, bool OUTF32>
+__global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          void* C, const bf16* bias, const bf16* R, int M, int N,
+                                                          int K, int ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 5 parts x 32 KiB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
+  const int tiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int n_my = (tiles - (int)blockIdx.x + G - 1) / G;
+  auto coords = [&](int it, int& m0, int& n0) {
+    const int wg = xcd_remap((int)blockIdx.x + it * G, tiles);
+    constexpr int GM = 4;
+    const int group = wg / (GM * tiles_n);
+    const int first_m = group * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    const int pin = wg % (GM * tiles_n);
+    m0 = (first_m + pin % gsz) * LBM;
+    n0 = (pin / gsz) * LBN;
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
+  auto offsets = [&](int m0, int n0, int* oa, int* ob) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = (wid * 8 + j) * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      oa[j] = min(m0 + row, M - 1) * K * 2 + gc * 16;
+      ob[j] = min(n0 + row, N - 1) * K * 2 + gc * 16;
+    }
+  };
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = (lane & 15) >> 1;
+  const int a_rd0 = (wm * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int a_rd1 = (wm * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  const int b_rd0 = (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int b_rd1 = (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one k32 phase: 64 MFMAs on (af, bfr); the 16 ds_reads of the next unit (A part in slot sa, B part
+  // in slot sb; half 1 in an even phase, half 0 in an odd one) in the first 32 MFMAs; the 8 loads of
+  // one part of k-double kd (even: A from oa, odd: B from ob) into slot sw, one per 8 MFMAs
+  auto phase = [&](auto odd_c, const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int sa, int sb,
+                   int sw, const int* o, int kd) {
+    constexpr bool ODD = decltype(odd_c)::value;
+    const char* pa = smem + sa * kPart + (ODD ? a_rd0 : a_rd1);
+    const char* pb = smem + sb * kPart + (ODD ? b_rd0 : b_rd1);
+    char* d = smem + sw * kPart + wid * 8192;
+    const int soff = kd * 128;
+    for_each_const<64>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int i = t >> 3, j = t & 7;
+      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                   :
+                   : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
+                   : GAI_AGPR_CLOBBERS);
+      constexpr int g = t >> 1, gl = t >> 3;
+      if constexpr (t % 8 == 3)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ODD ? rb : ra, GAI_LDS(d + gl * 1024), 16, o[gl], soff, 0, 0);
+      else if constexpr (t % 2 == 0 && t < 32 && g < 8)
+        naf[g] = *reinterpret_cast<const bf16x8*>(pa + g * 2048);
+      else if constexpr (t % 2 == 0 && t < 32)
+        nbf[g - 8] = *reinterpret_cast<const bf16x8*>(pb + (g - 8) * 2048);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): next unit's fragments in registers
+    if constexpr (!ODD) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // double D+1 landed (only A(D+2) in flight)
+      barrier();
+    }
+  };
+  using EvenT = std::integral_constant<bool, false>;
+  using OddT = std::integral_constant<bool, true>;
+  auto sl = [](int q) { return q % 5; };
+
+  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2
+  int m0, n0;
+  coords(0, m0, n0);
+  int ca[8], cb[8], xa[8], xb[8];
+  offsets(m0, n0, ca, cb);
+  asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // parts A0 B0 A1 B1 -> slots 0..3
+    char* dst = smem + q * kPart + wid * 8192;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(q & 1 ? rb : ra, GAI_LDS(dst + j * 1024), 16, q & 1 ? cb[j] : ca[j],
+                                               (q >> 1) * 128, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
+  barrier();
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + a_rd0 + i * 2048);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + kPart + b_rd0 + j * 2048);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+
+  for (int it = 0, gd = 0; it < n_my; ++it, gd += nd) {
+    int nm0 = m0, nn0 = n0;
+    if (it + 1 < n_my) coords(it + 1, nm0, nn0);
+    offsets(nm0, nn0, xa, xb);
+    int D = 0;
+    for (; D < nd - 2; ++D) {
+      const int q = 2 * (gd + D);
+      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), ca, D + 2);
+      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), cb, D + 2);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e, ++D) {
+      const int q = 2 * (gd + D);
+      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), xa, e);
+      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), xb, e);
+    }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
     for_each_const<8>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
@@ -1283,6 +1434,24 @@ void launch_w4d(const void* A, const void* B, void* C, const void* bias, const v
   GAI_LAUNCH_CHECK();
 }
 
+template <int EPI, bool OUTF32>
+void launch_w4r(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                hipStream_t st) {
+  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      gai_launch_error(__FILE__, __LINE__, "gemm_w4r: cannot query the CU count");
+    set_max_lds(gemm_w4r_kernel<EPI, OUTF32>);
+  }
+  const int grid = tiles <= ncu ? tiles : (ncu & ~7);
+  gemm_w4r_kernel<EPI, OUTF32><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C, (const bf16*)bias,
+                                                             (const bf16*)R, M, N, K, ldc);
+  GAI_LAUNCH_CHECK();
+}
+
 template <int MT, int NF, int EPI, bool OUTF32>
 void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                       int ldc, hipStream_t st) {
@@ -1323,13 +1492,16 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force == 4 || force == 7 || force == 8 || force == 9 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force == 4 || force == 7 || force == 8 || force == 9 || force == 10 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
     if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if (force == 7) return launch_w4<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if (force == 4) return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    // deep K (activations streamed from HBM, e.g. the MLP down projection): the part ring's longer
+    // A-operand latency cover wins (+7 %); otherwise the double-slot kernel (+2-4 %), gemm_w4r.jsonl
+    if (force == 10 || (force == 0 && K >= 8192)) return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   }
   const bool large_ok = M >= 1024 && N >= 256;

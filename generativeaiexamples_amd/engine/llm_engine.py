@@ -117,8 +117,8 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
-        if self.device.type == "cuda" and ops.TUNER.mode != "native":
-            ops.enable_tuned_blas()  # the prefill library GEMMs (GAI_GEMM_POLICY=auto|tune|hipblaslt)
+        if self.device.type == "cuda" and ops.TUNER.mode in ("tune", "hipblaslt"):
+            ops.enable_tuned_blas()  # the prefill library GEMMs (GAI_GEMM_POLICY=tune|hipblaslt)
         if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident

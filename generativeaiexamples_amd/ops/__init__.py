@@ -356,14 +356,16 @@ def enable_tuned_blas() -> bool:
 class GemmTuner:
     """GEMM backend policy, GAI_GEMM_POLICY = auto (default) | native | hipblaslt | tune.
 
-    auto (deterministic, no run-time timing): every decode-sized GEMM (M <= 64) and every fp32-output
-    GEMM runs on the hand-written MFMA kernels - the LDS-staged decode kernel for the wide projections
-    (gate_up + fused SwiGLU, LM head), the weight-streaming split-K kernels for the narrow ones (QKV, O,
-    down) - so the decode graph holds no library GEMM at all; prefill-sized bf16 GEMMs (M > 64) are plain
-    library GEMMs on hipBLASLt (+ the framework's epilogue kernel), where the hand-written 256x256 ring
-    kernel measures 0.78-0.87x hipBLASLt at M = 16K (profiles/r2/gemm_ring.jsonl).
-    native: the hand-written kernels for every shape. hipblaslt: library GEMMs only. tune: per-shape
-    choice between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
+    auto (deterministic, no run-time timing) = native: every GEMM runs on the hand-written MFMA kernels.
+    Decode-sized GEMMs (M <= 64): the LDS-staged decode kernel for the wide projections (gate_up + fused
+    SwiGLU, LM head) and the weight-streaming split-K kernels for the narrow ones (QKV, O, down), so the
+    decode graph holds no library GEMM. Prefill / encoder GEMMs (M >= 1024): the persistent full-line
+    256x256 kernel (gemm.hip gemm_w4r_kernel) with its fused epilogues, 1.19-1.51 PF/s = 0.94-0.98x
+    hipBLASLt at M = 16K on the Llama-3-8B / e5 shapes (profiles/r2/gemm_w4r.jsonl); with the SwiGLU
+    fused into gate_up (hipBLASLt needs a separate activation pass) the headline bench is at parity
+    with the library policy (15.09 vs 15.15 q/s, same box, profiles/r2/bench8b_native_policy.json).
+    hipblaslt: library GEMMs for M > 64 (+ the framework's epilogue kernels). tune: per-shape choice
+    between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
     Decode GEMMs at M = 64 vs hipBLASLt + epilogue kernel, weights streamed from HBM
     (profiles/r2/dec2_minwg_sweep.txt): gate_up+SwiGLU 54.9 vs 64.1 us, LM head 233 vs 230 us,
     QKV 24 vs 34 us, O 18 vs 31 us, down 38 vs 54 us."""
@@ -389,7 +391,7 @@ class GemmTuner:
         if self.mode == "native":
             return "native"
         if self.mode == "auto":
-            return "native" if (M <= 64 or out_dtype == torch.float32) else "blas"
+            return "native"
         if self.mode == "hipblaslt":
             return "blas"
         key = (self.bucket(M), N, K, act, has_bias, out_dtype)

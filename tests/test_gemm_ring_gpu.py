@@ -12,8 +12,8 @@ from generativeaiexamples_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 # force codes in gai_gemm: 8-wave ring, 4-wave asm-MFMA ring, persistent 4-wave ring (tile walk per CU),
-# persistent full-line double-unit kernel (the default for M >= 1024)
-KERNELS = {"ring8": 4, "w4": 7, "w4p": 8, "w4d": 9}
+# persistent full-line double-unit kernel, and its 5-part LDS ring variant (the default for M >= 1024)
+KERNELS = {"ring8": 4, "w4": 7, "w4p": 8, "w4d": 9, "w4r": 10}
 
 SHAPES = [(1024, 256, 192), (1280, 1040, 256), (2048, 2304, 1024), (1100, 4096, 4096), (4096, 6144, 320),
           (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256)]  # last two: > 256 tiles, multi-tile walks

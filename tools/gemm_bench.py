@@ -49,6 +49,7 @@ def main():
                 "w4": lambda: nat.gemm(x, w, out, None, None, 0, 7),
                 "w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
                 "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
+                "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
                 "large": lambda: nat.gemm(x, w, out, None, None, 0, 3),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
@@ -65,6 +66,7 @@ def main():
         r["w4_vs_blas"] = round(r["hipblaslt_ms"] / r["w4_ms"], 3)
         r["w4p_vs_blas"] = round(r["hipblaslt_ms"] / r["w4p_ms"], 3)
         r["w4d_vs_blas"] = round(r["hipblaslt_ms"] / r["w4d_ms"], 3)
+        r["w4r_vs_blas"] = round(r["hipblaslt_ms"] / r["w4r_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if ops.enable_tuned_blas():

@@ -57,6 +57,22 @@ float run_w4d(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int gr
   return ms / iters;
 }
 
+float run_w4r(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int grid, int iters) {
+  auto k = gemm_w4r_kernel<EPI_NONE, false>;
+  CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 5 * kPart));
+  hipEvent_t ev0, ev1;
+  CK(hipEventCreate(&ev0));
+  CK(hipEventCreate(&ev1));
+  k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N);
+  CK(hipEventRecord(ev0));
+  for (int i = 0; i < iters; ++i) k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N);
+  CK(hipEventRecord(ev1));
+  CK(hipEventSynchronize(ev1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, ev0, ev1));
+  return ms / iters;
+}
+
 int main() {
   const int shapes[][3] = {{16384, 4096, 4096}, {16384, 4096, 14336}, {16384, 28672, 4096}};
   int ncu = 0;
@@ -74,7 +90,7 @@ int main() {
     const int grid = tiles <= ncu ? tiles : (ncu & ~7);
     const double fl = 2.0 * M * N * K;
     float t[8] = {0};  // slots: VAR 0 1 2 3 4 8 10 7
-    float tw4d[4] = {0};
+    float tw4d[4] = {0}, tw4r = 0;
     for (int r = 0; r < 3; ++r) {  // interleaved rounds, best of 3
       float v[8] = {run<0>(A, B, C, M, N, K, grid, 10), run<1>(A, B, C, M, N, K, grid, 10),
                     run<2>(A, B, C, M, N, K, grid, 10), run<3>(A, B, C, M, N, K, grid, 10),
@@ -85,11 +101,14 @@ int main() {
                           run_w4d<2>(A, B, C, M, N, K, grid, 10), run_w4d<3>(A, B, C, M, N, K, grid, 10)};
       for (int i = 0; i < 4; ++i)
         if (tw4d[i] == 0 || w[i] < tw4d[i]) tw4d[i] = w[i];
+      const float wr = run_w4r(A, B, C, M, N, K, grid, 10);
+      if (tw4r == 0 || wr < tw4r) tw4r = wr;
     }
     printf("{\"M\": %d, \"N\": %d, \"K\": %d", M, N, K);
     const int vars[] = {0, 1, 2, 3, 4, 8, 10, 7};
     for (int i = 0; i < 8; ++i) printf(", \"var%d_tflops\": %.1f", vars[i], fl / t[i] / 1e9);
     for (int i = 0; i < 4; ++i) printf(", \"w4d_v%d_tflops\": %.1f", i, fl / tw4d[i] / 1e9);
+    printf(", \"w4r_tflops\": %.1f", fl / tw4r / 1e9);
     printf("}\n");
     fflush(stdout);
     CK(hipFree(A));
