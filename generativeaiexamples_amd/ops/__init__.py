@@ -362,8 +362,9 @@ class GemmTuner:
     decode graph holds no library GEMM. Prefill / encoder GEMMs (M >= 1024): the persistent full-line
     256x256 kernel (gemm.hip gemm_w4r_kernel) with its fused epilogues, 1.19-1.51 PF/s = 0.94-0.98x
     hipBLASLt at M = 16K on the Llama-3-8B / e5 shapes (profiles/r2/gemm_w4r.jsonl); with the SwiGLU
-    fused into gate_up (hipBLASLt needs a separate activation pass) the headline bench is at parity
-    with the library policy (15.09 vs 15.15 q/s, same box, profiles/r2/bench8b_native_policy.json).
+    fused into gate_up (hipBLASLt needs a separate activation pass) the headline bench is within
+    0.4-1.3 % of the library policy on the same box (15.09 vs 15.15 q/s; native / hipblaslt / native
+    15.43 / 15.59 / 15.36 q/s, profiles/r2/policy_ab/); the gap is the deep-K down projection (0.93-0.95x).
     hipblaslt: library GEMMs for M > 64 (+ the framework's epilogue kernels). tune: per-shape choice
     between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
     Decode GEMMs at M = 64 vs hipBLASLt + epilogue kernel, weights streamed from HBM
