@@ -95,8 +95,8 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, 
                     (float)k_scale, (float)v_scale, cur_stream());
 }
 
-// Decode QKV projection fused with RoPE + KV write (split-K path). False: nothing launched, the caller
-// runs linear + rope_kv_write.
+// QKV projection fused with RoPE + KV write: split-K path for decode (M <= 64), the prefill GEMM's
+// epilogue for M >= 1024. False: nothing launched, the caller runs linear + rope_kv_write.
 bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias, const Tensor& pos,
                   const Tensor& cos_sin, const Tensor& slots, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
                   int64_t Hq, int64_t Hkv, int64_t D, double k_scale, double v_scale, Tensor& ws, bool psw) {
@@ -112,10 +112,14 @@ bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias
   TORCH_CHECK(pos.numel() >= M && slots.numel() >= M && q_out.size(0) >= M, "gemm_rope_kv: batch mismatch");
   TORCH_CHECK(k_cache.size(-2) == 16 && k_cache.size(-1) == D && v_cache.size(-1) == 16, "bad kv cache layout");
   const int N = B.size(0);
-  TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
-              "gemm_rope_kv: workspace too small");
   if (bias) check_bf16(*bias, "bias");
   const int f8 = kv_cache_fp8(k_cache, v_cache);
+  if (M > 64)  // prefill: RoPE + KV write in the 256x256 GEMM's epilogue (ws unused)
+    return gai_gemm_prefill_rope_kv(A.data_ptr(), B.data_ptr(), opt_ptr(bias), pos.data_ptr<int>(),
+                                    cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
+                                    k_cache.data_ptr(), v_cache.data_ptr(), M, K, Hq, Hkv, D, f8, cur_stream()) != 0;
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
+              "gemm_rope_kv: workspace too small");
   return gai_gemm_splitk_rope_kv(A.data_ptr(), B.data_ptr(), opt_ptr(bias), pos.data_ptr<int>(),
                                  cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
                                  k_cache.data_ptr(), v_cache.data_ptr(), M, Hq, Hkv, D, f8, (float)k_scale,

@@ -23,6 +23,12 @@ void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, co
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
               int epi, int out_f32, int force, hipStream_t st);
 
+// gemm.hip prefill QKV projection (M >= 1024, D = 128, bf16 KV) with (+ bias) -> RoPE -> q_out / paged K, V^T
+// caches fused into the GEMM epilogue (as gai_gemm + gai_rope_kv_write); returns 0 (nothing launched) otherwise
+int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
+                             const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq,
+                             int Hkv, int D, int kv_fp8, hipStream_t st);
+
 // gemm_fp8.hip (force: 0 auto, 2 tiled 128x128, 3 large 256x256; OCP e4m3fn operands, per-row sa[M] x per-channel sb[N] scales; epi as gai_gemm + 7 bias+quick-gelu)
 void gai_gemm_fp8(const void* A, const void* B, const float* sa, const float* sb, void* C, const void* bias,
                   const void* R, int M, int N, int K, int ldc, int epi, int out_f32, int force, hipStream_t st);

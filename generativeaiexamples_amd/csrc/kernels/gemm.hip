@@ -20,6 +20,7 @@
 #include "gai_common.h"
 #include "gai_kernels.h"
 #include "gai_epilogue.h"
+#include "gai_rope.h"
 
 #include <utility>
 
@@ -953,6 +954,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(const bf16* __restrict
 // The last two odd phases of a tile load the next tile's doubles 0 and 1, so its epilogue overlaps them.
 // ----------------------------------------------------------------------------------------------
 constexpr int kDblBytes = 2 * 256 * 64 * 2;  // A + B, 64 k
+
+// Prefill QKV epilogue (EPI_ROPE_KV, gemm_w4d_kernel only): (+ bias) -> bf16 -> RoPE -> q_out / paged K,
+// V^T caches, exactly the rounding sequence of gemm + rope_kv_write, without the bf16 qkv round trip.
+constexpr int EPI_ROPE_KV = 100;
+struct RopeKvArgs {
+  const int* pos = nullptr;
+  const float* cos_sin = nullptr;
+  const int* slots = nullptr;
+  bf16* q_out = nullptr;
+  bf16* k_cache = nullptr;
+  bf16* v_cache = nullptr;
+  int Hq = 0, Hkv = 0;
+};
 constexpr int kDblHalf = 256 * 64 * 2;
 
 // VAR (microbench ablations only; 0 in the framework): bit 0 = the 16 loads issued in a burst over the
@@ -961,7 +975,7 @@ constexpr int kDblHalf = 256 * 64 * 2;
 template <int EPI, bool OUTF32, int VAR = 0>
 __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc) {
+                                                          int K, int ldc, RopeKvArgs rk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 slots x [A 32K | B 32K]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1092,7 +1106,27 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
       constexpr int i = decltype(ic)::value;
       f32x4 row[8];
       read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
-      epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+      if constexpr (EPI == EPI_ROPE_KV) {
+        // the wave's 128 columns are one head h of [Hq | Hkv | Hkv]; lane (m, q) holds dims 16j + 4q + r
+        // (tile j) and, in tile j + 4, their rotate-half partners 64 further on
+        const int m = m0 + wm * 128 + 16 * i + (lane & 15), nb = n0 + wn * 128, q = lane >> 4;
+        if (m < M && nb < N) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            bf16x4 x1, x2;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = nb + 16 * jj + 4 * q + r;
+              x1[r] = (bf16)(row[jj][r] + (bias ? (float)bias[n] : 0.f));
+              x2[r] = (bf16)(row[jj + 4][r] + (bias ? (float)bias[n + 64] : 0.f));
+            }
+            rope_kv_store<128, bf16>(x1, x2, m, nb / 128, 16 * jj + 4 * q, rk.pos, rk.cos_sin, rk.slots, rk.q_out,
+                                     rk.k_cache, rk.v_cache, rk.Hq, rk.Hkv, 1, 1.f, 1.f);
+          }
+        }
+      } else {
+        epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+      }
     });
     asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
     m0 = nm0;
@@ -1418,7 +1452,7 @@ void launch_w4p(const void* A, const void* B, void* C, const void* bias, const v
 
 template <int EPI, bool OUTF32>
 void launch_w4d(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st) {
+                hipStream_t st, RopeKvArgs rk = {}) {
   const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
   static int ncu = 0;
   if (!ncu) {
@@ -1430,7 +1464,7 @@ void launch_w4d(const void* A, const void* B, void* C, const void* bias, const v
   }
   const int grid = tiles <= ncu ? tiles : (ncu & ~7);
   gemm_w4d_kernel<EPI, OUTF32><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                 (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
+                                                                 (const bf16*)bias, (const bf16*)R, M, N, K, ldc, rk);
   GAI_LAUNCH_CHECK();
 }
 
@@ -1535,5 +1569,25 @@ void gai_gemm(const void* A, const void* B, void* C, const void* bias, const voi
       gai_launch_error(__FILE__, __LINE__, "gemm: unknown epilogue");
   }
 #undef GAI_GEMM_EPI
+}
+
+int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
+                             const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq,
+                             int Hkv, int D, int kv_fp8, hipStream_t st) {
+  const int N = (Hq + 2 * Hkv) * D;
+  if (D != 128 || kv_fp8 || M < 1024 || K % 64 || K < 192 || (size_t)M * K * 2 >= (1ull << 31) ||
+      (size_t)N * K * 2 >= (1ull << 31))
+    return 0;
+  RopeKvArgs rk;
+  rk.pos = pos;
+  rk.cos_sin = cos_sin;
+  rk.slots = slots;
+  rk.q_out = (bf16*)q_out;
+  rk.k_cache = (bf16*)k_cache;
+  rk.v_cache = (bf16*)v_cache;
+  rk.Hq = Hq;
+  rk.Hkv = Hkv;
+  launch_w4d<EPI_ROPE_KV, false>(A, B, nullptr, bias, nullptr, M, N, K, N, st, rk);
+  return 1;
 }
 #endif  // GAI_GEMM_KERNELS_ONLY

@@ -497,7 +497,9 @@ class LlamaModel:
         fuse = (res.is_cuda and ctx.tp_size == 1 and c.norm != "layernorm" and not self.lora_names and T <= 64
                 and os.environ.get("GAI_FUSE_NORM", "1") == "1")
         xn = None
-        fuse_qkv = (res.is_cuda and T <= 64 and not self.lora_names and not c.qk_norm
+        # decode (T <= 64): split-K partials -> RoPE -> q / paged KV in one kernel; prefill (T >= 1024): the
+        # same in the 256x256 GEMM's epilogue (ops.linear_rope_kv falls back where the kernels do not apply)
+        fuse_qkv = (res.is_cuda and (T <= 64 or T >= 1024) and not self.lora_names and not c.qk_norm
                     and os.environ.get("GAI_FUSE_ROPE", "1") == "1")
         # TP prefill: row-parallel projections pipelined with their all-reduce (DistContext.tp_linear_all_reduce)
         overlap = (ctx.tp_size > 1 and not self.lora_names and os.environ.get("GAI_TP_OVERLAP", "1") == "1"
@@ -512,7 +514,7 @@ class LlamaModel:
                 x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
             kc, vc = kv.layer(i)
             ks, vs = kv.scales(i)
-            if fuse_qkv:  # decode: QKV split-K partials -> RoPE -> q / paged KV in one kernel
+            if fuse_qkv:
                 ops.linear_rope_kv(x, w[p + "qkv"], w.get(p + "qkv_b"), fb.positions, self.cos_sin, fb.slots, q, kc,
                                    vc, self.hq, self.hkv, hd, ks, vs)
             else:

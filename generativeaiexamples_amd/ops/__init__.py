@@ -173,7 +173,8 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
                    k_cache, v_cache, Hq: int, Hkv: int, D: int, k_scale=1.0, v_scale=1.0) -> None:
     """QKV projection + RoPE + paged KV write. For decode-sized M the split-K QKV partials are summed,
     rotated and scattered into q_out / the K, V^T caches by ONE kernel (no reduce launch, no bf16 qkv
-    round trip, no rope_kv launch); otherwise ``linear`` + ``rope_kv_write``. Same bf16 roundings."""
+    round trip, no rope_kv launch); for prefill (M >= 1024, head_dim 128, bf16 KV) the 256x256 GEMM's
+    epilogue does the same; otherwise ``linear`` + ``rope_kv_write``. Same bf16 roundings."""
     K = x.shape[-1]
     M = x.numel() // K
     if (x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and 1 <= M <= 64
@@ -183,6 +184,13 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x.device)
         if nat.gemm_rope_kv(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, positions, cos_sin, slots,
                             q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None):
+            return
+    if (x.is_cuda and not isinstance(w, Fp8Weight) and _GEMM_FORCE == 0 and M >= 1024 and TUNER.mode in ("auto", "native")
+            and positions.dtype == torch.int32 and slots.dtype == torch.int32):
+        # prefill: RoPE + paged KV write in the 256x256 GEMM's epilogue (no bf16 qkv round trip)
+        ws = torch.empty(0, dtype=torch.float32, device=x.device)
+        if native().gemm_rope_kv(x.reshape(M, K).contiguous(), w, bias, positions, cos_sin, slots, q_out, k_cache,
+                                 v_cache, Hq, Hkv, D, k_scale, v_scale, ws, False):
             return
     qkv = linear(x, w, bias=bias)
     rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, True, k_scale, v_scale)

@@ -91,3 +91,40 @@ def test_ring_gemm_repeatable(cuda, M, N, K, kern):
         assert torch.equal(_run(x, w, None, None, None, force=f), y0)
     y_ref = ref.linear(x.cpu(), w.cpu())
     assert ((y0.float().cpu() - y_ref.float()).abs() <= 3e-2 + 2e-2 * y_ref.float().abs()).all()
+
+
+@pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(1024, 512, 4, 2, False), (1300, 4096, 32, 8, False),
+                                                  (2048, 256, 8, 2, True)])
+def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
+    """Prefill QKV GEMM with RoPE + paged K / V^T write in its epilogue == gemm + rope_kv_write (same
+    accumulators, same bf16 roundings); skipped slots (-1) leave the caches untouched."""
+    torch.manual_seed(M + K)
+    D, nblk = 128, (M + 15) // 16 + 8
+    N = (Hq + 2 * Hkv) * D
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, dtype=torch.bfloat16) if with_bias else None
+    pos = torch.randint(0, 4096, (M,), device=cuda, dtype=torch.int32)
+    slots = torch.randperm(nblk * 16, device=cuda)[:M].to(torch.int32)
+    slots[::7] = -1
+    cs = ops.rope_cos_sin(4096, D, 500000.0, device=cuda)
+    outs = []
+    for fused in (True, False):
+        q = torch.full((M, Hq, D), float("nan"), device=cuda, dtype=torch.bfloat16)
+        kc = torch.zeros(nblk, Hkv, 16, D, device=cuda, dtype=torch.bfloat16)
+        vc = torch.zeros(nblk, Hkv, D, 16, device=cuda, dtype=torch.bfloat16)
+        if fused:
+            assert ops.native().gemm_rope_kv(x, w, bias, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0,
+                                             torch.empty(0, device=cuda), False)
+        else:
+            qkv = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+            ops.native().gemm(x, w, qkv, bias, None, ops.EPI["bias"] if with_bias else 0, 0)
+            ops.rope_kv_write(qkv, pos, cs, slots, q, kc, vc, Hq, Hkv, D, True)
+        outs.append((q, kc, vc))
+    # same accumulators and roundings; hipcc may contract the rotation's mul-sub into an FMA differently at
+    # the two call sites, so a value that cancels to ~0 can differ in its last bit (as the decode test)
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-5)
+        assert (a != b).sum().item() <= max(2, a.numel() // 10000)
+    assert not torch.isnan(outs[0][0]).any()
+    assert outs[0][1].float().abs().sum() > 0 and outs[0][2].float().abs().sum() > 0  # caches written
