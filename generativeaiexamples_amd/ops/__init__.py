@@ -373,6 +373,8 @@ class GemmTuner:
     fused into gate_up (hipBLASLt needs a separate activation pass) the headline bench is within
     0.4-1.3 % of the library policy on the same box (15.09 vs 15.15 q/s; native / hipblaslt / native
     15.43 / 15.59 / 15.36 q/s, profiles/r2/policy_ab/); the gap is the deep-K down projection (0.93-0.95x).
+    Since then the prefill QKV GEMM also applies RoPE + the paged KV write in its epilogue (native
+    policies only, linear_rope_kv): +0.9 % on the headline (profiles/r2/prefill_rope_fused/).
     hipblaslt: library GEMMs for M > 64 (+ the framework's epilogue kernels). tune: per-shape choice
     between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
     Decode GEMMs at M = 64 vs hipBLASLt + epilogue kernel, weights streamed from HBM
