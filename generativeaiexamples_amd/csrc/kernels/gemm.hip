@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
 }
 
 // ----------------------------------------------------------------------------------------------
-// Part-ring variant of gemm_w4d_kernel (the default prefill GEMM for K >= 8192): the same full-line double units, but the A and B halves of a
+// Part-ring variant of gemm_w4d_kernel (the default prefill GEMM for K >= 8192 or N >= 16384): the same full-line double units, but the A and B halves of a
 // double are separate 32 KiB *parts* in a 5-part ring (160 KiB: all of the LDS), A(D), B(D), A(D+1), ...
 // Part q lives in slot q % 5. The A part of double D+2 is loaded during the even phase 2D (into the
 // slot B(D-1) left) and its B part during the odd phase 2D+1 (into the slot A(D) left), 8 loads per
@@ -1533,9 +1533,11 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
     if (force == 4) return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    // deep K (activations streamed from HBM, e.g. the MLP down projection): the part ring's longer
-    // A-operand latency cover wins (+7 %); otherwise the double-slot kernel (+2-4 %), gemm_w4r.jsonl
-    if (force == 10 || (force == 0 && K >= 8192)) return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
+    // part ring's longer A-operand latency cover wins (+7 % / +1-5 %); otherwise the double-slot kernel
+    // (+2-4 % on O / e5), profiles/r2/gemm_w4r.jsonl, gemm_rule.jsonl, gemm_w4p_ab.jsonl
+    if (force == 10 || (force == 0 && (K >= 8192 || N >= 16384)))
+      return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   }
   const bool large_ok = M >= 1024 && N >= 256;
