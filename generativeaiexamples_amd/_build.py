@@ -37,11 +37,29 @@ def _newest_header() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
+def _includes(src: Path, seen: set | None = None) -> set:
+    """Project headers a source includes, transitively (quoted includes found in csrc/include or next to it)."""
+    import re
+
+    seen = set() if seen is None else seen
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', src.read_text(errors="ignore"), re.M):
+        for d in (src.parent, CSRC / "include", CSRC / "runtime"):
+            h = d / name
+            if h.exists() and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+                break
+    return seen
+
+
 def _needs(obj: Path, src: Path, hdr_time: float) -> bool:
+    """Rebuild when the object is older than its source or than any project header it includes."""
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or hdr_time > t
+    if src.stat().st_mtime > t:
+        return True
+    return any(h.stat().st_mtime > t for h in _includes(src))
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

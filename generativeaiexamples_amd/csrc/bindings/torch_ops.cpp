@@ -193,7 +193,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
 }
 
 void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p, const Tensor& top_k,
-            const Tensor& seeds, int64_t step, Tensor& out) {
+            const Tensor& seeds, int64_t step, Tensor& out, const c10::optional<Tensor>& ws) {
   check_f32(logits, "logits");
   check_f32(temperature, "temperature");
   check_f32(top_p, "top_p");
@@ -202,9 +202,20 @@ void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p
   TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
   check_i32(out, "out");
   const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
+  void* wp = nullptr;
+  size_t wb = 0;
+  if (ws.has_value() && ws->defined()) {
+    check_dev(*ws, "sample workspace");
+    wp = ws->data_ptr();
+    wb = ws->numel() * ws->element_size();
+  }
   gai_sample(logits.data_ptr<float>(), B, V, logits.stride(0), temperature.data_ptr<float>(),
              top_p.data_ptr<float>(), top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), step, out.data_ptr<int>(),
-             cur_stream());
+             wp, wb, cur_stream());
+}
+
+int64_t sample_ws_bytes(int64_t B, int64_t V) { return (int64_t)gai_sample_ws_bytes((int)B, (int)V);
 }
 
 void apply_penalties(Tensor& logits, const Tensor& tok_ids, const Tensor& tok_cnt, const Tensor& n,
@@ -582,7 +593,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv) { return gai_attn_prefill_rows_per_tile(hq, hkv); });
   m.def("attn_decode", &attn_decode);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
+        py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none());
+  m.def("sample_ws_bytes", &sample_ws_bytes);
   m.def("apply_penalties", &apply_penalties);
   m.def("token_mask", &token_mask);
   m.def("sim_topk", &sim_topk);

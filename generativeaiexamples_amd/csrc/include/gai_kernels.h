@@ -70,8 +70,10 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                      float v_scale, hipStream_t st);
 
 // sampling.hip
+size_t gai_sample_ws_bytes(int B, int V);
 void gai_sample(const float* logits, int B, int V, long ld, const float* temperature, const float* top_p,
-                const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, hipStream_t st);
+                const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, void* ws, size_t ws_bytes,
+                hipStream_t st);
 void gai_token_mask(float* logits, long ld, int V, const int* rows, int R, const uint32_t* mask, int W,
                     hipStream_t st);
 void gai_apply_penalties(float* logits, int B, long ld, const int* tok_ids, const int* tok_cnt, const int* n,

@@ -292,59 +292,388 @@ __device__ bool nucleus_fast(const float* x, int V, float mx, float invT, float 
   return true;
 }
 
-__global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restrict__ logits, int V, long ld,
-                                                          const float* __restrict__ temperature,
-                                                          const float* __restrict__ top_p,
-                                                          const int* __restrict__ top_k,
-                                                          const int64_t* __restrict__ seeds, int64_t step,
-                                                          int* __restrict__ out_tokens) {
-  __shared__ float hist[256];
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  __shared__ float red[4];
-  __shared__ uint64_t cand[kCap];
-  __shared__ int cnt[2];
-  const int row = blockIdx.x;
-  const float* x = logits + (size_t)row * ld;
-  const float T = temperature[row];
+struct SampleSmem {
+  float hist[256];
+  float sv[16];
+  int si[16];
+  float red[4];
+  uint64_t cand[kCap];
+  int cnt[2];
+};
 
+// Whole-row sampler, one 1024-thread workgroup: argmax, then the nucleus fast path or the radix passes.
+__device__ void sample_row_full(const float* x, int V, float T, int k, float p, uint64_t seed, int64_t step,
+                                SampleSmem& sm, int* out) {
   ArgMax am{-INFINITY, 0x7fffffff};
   row_for_each(x, V, [&](float xv, int i) { am = argmax_merge(am, ArgMax{xv, i}); });
-  am = block_argmax(am, sv, si);
+  am = block_argmax(am, sm.sv, sm.si);
   if (T <= 0.f) {
-    if (threadIdx.x == 0) out_tokens[row] = am.i;
+    if (threadIdx.x == 0) *out = am.i;
     return;
   }
   const float mx = am.v, invT = 1.f / T;
-  {
-    const int k = top_k[row];
-    const float p = top_p[row];
-    if ((k <= 0 || k >= V) && p < 1.f &&
-        nucleus_fast(x, V, mx, invT, p, (uint64_t)seeds[row], step, sv, si, cand, cnt, out_tokens + row))
-      return;
-  }
+  if ((k <= 0 || k >= V) && p < 1.f && nucleus_fast(x, V, mx, invT, p, seed, step, sm.sv, sm.si, sm.cand, sm.cnt, out))
+    return;
   uint32_t floor_key = 0;
-  const int k = top_k[row];
-  if (k > 0 && k < V) floor_key = radix_select<false>(x, V, mx, invT, 0u, (float)k, hist, red);
-  const float p = top_p[row];
+  if (k > 0 && k < V) floor_key = radix_select<false>(x, V, mx, invT, 0u, (float)k, sm.hist, sm.red);
   if (p < 1.f) {
     float s = 0.f;
     for (int i = threadIdx.x; i < V; i += kThreads) {
       const float xv = x[i];
       if (fkey(xv) >= floor_key) s += __expf((xv - mx) * invT);
     }
-    s = block_sum(s, sv);
-    floor_key = radix_select<true>(x, V, mx, invT, floor_key, p * s, hist, red);
+    s = block_sum(s, sm.sv);
+    floor_key = radix_select<true>(x, V, mx, invT, floor_key, p * s, sm.hist, sm.red);
   }
-  const uint64_t seed = (uint64_t)seeds[row];
   ArgMax best{-INFINITY, 0x7fffffff};
   for (int i = threadIdx.x; i < V; i += kThreads) {
     const float xv = x[i];
     if (fkey(xv) < floor_key) continue;
     best = argmax_merge(best, ArgMax{(xv - mx) * invT + gumbel(seed, (uint64_t)step, (uint32_t)i), i});
   }
-  best = block_argmax(best, sv, si);
-  if (threadIdx.x == 0) out_tokens[row] = best.i < V ? best.i : am.i;
+  best = block_argmax(best, sm.sv, sm.si);
+  if (threadIdx.x == 0) *out = best.i < V ? best.i : am.i;
+}
+
+__global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restrict__ logits, int V, long ld,
+                                                          const float* __restrict__ temperature,
+                                                          const float* __restrict__ top_p,
+                                                          const int* __restrict__ top_k,
+                                                          const int64_t* __restrict__ seeds, int64_t step,
+                                                          int* __restrict__ out_tokens) {
+  __shared__ SampleSmem sm;
+  const int row = blockIdx.x;
+  sample_row_full(logits + (size_t)row * ld, V, temperature[row], top_k[row], top_p[row], (uint64_t)seeds[row], step,
+                  sm, out_tokens + row);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-row sampler (V >= kSplitMinV). One workgroup per row leaves 3/4 of the chip idle at batch 64 and
+// streams each 513 KB row through one CU (~125 us per decode step at B = 64, V = 128256). Here:
+//  1. split_stats   grid (S, B), 256 threads, kChunk logits per workgroup held in registers: chunk max,
+//                   argmax, sum exp((x - max) / T); for pure-temperature rows also the chunk's Gumbel-max.
+//  2. split_cands   grid (S, B): the row max M from the S partials, then every element of the chunk with
+//                   (M - x) / T < kCut (the same candidate set as nucleus_fast) compacted to global slots.
+//  3. resolve       grid B, 1024 threads: the row's softmax mass from the partials, the candidates in LDS,
+//                   count-radix top-k / mass-radix top-p cut on the candidates, Gumbel-max over the
+//                   survivors. Rows whose cut is not decidable on the candidates (top-k beyond them, a
+//                   nucleus reaching past kCut, > kSlot candidates in a chunk) take sample_row_full.
+// Same token as sample_kernel for a fixed (seed, step) up to float summation order at exact-cut ties.
+constexpr int kChunk = 8192;   // logits per split workgroup (32 per thread, 8 float4 registers)
+constexpr int kSplitT = 256;
+constexpr int kSlot = 256;     // candidate slots per chunk
+constexpr int kSplitMinV = 16384;
+constexpr int kPartW = 8;      // words per (row, split) partial: max, sum, argmax, gval, gidx, count
+
+__device__ __forceinline__ int nsplit(int V) { return (V + kChunk - 1) / kChunk; }
+
+__global__ __launch_bounds__(kSplitT) void sample_split_stats(const float* __restrict__ logits, int V, long ld,
+                                                              const float* __restrict__ temperature,
+                                                              const float* __restrict__ top_p,
+                                                              const int* __restrict__ top_k,
+                                                              const int64_t* __restrict__ seeds, int64_t step,
+                                                              float* __restrict__ part) {
+  __shared__ float sv[8];
+  __shared__ int si[8];
+  const int row = blockIdx.y, sp = blockIdx.x, S = gridDim.x, tid = threadIdx.x;
+  const int c0 = sp * kChunk;
+  const float* x = logits + (size_t)row * ld;
+  constexpr int U = kChunk / (4 * kSplitT);
+  float4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = c0 + 4 * (u * kSplitT + tid);
+    if (i + 3 < V) {
+      v[u] = *reinterpret_cast<const float4*>(x + i);
+    } else {
+      v[u].x = i < V ? x[i] : -INFINITY;
+      v[u].y = i + 1 < V ? x[i + 1] : -INFINITY;
+      v[u].z = i + 2 < V ? x[i + 2] : -INFINITY;
+      v[u].w = i + 3 < V ? x[i + 3] : -INFINITY;
+    }
+  }
+  ArgMax am{-INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = c0 + 4 * (u * kSplitT + tid);
+    am = argmax_merge(am, ArgMax{v[u].x, i});
+    am = argmax_merge(am, ArgMax{v[u].y, i + 1});
+    am = argmax_merge(am, ArgMax{v[u].z, i + 2});
+    am = argmax_merge(am, ArgMax{v[u].w, i + 3});
+  }
+  // workgroup argmax (4 waves)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = argmax_merge(am, ArgMax{__shfl_xor(am.v, o, 64), __shfl_xor(am.i, o, 64)});
+  if ((tid & 63) == 0) sv[tid >> 6] = am.v, si[tid >> 6] = am.i;
+  __syncthreads();
+  am = ArgMax{sv[0], si[0]};
+  for (int w = 1; w < kSplitT / 64; ++w) am = argmax_merge(am, ArgMax{sv[w], si[w]});
+  __syncthreads();
+  const float T = temperature[row];
+  float* pw = part + ((size_t)row * S + sp) * kPartW;
+  if (T <= 0.f) {
+    if (tid == 0) pw[0] = am.v, pw[2] = __int_as_float(am.i);
+    return;
+  }
+  const float m = am.v, invT = 1.f / T;
+  float s = 0.f;
+  if (m > -INFINITY) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      s += __expf((v[u].x - m) * invT) + __expf((v[u].y - m) * invT) + __expf((v[u].z - m) * invT) +
+           __expf((v[u].w - m) * invT);
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) sv[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kSplitT / 64; ++w) t += sv[w];
+    pw[0] = m, pw[1] = t, pw[2] = __int_as_float(am.i);
+  }
+  const int k = top_k[row];
+  if (top_p[row] < 1.f || (k > 0 && k < V)) return;
+  // pure temperature sampling: Gumbel-max over the whole row = max over chunks of x / T + G_i
+  __syncthreads();
+  const uint64_t seed = (uint64_t)seeds[row];
+  ArgMax g{-INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = c0 + 4 * (u * kSplitT + tid);
+    const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i + q < V && e[q] > -INFINITY)
+        g = argmax_merge(g, ArgMax{(e[q] - m) * invT + gumbel(seed, (uint64_t)step, (uint32_t)(i + q)), i + q});
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) g = argmax_merge(g, ArgMax{__shfl_xor(g.v, o, 64), __shfl_xor(g.i, o, 64)});
+  if ((tid & 63) == 0) sv[tid >> 6] = g.v, si[tid >> 6] = g.i;
+  __syncthreads();
+  if (tid == 0) {
+    g = ArgMax{sv[0], si[0]};
+    for (int w = 1; w < kSplitT / 64; ++w) g = argmax_merge(g, ArgMax{sv[w], si[w]});
+    pw[3] = g.v + m * invT;  // comparable across chunks: x / T + G
+    pw[4] = __int_as_float(g.i);
+  }
+}
+
+__device__ __forceinline__ bool split_needs_cands(float T, float p, int k, int V) {
+  return T > 0.f && (p < 1.f || (k > 0 && k < V));
+}
+
+__global__ __launch_bounds__(kSplitT) void sample_split_cands(const float* __restrict__ logits, int V, long ld,
+                                                              const float* __restrict__ temperature,
+                                                              const float* __restrict__ top_p,
+                                                              const int* __restrict__ top_k,
+                                                              float* __restrict__ part,
+                                                              uint64_t* __restrict__ cands) {
+  __shared__ int cnt;
+  const int row = blockIdx.y, sp = blockIdx.x, S = gridDim.x, tid = threadIdx.x, lane = tid & 63;
+  const float T = temperature[row];
+  if (!split_needs_cands(T, top_p[row], top_k[row], V)) return;
+  const float* pr = part + (size_t)row * S * kPartW;
+  float M = -INFINITY;
+  for (int j = 0; j < S; ++j) M = fmaxf(M, pr[j * kPartW]);
+  const float invT = 1.f / T;
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  const int c0 = sp * kChunk;
+  const float* x = logits + (size_t)row * ld;
+  uint64_t* out = cands + ((size_t)row * S + sp) * kSlot;
+  constexpr int U = kChunk / (4 * kSplitT);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = c0 + 4 * (u * kSplitT + tid);
+    float4 v;
+    if (i + 3 < V) {
+      v = *reinterpret_cast<const float4*>(x + i);
+    } else {
+      v.x = i < V ? x[i] : -INFINITY;
+      v.y = i + 1 < V ? x[i + 1] : -INFINITY;
+      v.z = i + 2 < V ? x[i + 2] : -INFINITY;
+      v.w = i + 3 < V ? x[i + 3] : -INFINITY;
+    }
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool c = e[q] > -INFINITY && (M - e[q]) * invT < kCut;
+      const unsigned long long msk = __ballot(c);
+      if (msk == 0) continue;
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&cnt, __popcll(msk));
+      base = __shfl(base, 0, 64);
+      const int pos = base + __popcll(msk & ((1ull << lane) - 1ull));
+      if (c && pos < kSlot) out[pos] = ((uint64_t)fkey(e[q]) << 32) | (uint32_t)(i + q);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) part[((size_t)row * S + sp) * kPartW + 5] = __int_as_float(cnt);
+}
+
+// radix_select over the LDS candidate list (keys in the high words)
+template <bool MASS>
+__device__ uint32_t radix_select_cands(const uint64_t* cand, int n, float mx, float invT, uint32_t floor_key,
+                                       float target, float* hist, float* red) {
+  uint32_t prefix = 0;
+  float remaining = target;
+#pragma unroll 1
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int b = threadIdx.x; b < 256; b += kThreads) hist[b] = 0.f;
+    __syncthreads();
+    const uint32_t hi_mask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    for (int j = threadIdx.x; j < n; j += kThreads) {
+      const uint32_t kk = (uint32_t)(cand[j] >> 32);
+      if (kk < floor_key || (kk & hi_mask) != prefix) continue;
+      const float w = MASS ? __expf((key_to_float(kk) - mx) * invT) : 1.f;
+      atomicAdd(&hist[(kk >> shift) & 255], w);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x;
+      float loc[4];
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        loc[j] = hist[255 - (4 * l + j)];
+        s += loc[j];
+      }
+      float incl = s;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(incl, o, 64);
+        if (l >= o) incl += t;
+      }
+      float run = incl - s;
+      int found = -1;
+      float above = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (found < 0 && run + loc[j] >= remaining) {
+          found = 255 - (4 * l + j);
+          above = run;
+        }
+        run += loc[j];
+      }
+      const unsigned long long hit = __ballot(found >= 0);
+      int src = hit ? __ffsll((long long)hit) - 1 : 63;
+      const int fb = __shfl(found, src, 64);
+      const float ab = __shfl(above, src, 64);
+      if (l == 0) {
+        red[0] = hit ? (float)fb : 0.f;
+        red[1] = hit ? ab : 0.f;
+      }
+    }
+    __syncthreads();
+    const int b = (int)red[0];
+    remaining -= red[1];
+    prefix |= ((uint32_t)b) << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __restrict__ logits, int V, long ld,
+                                                                 const float* __restrict__ temperature,
+                                                                 const float* __restrict__ top_p,
+                                                                 const int* __restrict__ top_k,
+                                                                 const int64_t* __restrict__ seeds, int64_t step,
+                                                                 const float* __restrict__ part,
+                                                                 const uint64_t* __restrict__ cands, int S,
+                                                                 int* __restrict__ out_tokens) {
+  __shared__ SampleSmem sm;
+  __shared__ int offs[129];
+  __shared__ int flag;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float T = temperature[row];
+  const int k = top_k[row];
+  const float p = top_p[row];
+  const uint64_t seed = (uint64_t)seeds[row];
+  const float* pr = part + (size_t)row * S * kPartW;
+  // row max / argmax from the partials (first index among equal maxima, as the whole-row kernel)
+  ArgMax am{-INFINITY, 0x7fffffff};
+  for (int j = 0; j < S; ++j) am = argmax_merge(am, ArgMax{pr[j * kPartW], __float_as_int(pr[j * kPartW + 2])});
+  if (T <= 0.f) {
+    if (tid == 0) out_tokens[row] = am.i;
+    return;
+  }
+  const float M = am.v, invT = 1.f / T;
+  if (!split_needs_cands(T, p, k, V)) {
+    ArgMax g{-INFINITY, 0x7fffffff};
+    for (int j = 0; j < S; ++j) g = argmax_merge(g, ArgMax{pr[j * kPartW + 3], __float_as_int(pr[j * kPartW + 4])});
+    if (tid == 0) out_tokens[row] = g.i < V ? g.i : am.i;
+    return;
+  }
+  // candidate list: per-chunk counts -> offsets (S <= 128 chunks)
+  if (tid == 0) {
+    int o = 0, bad = S > 128;
+    for (int j = 0; j < S && !bad; ++j) {
+      const int c = __float_as_int(pr[j * kPartW + 5]);
+      if (c > kSlot) bad = 1;
+      offs[j] = o;
+      o += c;
+    }
+    offs[S < 128 ? S : 128] = o;
+    flag = bad || o > kCap;
+  }
+  __syncthreads();
+  if (flag) {
+    sample_row_full(logits + (size_t)row * ld, V, T, k, p, seed, step, sm, out_tokens + row);
+    return;
+  }
+  const int n = offs[S];
+  for (int j = 0; j < S; ++j) {
+    const int c = offs[j + 1] - offs[j];
+    for (int q = tid; q < c; q += kThreads) sm.cand[offs[j] + q] = cands[((size_t)row * S + j) * kSlot + q];
+  }
+  __syncthreads();
+  uint32_t floor_key = 0;
+  int fallback = 0;
+  if (k > 0 && k < V) {
+    if (n < k) fallback = 1;  // the k-th largest lies outside the candidates
+    else floor_key = radix_select_cands<false>(sm.cand, n, M, invT, 0u, (float)k, sm.hist, sm.red);
+  }
+  if (!fallback && p < 1.f) {
+    float total = 0.f;
+    if (k > 0 && k < V) {  // mass of the top-k set (all candidates)
+      float s = 0.f;
+      for (int j = tid; j < n; j += kThreads) {
+        const uint32_t kk = (uint32_t)(sm.cand[j] >> 32);
+        if (kk >= floor_key) s += __expf((key_to_float(kk) - M) * invT);
+      }
+      total = block_sum(s, sm.sv);
+    } else {
+      for (int j = 0; j < S; ++j) {
+        const float mj = pr[j * kPartW];
+        if (mj > -INFINITY) total += pr[j * kPartW + 1] * __expf((mj - M) * invT);
+      }
+    }
+    // the candidates must hold >= p of the mass, else the nucleus reaches past kCut
+    float s = 0.f;
+    for (int j = tid; j < n; j += kThreads) {
+      const uint32_t kk = (uint32_t)(sm.cand[j] >> 32);
+      if (kk >= floor_key) s += __expf((key_to_float(kk) - M) * invT);
+    }
+    s = block_sum(s, sm.sv);
+    if (s < p * total) fallback = 1;
+    else floor_key = radix_select_cands<true>(sm.cand, n, M, invT, floor_key, p * total, sm.hist, sm.red);
+  }
+  if (fallback) {
+    __syncthreads();
+    sample_row_full(logits + (size_t)row * ld, V, T, k, p, seed, step, sm, out_tokens + row);
+    return;
+  }
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int j = tid; j < n; j += kThreads) {
+    const uint64_t e = sm.cand[j];
+    const uint32_t kk = (uint32_t)(e >> 32);
+    if (kk < floor_key) continue;
+    const uint32_t idx = (uint32_t)e;
+    best = argmax_merge(best, ArgMax{(key_to_float(kk) - M) * invT + gumbel(seed, (uint64_t)step, idx), (int)idx});
+  }
+  best = block_argmax(best, sm.sv, sm.si);
+  if (tid == 0) out_tokens[row] = best.i < V ? best.i : am.i;
 }
 
 // logits[b, t] -= freq * count + presence * (count > 0) for the tokens generated so far.
@@ -390,10 +719,32 @@ void gai_token_mask(float* logits, long ld, int V, const int* rows, int R, const
   GAI_LAUNCH_CHECK();
 }
 
+size_t gai_sample_ws_bytes(int B, int V) {
+  if (V < kSplitMinV) return 0;
+  const size_t S = (size_t)((V + kChunk - 1) / kChunk);
+  return (size_t)B * S * (kPartW * sizeof(float) + kSlot * sizeof(uint64_t));
+}
+
 void gai_sample(const float* logits, int B, int V, long ld, const float* temperature, const float* top_p,
-                const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, hipStream_t st) {
+                const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens, void* ws, size_t ws_bytes,
+                hipStream_t st) {
   if (B == 0) return;
-  sample_kernel<<<B, kThreads, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, out_tokens);
+  const size_t need = gai_sample_ws_bytes(B, V);
+  const int S = (V + kChunk - 1) / kChunk;
+  if (need == 0 || ws == nullptr || ws_bytes < need || S > 128 || (ld & 3) ||
+      (reinterpret_cast<uintptr_t>(logits) & 15)) {
+    sample_kernel<<<B, kThreads, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, out_tokens);
+    GAI_LAUNCH_CHECK();
+    return;
+  }
+  uint64_t* cands = reinterpret_cast<uint64_t*>(ws);
+  float* part = reinterpret_cast<float*>(cands + (size_t)B * S * kSlot);
+  sample_split_stats<<<dim3(S, B), kSplitT, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part);
+  GAI_LAUNCH_CHECK();
+  sample_split_cands<<<dim3(S, B), kSplitT, 0, st>>>(logits, V, ld, temperature, top_p, top_k, part, cands);
+  GAI_LAUNCH_CHECK();
+  sample_split_resolve<<<B, kThreads, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part, cands,
+                                               S, out_tokens);
   GAI_LAUNCH_CHECK();
 }
 

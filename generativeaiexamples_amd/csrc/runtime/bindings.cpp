@@ -112,7 +112,17 @@ PYBIND11_MODULE(_rt, m) {
            },
            py::arg("ids"), py::arg("steps"),
            "reserve KV pages for a multi-step decode run; [len(ids), max_blocks] int32 block tables or None")
-      .def("advance_decode", &Scheduler::advance_decode, py::arg("ids"), py::arg("toks"), py::arg("steps"))
+      .def("reserve_upto",
+           [](Scheduler& s, const std::vector<int64_t>& ids, const std::vector<int>& upto) -> py::object {
+             std::vector<int32_t> bt;
+             int mb = 0;
+             if (!s.reserve_upto(ids, upto, bt, mb)) return py::none();
+             return arr2(bt, mb);
+           },
+           py::arg("ids"), py::arg("upto"),
+           "own the KV pages of the first upto[i] positions of each sequence; block tables or None")
+      .def("advance_decode", &Scheduler::advance_decode, py::arg("ids"), py::arg("toks"), py::arg("steps"),
+           py::arg("chained") = false)
       .def("num_waiting", &Scheduler::num_waiting)
       .def("num_running", &Scheduler::num_running)
       .def("num_free_blocks", &Scheduler::num_free_blocks)

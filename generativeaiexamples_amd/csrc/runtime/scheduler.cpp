@@ -233,14 +233,39 @@ bool Scheduler::reserve_decode(const std::vector<int64_t>& ids, int steps, std::
   return true;
 }
 
-void Scheduler::advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps) {
+bool Scheduler::reserve_upto(const std::vector<int64_t>& ids, const std::vector<int>& upto,
+                             std::vector<int32_t>& block_tables, int& max_blocks) {
+  if (upto.size() != ids.size()) throw std::runtime_error("reserve_upto: size mismatch");
+  int need = 0;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    auto it = seqs_.find(ids[i]);
+    if (it == seqs_.end()) throw std::runtime_error("reserve_upto: unknown sequence");
+    if (upto[i] > max_model_len_) return false;
+    need += std::max(0, (upto[i] + kBlockSize - 1) / kBlockSize - (int)it->second->blocks.size());
+  }
+  if (need > 0 && !bm_.can_allocate(need)) return false;
+  max_blocks = 1;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    Sequence& s = *seqs_[ids[i]];
+    ensure_blocks(s, upto[i]);
+    max_blocks = std::max(max_blocks, (int)s.blocks.size());
+  }
+  block_tables.assign(ids.size() * (size_t)max_blocks, 0);
+  for (size_t i = 0; i < ids.size(); ++i) {
+    const Sequence& s = *seqs_[ids[i]];
+    std::copy(s.blocks.begin(), s.blocks.end(), block_tables.begin() + i * (size_t)max_blocks);
+  }
+  return true;
+}
+
+void Scheduler::advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps, bool chained) {
   if (toks.size() != ids.size() * (size_t)steps) throw std::runtime_error("advance_decode: size mismatch");
   for (size_t i = 0; i < ids.size(); ++i) {
     auto it = seqs_.find(ids[i]);
     if (it == seqs_.end()) continue;  // finished / aborted during the run
     Sequence& s = *it->second;
     s.tokens.insert(s.tokens.end(), toks.begin() + i * steps, toks.begin() + (i + 1) * steps);
-    s.num_computed += steps - 1;
+    s.num_computed += chained ? steps : steps - 1;
     if ((int)s.blocks.size() * kBlockSize < s.num_computed)
       throw std::runtime_error("advance_decode: sequence advanced past its reserved pages");
     commit_full_blocks(s);

@@ -74,7 +74,14 @@ class Scheduler {
                       int& max_blocks);
   // After such a run: appends `steps` sampled tokens per id (toks is [ids.size(), steps] row-major)
   // and marks steps-1 more of them as computed (the last sampled token is the next step's input).
-  void advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps);
+  // chained = the run's first input was the previous run's last token, fed on the device (pipelined
+  // runs, LLMEngine): that token was not scheduled by schedule(), so all `steps` positions are computed.
+  void advance_decode(const std::vector<int64_t>& ids, const std::vector<int>& toks, int steps, bool chained = false);
+  // Pipelined multi-step decode: make every sequence ids[i] own the KV pages of its first upto[i] token
+  // positions (absolute counts, <= max_model_len), all-or-nothing, and fill the block tables as
+  // reserve_decode does. Used to reserve run r+1 while run r is still executing on the device.
+  bool reserve_upto(const std::vector<int64_t>& ids, const std::vector<int>& upto, std::vector<int32_t>& block_tables,
+                    int& max_blocks);
 
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }

@@ -239,6 +239,14 @@ class Guide:
 
         return _rt.Matcher(self.grammar)
 
+    @property
+    def min_tokens(self) -> int:
+        """Token budget below which a request cannot be guaranteed to close its value: the mask walk counts
+        one character per remaining token, so the shortest completion needs this many tokens."""
+        if not hasattr(self, "_min_tokens"):
+            self._min_tokens = int(self.matcher().min_chars) + 1  # + the end-of-sequence token
+        return self._min_tokens
+
     @classmethod
     def _get(cls, key, build):
         with _LOCK:

@@ -90,6 +90,7 @@ class Request:
     lora_slot: int = 0
     max_new: int = 0
     matcher: Any = None  # constrained decoding (engine/guided.py): this request's grammar state
+    mask_empty: bool = False  # the grammar allows no token within the remaining budget
 
     @property
     def text(self) -> str:
@@ -109,6 +110,19 @@ class RequestOutput:
     finish_reason: Optional[str] = None
 
 
+@dataclass
+class _Run:
+    """A K-step decode graph run enqueued on the device whose sampled tokens are not processed yet."""
+    ids: List[int]            # sequence ids in row order
+    reqs: List[Request]
+    K: int
+    n: int
+    chained: bool             # first input fed on the device from the previous run's last token
+    base: List[int]           # absolute position of each row's first input token
+    host: Any                 # [K, bucket] int32 tokens (pinned; valid once `done` has completed)
+    done: Any = None          # device event after the tokens' D2H copy (None: already synchronous)
+
+
 class LLMEngine:
     def __init__(self, model, tokenizer: Tokenizer, cfg: EngineConfig | None = None):
         self.model, self.tok = model, tokenizer
@@ -117,8 +131,6 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
-        if self.device.type == "cuda" and ops.TUNER.mode in ("tune", "hipblaslt"):
-            ops.enable_tuned_blas()  # the prefill library GEMMs (GAI_GEMM_POLICY=tune|hipblaslt)
         if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
@@ -153,7 +165,13 @@ class LLMEngine:
                                                  mc.head_dim, max(cfg.max_model_len,
                                                                   getattr(model, "max_cross_tokens", 0)),
                                                  self.device)
-        self.stager = HostStager(self.device)
+        # two staging banks used by alternate launches: a pipelined run's H2D copies may still be queued
+        # behind the run in flight when the host stages the next one (HostStager.reset waits on the fence)
+        self.stagers = [HostStager(self.device), HostStager(self.device)]
+        self.stager = self.stagers[0]
+        self._pending: Optional[_Run] = None  # multi-step run enqueued, tokens not processed yet
+        self._launches = 0
+        self._tok_host = None  # 2 pinned [K * max bucket] int32 token buffers (alternate launches)
         self._masks = None  # guided-decoding mask builder (lazy)
         self._timing = os.environ.get("GAI_STEP_TIMING") == "1"
         self.phase_ms: Dict[str, float] = {}
@@ -165,7 +183,8 @@ class LLMEngine:
         self.graphs: Dict[int, tuple] = {}
         self.multi_graphs: Dict[int, tuple] = {}
         self.lock = threading.RLock()
-        self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0, multi_step_runs=0)
+        self.stats = dict(prefill_tokens=0, decode_tokens=0, steps=0, graph_steps=0, multi_step_runs=0,
+                          chained_runs=0)
         self.eos = set(mc.eos_token_ids) | set(getattr(tokenizer, "eos_ids", ()) or ())
         self.chan = None
         if self.tp_size > 1:
@@ -262,7 +281,7 @@ class LLMEngine:
             self.model.release_request(sid)
 
     def has_work(self) -> bool:
-        return self.sched.has_work()
+        return self._pending is not None or self.sched.has_work()
 
     # ------------------------------------------------------------------ batch construction
     def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
@@ -411,12 +430,13 @@ class LLMEngine:
                           decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
 
         def run():
+            # every step first advances rows < n_valid from the previous sampled token: at j = 0 that is
+            # toks[K-1], the last token of the previous run (pipelined) or the host-fed input token
             for j in range(K):
+                ops.decode_advance(toks[(j - 1) % K], ids, pos, ctx, slots, bt, n_valid)
                 logits = self.model.forward(fb, self.kv, self.decode_ws)
                 ops.sample(logits, samp["temperature"], samp["top_p"], samp["top_k"], samp["seeds"], j,
                            out=toks[j])
-                if j + 1 < K:
-                    ops.decode_advance(toks[j], ids, pos, ctx, slots, bt, n_valid)
 
         g = None
         if d.type == "cuda" and self.cfg.use_graphs:
@@ -430,6 +450,13 @@ class LLMEngine:
                 run()
         self.multi_graphs[bs] = (g, run, fb, samp, n_valid, toks)
 
+    def _worth_multi(self, reqs, extra: int = 0) -> bool:
+        """A K-step run pays off when some row still needs >= 3K/4 tokens (rows that finish inside the run
+        compute discarded tokens; a nearly-finished batch is cheaper as single steps). ``extra``: tokens
+        per row already sampled by unprocessed runs."""
+        K = self.cfg.decode_steps
+        return max(r.max_new - len(r.output_ids) - extra for r in reqs) >= (3 * K) // 4
+
     def _multi_steps_for(self, b, reqs) -> int:
         """K if this pure-decode batch can run a K-step graph, else 1."""
         K = self.cfg.decode_steps
@@ -441,10 +468,14 @@ class LLMEngine:
         for r in reqs:
             if r is None or r.finished or r.params.has_penalty or r.params.guided is not None:
                 return 1
-            n = len(r.output_ids)
-            if r.params.max_tokens - n < K or len(r.prompt_ids) + n + K > lim:
+            if len(r.prompt_ids) + len(r.output_ids) + K > lim:
                 return 1
-        return K
+        return K if self._worth_multi(reqs) else 1
+
+    def _run_seeds(self, reqs) -> np.ndarray:
+        # per-run seed stream: the graph bakes the in-run step index, the host mixes in the engine step
+        return (np.asarray([r.seed for r in reqs], np.int64) * np.int64(0x9E3779B1)
+                + np.int64(self.step_count) * np.int64(0x632BE5AB)) & np.int64(0x7FFFFFFFFFFFFFFF)
 
     def _plan_multi(self, b, reqs, K: int) -> Optional[dict]:
         ids_list = list(b.decode_seq_ids)
@@ -456,63 +487,131 @@ class LLMEngine:
         temp = np.fromiter((0.0 if p.top_k == 1 else p.temperature for p in params), np.float32, n)
         top_p = np.fromiter((p.top_p for p in params), np.float32, n)
         top_k = np.fromiter((p.top_k for p in params), np.int32, n)
-        # per-run seed stream: the graph bakes the in-run step index, the host mixes in the engine step
-        seeds = (np.asarray([r.seed for r in reqs], np.int64) * np.int64(0x9E3779B1)
-                 + np.int64(self.step_count) * np.int64(0x632BE5AB)) & np.int64(0x7FFFFFFFFFFFFFFF)
-        return dict(op="multi", K=int(K), n=n, arr=[b.token_ids, b.positions, b.slots, b.decode_ctx, bt_np, temp,
-                                                     top_p, top_k, seeds, np.asarray([n], np.int32)])
+        # host-fed first run: the graph's leading decode_advance moves (token, position - 1) to the input row
+        return dict(op="multi", K=int(K), n=n, chained=False,
+                    arr=[b.token_ids, np.asarray(b.positions, np.int32) - 1, bt_np, temp, top_p, top_k,
+                         self._run_seeds(reqs), np.asarray([n], np.int32)])
 
-    def _exec_multi(self, plan: dict) -> Optional[np.ndarray]:
-        """Run a K-step decode graph from a plan; the leader gets the sampled tokens [K, n] back."""
+    def _bank(self) -> HostStager:
+        """Switch to the other staging bank for this launch (waits for that bank's previous copies)."""
+        self._launches += 1
+        self.stager = self.stagers[self._launches & 1]
+        self.stager.reset()
+        return self.stager
+
+    def _exec_multi(self, plan: dict) -> Optional[tuple]:
+        """Enqueue a K-step decode graph run from a plan (no host sync). The leader gets (host token
+        buffer [K, bucket], completion event) back; followers None."""
         n, K = plan["n"], plan["K"]
         bs = self._graph_bucket(n)
         if bs not in self.multi_graphs:
             self._capture_multi(bs)
         g, run, fb, samp, n_valid, toks = self.multi_graphs[bs]
+        st = self._bank()
         src = self._to_device(plan["arr"])
-        fb.token_ids[:n].copy_(src[0])
-        fb.positions[:n].copy_(src[1])
-        fb.slots[:n].copy_(src[2])
-        fb.decode_ctx[:n].copy_(src[3])
-        mb = plan["arr"][4].shape[1]
-        fb.decode_block_tables[:n, :mb].copy_(src[4])
-        if n < bs:
-            fb.token_ids[n:].zero_()
-            fb.positions[n:].zero_()
-            fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
-            fb.decode_ctx[n:].fill_(1)
-            fb.decode_block_tables[n:, 0].fill_(self.pad_block)
-        samp["temperature"][:n].copy_(src[5])
-        samp["top_p"][:n].copy_(src[6])
-        samp["top_k"][:n].copy_(src[7])
-        samp["seeds"][:n].copy_(src[8])
-        n_valid.copy_(src[9])
+        if plan["chained"]:  # inputs are already on the device: new page tables and seeds only
+            bt, seeds = src
+            fb.decode_block_tables[:n, :bt.shape[1]].copy_(bt)
+            samp["seeds"][:n].copy_(seeds)
+        else:
+            toks[K - 1, :n].copy_(src[0])
+            fb.positions[:n].copy_(src[1])
+            mb = plan["arr"][2].shape[1]
+            fb.decode_block_tables[:n, :mb].copy_(src[2])
+            if n < bs:
+                fb.token_ids[n:].zero_()
+                fb.positions[n:].zero_()
+                fb.slots[n:].fill_(self.pad_block * ops.BLOCK)
+                fb.decode_ctx[n:].fill_(1)
+                fb.decode_block_tables[n:, 0].fill_(self.pad_block)
+            samp["temperature"][:n].copy_(src[3])
+            samp["top_p"][:n].copy_(src[4])
+            samp["top_k"][:n].copy_(src[5])
+            samp["seeds"][:n].copy_(src[6])
+            n_valid.copy_(src[7])
         if g is not None:
             g.replay()
             self.stats["graph_steps"] += K
         else:
             run()  # eager (CPU / graphs off): same device-side feedback, no host round trip per token
         self.stats["multi_step_runs"] += 1
-        host = toks[:, :n].cpu().numpy() if self.leader else None  # [K, n]
+        out = None
+        if self.leader:
+            if self.device.type == "cuda":
+                if self._tok_host is None:
+                    cap = K * max(self.cfg.graph_batch_sizes)
+                    self._tok_host = [torch.empty(cap, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+                buf = self._tok_host[self._launches & 1][:K * bs].view(K, bs)
+                buf.copy_(toks, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                out = (buf.numpy(), ev)
+            else:
+                out = (toks.clone().numpy(), None)
+        st.fence()
         self._step_done()
-        return host
+        return out
 
-    def _finish_multi(self, b, reqs, K: int, host: np.ndarray) -> List[RequestOutput]:
-        ids_list = list(b.decode_seq_ids)
-        n = len(ids_list)
+    def _launch_multi(self, b, reqs, K: int) -> bool:
+        plan = self._plan_multi(b, reqs, K)
+        if plan is None:
+            return False
         self.step_count += K - 1
-        self.stats["decode_tokens"] += n * (K - 1)
+        self.stats["decode_tokens"] += plan["n"] * (K - 1)
+        self._publish(plan)
+        with roctx_range("decode_multi"):
+            host, ev = self._exec_multi(plan)
+        base = [int(p) for p in b.positions]
+        self._pending = _Run([int(x) for x in b.decode_seq_ids], reqs, K, plan["n"], False, base, host, ev)
+        return True
+
+    def _chain(self, run: _Run) -> Optional[_Run]:
+        """Enqueue run r+1 of a pending run r (before r's tokens are read), or None when the batch should
+        go back to the scheduler: requests waiting, the bucket shrank, too few tokens left, no KV pages."""
+        if self.sched.num_waiting() > 0:
+            return None
+        alive = [i for i, r in enumerate(run.reqs) if not r.finished]
+        if not alive or self._graph_bucket(len(alive)) != self._graph_bucket(run.n):
+            return None
+        K = run.K
+        if not self._worth_multi([run.reqs[i] for i in alive], extra=K):
+            return None
+        base = [p + K for p in run.base]
+        if max(base) + K > self.cfg.max_model_len:  # every row, finished ones included (page-table width)
+            return None
+        bt = self.sched.reserve_upto([run.ids[i] for i in alive], [base[i] + K for i in alive])
+        if bt is None:
+            return None
+        full = np.full((run.n, bt.shape[1]), self.pad_block, np.int32)  # finished rows: scratch page
+        full[alive] = bt
+        self.step_count += K
+        self.stats["steps"] += 1
+        self.stats["chained_runs"] += 1
+        self.stats["decode_tokens"] += len(alive) * K
+        plan = dict(op="multi", K=K, n=run.n, chained=True,
+                    arr=[full, self._run_seeds(run.reqs)])
+        self._publish(plan)
+        with roctx_range("decode_multi"):
+            host, ev = self._exec_multi(plan)
+        return _Run(run.ids, run.reqs, K, run.n, True, base, host, ev)
+
+    def _complete(self, run: _Run) -> List[RequestOutput]:
+        """Wait for a run's tokens and apply them (stop conditions, detokenisation, scheduler state)."""
+        if run.done is not None:
+            run.done.synchronize()
         self._mark("forward")
+        host = run.host[:, :run.n]
         outs: List[RequestOutput] = []
-        alive = list(range(n))
-        for j in range(K):
-            outs += self._process([ids_list[i] for i in alive], [reqs[i] for i in alive],
-                                  host[j, alive].tolist(), defer_append=True)
-            alive = [i for i in alive if not reqs[i].finished]
+        alive = [i for i in range(run.n) if not run.reqs[i].finished]
+        for j in range(run.K):
             if not alive:
                 break
+            outs += self._process([run.ids[i] for i in alive], [run.reqs[i] for i in alive],
+                                  host[j, alive].tolist(), defer_append=True)
+            alive = [i for i in alive if not run.reqs[i].finished]
         if alive:
-            self.sched.advance_decode([ids_list[i] for i in alive], host[:, alive].T.reshape(-1).tolist(), K)
+            self.sched.advance_decode([run.ids[i] for i in alive], host[:, alive].T.reshape(-1).tolist(), run.K,
+                                      run.chained)
         self._mark("process")
         return outs
 
@@ -538,6 +637,7 @@ class LLMEngine:
     def _exec_single(self, plan: dict, reqs=None) -> Optional[List[int]]:
         """Forward of a one-token step on this rank; the leader also samples (followers need no tokens:
         the next plan carries them)."""
+        st = self._bank()
         if plan["op"] == "graph":
             logits = self._run_graph(plan)
         else:
@@ -555,6 +655,7 @@ class LLMEngine:
             t = ops.sample(logits, temp, top_p, top_k, seeds, plan["step"])
             self._mark("sample")
             toks = t.cpu().tolist()
+        st.fence()
         self._step_done()
         return toks
 
@@ -593,8 +694,12 @@ class LLMEngine:
         with self.lock:
             if self._timing:
                 self._t_mark = time.perf_counter()
+            if self._pending is not None:
+                # pipelined decode: enqueue run r+1, then process run r while r+1 executes
+                run = self._pending
+                self._pending = self._chain(run)
+                return self._complete(run)
             b = self.sched.schedule()
-            self.stager.reset()  # the previous step ended with a sync on its sampled tokens
             self._mark("schedule")
             n_tok = b.num_tokens
             if n_tok == 0:
@@ -608,13 +713,8 @@ class LLMEngine:
             if P == 0 and nd and self.cfg.decode_steps > 1:
                 dreqs = [self.requests.get(s) for s in b.decode_seq_ids]
                 K = self._multi_steps_for(b, dreqs)
-                if K > 1:
-                    plan = self._plan_multi(b, dreqs, K)
-                    if plan is not None:
-                        self._publish(plan)
-                        with roctx_range("decode_multi"):
-                            host = self._exec_multi(plan)
-                        return self._finish_multi(b, dreqs, K, host)
+                if K > 1 and self._launch_multi(b, dreqs, K):
+                    return []  # its tokens are processed by the next step(), after run 2 is enqueued
             plan, seq_order, reqs = self._plan_single(b)
             self._publish(plan)
             with roctx_range("prefill" if P else "decode"):
@@ -637,7 +737,6 @@ class LLMEngine:
             op = plan["op"]
             if op in ("yield", "stop"):
                 return op
-            self.stager.reset()
             if op == "multi":
                 self._exec_multi(plan)
             elif op in ("graph", "eager"):
@@ -701,6 +800,10 @@ class LLMEngine:
         if gw < words:  # logits wider than the tokenizer's vocabulary: the extra ids stay disallowed
             mask = np.concatenate([mask, np.zeros((len(rows), words - gw), np.int32)], 1)
         mask = np.ascontiguousarray(mask[:, :words])
+        for j, i in enumerate(rows):  # nothing allowed (budget exhausted): the request ends, its sample is dropped
+            if not mask[j].any():
+                reqs[i].mask_empty = True
+                mask[j] = -1
         ops.token_mask(logits, *self._to_device([np.asarray(rows, np.int32), mask]))
 
     def _process(self, seq_order, reqs, toks, defer_append: bool = False) -> List[RequestOutput]:
@@ -714,6 +817,14 @@ class LLMEngine:
                 continue
             if req.first_token_time is None:
                 req.first_token_time = now
+            if req.mask_empty:  # no token was allowed: finish without the (meaningless) sample
+                req.finished, req.finish_reason, req.finish_time = True, "length", now
+                self.sched.finish(sid)
+                self.requests.pop(sid, None)
+                self._release(sid)
+                self.by_rid.pop(req.request_id, None)
+                outs.append(RequestOutput(req.request_id, -1, req.detok.flush(), True, "length"))
+                continue
             req.output_ids.append(t)
             if req.params.has_penalty:
                 req.token_counts[t] = req.token_counts.get(t, 0) + 1

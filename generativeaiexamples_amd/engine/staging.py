@@ -5,8 +5,11 @@ sampling parameters) to the GPU. Allocating pinned memory per step (``tensor.pin
 host time on every decode step; instead one persistent pinned int32 buffer and one device buffer are
 reused: ``stage`` bump-allocates regions of them within a step (8-byte aligned, so int64/fp32 arrays
 can be reinterpreted), packs the arrays with numpy and issues ONE async H2D copy per call.
-``reset()`` at the start of a step recycles the regions - safe because the engine synchronises on
-the sampled tokens at the end of every step, so no copy from the previous step is still in flight.
+``reset()`` recycles the regions once the copies issued since the last ``fence()`` have executed
+(the engine alternates two stagers between launches, so a pipelined run's copies can still be queued
+behind the run in flight while the other bank is filled). A step that stages more than the capacity
+gets an extra region for the rest of that step (regions already in flight never move); the next
+``reset()`` folds the extra size into one larger buffer.
 """
 from __future__ import annotations
 
@@ -20,6 +23,9 @@ class HostStager:
     def __init__(self, device, capacity: int = 1 << 18):
         self.device = torch.device(device)
         self.pin = self.device.type == "cuda"
+        self._event = None
+        self._retired: list = []  # regions replaced within the current step (copies may be in flight)
+        self._grow_to = 0
         self._alloc(capacity)
 
     def _alloc(self, n: int):
@@ -29,7 +35,20 @@ class HostStager:
         self.dev = torch.empty(n, dtype=torch.int32, device=self.device) if self.pin else self.host
         self.off = 0
 
+    def fence(self):
+        """Mark the end of a launch's copies (the next reset() waits for them)."""
+        if self.pin:
+            self._event = torch.cuda.Event()
+            self._event.record()
+
     def reset(self):
+        if self._event is not None:
+            self._event.synchronize()
+            self._event = None
+        self._retired.clear()
+        if self._grow_to > self.capacity:
+            self._alloc(self._grow_to)
+        self._grow_to = 0
         self.off = 0
 
     def stage(self, arrays: Sequence[np.ndarray]) -> List[torch.Tensor]:
@@ -44,9 +63,12 @@ class HostStager:
             total += (words + 1) & ~1  # keep every region 8-byte aligned
         start = self.off
         if start + total > self.capacity:
-            if start:  # this step already staged regions that are in flight: never move them
-                raise RuntimeError("HostStager: step staging exceeds capacity; construct with a larger capacity")
+            # regions staged earlier in this step may be in flight: keep them alive, continue in a new region
+            self._grow_to = max(self._grow_to, 2 * self.capacity, start + 2 * total)
+            if start:
+                self._retired.append((self.host, self.dev))
             self._alloc(max(2 * self.capacity, total))
+            start = 0
         for a, o, words in metas:
             self.host_np[start + o:start + o + words] = a.reshape(-1).view(np.int32)
         if self.pin and total:

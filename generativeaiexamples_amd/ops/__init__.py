@@ -133,13 +133,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x2.device)
         nat.gemm_splitk(x2, psw, out, bias, residual, epi, ws, True)
         return out
-    if residual is None and TUNER.pick(M, N, K, act, bias is not None, out_dtype, x2, w) == "blas":
-        if out is None:
-            return _blas_linear(x2, w, bias, act, out_dtype).view(*lead, ncol)
-        if act is None and out_dtype == x.dtype and out.is_contiguous():  # library GEMM straight into `out`
-            o2 = out.view(M, N)
-            torch.addmm(bias, x2, w.t(), out=o2) if bias is not None else torch.mm(x2, w.t(), out=o2)
-            return out
     if out is None:
         out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
     _native_gemm(x2, w, out, bias, residual, epi)
@@ -177,15 +170,14 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     epilogue does the same; otherwise ``linear`` + ``rope_kv_write``. Same bf16 roundings."""
     K = x.shape[-1]
     M = x.numel() // K
-    if (x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and 1 <= M <= 64
-            and TUNER.mode != "hipblaslt"):
+    if x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and 1 <= M <= 64:
         nat = native()
         psw = getattr(w, "_gai_psw", None)
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x.device)
         if nat.gemm_rope_kv(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, positions, cos_sin, slots,
                             q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None):
             return
-    if (x.is_cuda and not isinstance(w, Fp8Weight) and _GEMM_FORCE == 0 and M >= 1024 and TUNER.mode in ("auto", "native")
+    if (x.is_cuda and not isinstance(w, Fp8Weight) and _GEMM_FORCE == 0 and M >= 1024
             and positions.dtype == torch.int32 and slots.dtype == torch.int32):
         # prefill: RoPE + paged KV write in the 256x256 GEMM's epilogue (no bf16 qkv round trip)
         ws = torch.empty(0, dtype=torch.float32, device=x.device)
@@ -228,24 +220,6 @@ def _native_gemm(x2, w, out, bias, residual, epi):
         nat.gemm_splitk(x2, w, out, bias, residual, epi, ws)
     else:
         native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE)
-
-
-def _blas_linear(x2, w, bias, act, out_dtype):
-    """hipBLASLt GEMM (plain library GEMM) + the framework's own elementwise epilogue kernel."""
-    y = torch.addmm(bias, x2, w.t()) if bias is not None else torch.mm(x2, w.t())
-    if act == "swiglu":
-        z = torch.empty(y.shape[0], y.shape[1] // 2, dtype=y.dtype, device=y.device)
-        native().silu_mul_interleaved(y, z)
-        y = z
-    elif act == "gelu":
-        z = torch.empty_like(y)
-        native().gelu(y, z)
-        y = z
-    elif act == "relu":
-        y = torch.relu_(y)
-    elif act == "quick_gelu":
-        y = y * torch.sigmoid(1.702 * y)
-    return y if out_dtype == y.dtype else y.to(out_dtype)
 
 
 _FP8_FORCE = int(os.environ.get("GAI_FP8_FORCE", "0"))  # 0 auto, 2 tiled, 3 large
@@ -323,126 +297,10 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias=None, residual=None, act=None
     return out
 
 
-_TUNED_BLAS = False
-
-
-def enable_tuned_blas() -> bool:
-    """Load the hipBLASLt solutions measured on MI355X for the prefill GEMM shapes (PyTorch TunableOp,
-    lookup only - no tuning at run time). profiles/r1/tunableop_prefill_gemms.jsonl: Llama-3-8B QKV
-    (M = 16384) 1265 -> 1615 TF/s, O 1459 -> 1627 TF/s; gate_up / down keep the default solution.
-    Shapes not in the table use hipBLASLt's heuristic. GAI_TUNABLEOP=0 disables."""
-    global _TUNED_BLAS
-    if _TUNED_BLAS or os.environ.get("GAI_TUNABLEOP", "1") == "0" or not torch.cuda.is_available():
-        return _TUNED_BLAS
-    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "data", "tunableop_mi355x.csv")
-    if not os.path.exists(path):
-        return False
-    import tempfile
-
-    import torch.cuda.tunable as tunable
-
-    import atexit
-    import warnings
-
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    tunable.record_untuned_enable(False)
-    # results are written back to the *current* filename at exit: point it at a scratch file, removed
-    # again at exit
-    scratch = os.path.join(tempfile.gettempdir(), f"gai_tunableop_{os.getpid()}.csv")
-    tunable.set_filename(scratch)
-    atexit.register(lambda: os.path.exists(scratch) and os.remove(scratch))
-    _TUNED_BLAS = bool(tunable.read_file(path))
-    if not _TUNED_BLAS:
-        # validator rows of another hipBLASLt / PyTorch build: the table does not apply
-        warnings.warn(f"TunableOp table {path} was rejected by this hipBLASLt/PyTorch build; "
-                      "using hipBLASLt's default heuristics")
-        tunable.enable(False)
-    return _TUNED_BLAS
-
-
-class GemmTuner:
-    """GEMM backend policy, GAI_GEMM_POLICY = auto (default) | native | hipblaslt | tune.
-
-    auto (deterministic, no run-time timing) = native: every GEMM runs on the hand-written MFMA kernels.
-    Decode-sized GEMMs (M <= 64): the LDS-staged decode kernel for the wide projections (gate_up + fused
-    SwiGLU, LM head) and the weight-streaming split-K kernels for the narrow ones (QKV, O, down), so the
-    decode graph holds no library GEMM. Prefill / encoder GEMMs (M >= 1024): the persistent full-line
-    256x256 kernel (gemm.hip gemm_w4r_kernel) with its fused epilogues, 1.19-1.51 PF/s = 0.94-0.98x
-    hipBLASLt at M = 16K on the Llama-3-8B / e5 shapes (profiles/r2/gemm_w4r.jsonl); with the SwiGLU
-    fused into gate_up (hipBLASLt needs a separate activation pass) the headline bench is within
-    0.4-1.3 % of the library policy on the same box (15.09 vs 15.15 q/s; native / hipblaslt / native
-    15.43 / 15.59 / 15.36 q/s, profiles/r2/policy_ab/); the gap is the deep-K down projection (0.93-0.95x).
-    Since then the prefill QKV GEMM also applies RoPE + the paged KV write in its epilogue (native
-    policies only, linear_rope_kv): +0.9 % on the headline (profiles/r2/prefill_rope_fused/).
-    hipblaslt: library GEMMs for M > 64 (+ the framework's epilogue kernels). tune: per-shape choice
-    between the two, timed on the first call of each (M-bucket, N, K, epilogue) outside capture.
-    Decode GEMMs at M = 64 vs hipBLASLt + epilogue kernel, weights streamed from HBM
-    (profiles/r2/dec2_minwg_sweep.txt): gate_up+SwiGLU 54.9 vs 64.1 us, LM head 233 vs 230 us,
-    QKV 24 vs 34 us, O 18 vs 31 us, down 38 vs 54 us."""
-
-    def __init__(self):
-        self.mode = os.environ.get("GAI_GEMM_POLICY", "auto")
-        self.cache: dict = {}
-        self.log: list = []
-
-    @staticmethod
-    def bucket(M: int) -> int:
-        b = 1
-        while b < M:
-            b *= 2
-        return min(b, 1 << 16)
-
-    def heuristic(self, M, N, K, act, out_dtype) -> str:
-        if out_dtype == torch.float32:
-            return "native"
-        return "native" if M <= 8 else "blas"
-
-    def pick(self, M, N, K, act, has_bias, out_dtype, x2, w) -> str:
-        if self.mode == "native":
-            return "native"
-        if self.mode == "auto":
-            return "native"
-        if self.mode == "hipblaslt":
-            return "blas"
-        key = (self.bucket(M), N, K, act, has_bias, out_dtype)
-        got = self.cache.get(key)
-        if got is not None:
-            return got
-        if torch.cuda.is_current_stream_capturing():
-            return self.heuristic(M, N, K, act, out_dtype)
-        got = self._measure(x2, w, act, has_bias, out_dtype, M, N)
-        self.cache[key] = got
-        return got
-
-    def _measure(self, x2, w, act, has_bias, out_dtype, M, N) -> str:
-        bias = torch.zeros(N, dtype=x2.dtype, device=x2.device) if has_bias else None
-        ncol = N // 2 if act == "swiglu" else N
-        out = torch.empty(M, ncol, dtype=out_dtype, device=x2.device)
-        epi = EPI[act] if act else (EPI["bias"] if has_bias else 0)
-
-        def run_native():
-            _native_gemm(x2, w, out, bias, None, epi)
-
-        def run_blas():
-            _blas_linear(x2, w, bias, act, out_dtype)
-
-        ts = {}
-        for name, fn in (("native", run_native), ("blas", run_blas)):
-            fn()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(3):
-                fn()
-            e.record()
-            e.synchronize()
-            ts[name] = s.elapsed_time(e) / 3
-        best = min(ts, key=ts.get)
-        self.log.append({"M": M, "N": N, "K": x2.shape[1], "act": act, "bias": has_bias, **ts, "pick": best})
-        return best
-
-
-TUNER = GemmTuner()
+# One GEMM backend: every GEMM above is a hand-written gfx950 MFMA kernel (decode M <= 64: gemm_decode.hip /
+# gemm_splitk.hip; prefill / encoder: the persistent 256x256 kernels of gemm.hip; fp8: gemm_fp8.hip). The
+# same-box A/B against hipBLASLt (the library prefill GEMMs, profiles/r2/policy_ab*) lives in
+# tools/blas_ab.py, outside the product code path.
 
 
 # ---------------------------------------------------------------------------------------------
@@ -565,7 +423,10 @@ def sample(logits, temperature, top_p, top_k, seeds, step: int, out=None):
     if not logits.is_cuda:
         return _into(out, ref.sample(logits, temperature, top_p, top_k, seeds, step).to(torch.int32))
     out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device) if out is None else out
-    native().sample(logits, temperature, top_p, top_k, seeds, int(step), out)
+    nat = native()
+    nb = nat.sample_ws_bytes(logits.shape[0], logits.shape[1])  # split-row path (V >= 16K): 3 small kernels
+    ws = torch.empty(nb, dtype=torch.uint8, device=logits.device) if nb else None
+    nat.sample(logits, temperature, top_p, top_k, seeds, int(step), out, ws)
     return out
 
 

@@ -215,13 +215,17 @@ def decode_stream(s: Stream, doc: "PdfDocument" = None) -> Optional[bytes]:
     for f, p in zip(fl, pl):
         f = str(f)
         if f in ("FlateDecode", "Fl"):
+            # bounded inflate: a small crafted stream (zip bomb) must not exhaust the ingest server's memory
+            budget = doc.inflate_budget() if doc is not None else MAX_STREAM_BYTES
             try:
-                data = zlib.decompress(data)
+                z = zlib.decompressobj()
+                data = z.decompress(data, budget + 1)
             except zlib.error:
-                try:
-                    data = zlib.decompressobj().decompress(data)
-                except zlib.error:
-                    return None
+                return None
+            if len(data) > budget or z.unconsumed_tail:
+                return None  # over the per-stream / per-document budget: skip the stream
+            if doc is not None:
+                doc.inflated += len(data)
             if isinstance(p, dict) and int(p.get("Predictor", 1)) >= 10:
                 data = _png_unpredict(data, int(p.get("Columns", 1)), int(p.get("Colors", 1)),
                                       int(p.get("BitsPerComponent", 8)))
@@ -395,12 +399,20 @@ class PdfPage:
 _OBJ_RE = re.compile(rb"(\d+)\s+(\d+)\s+obj\b")
 
 
+MAX_STREAM_BYTES = 64 << 20     # inflated bytes per stream
+MAX_DOCUMENT_BYTES = 512 << 20  # inflated bytes per document
+
+
 class PdfDocument:
     def __init__(self, data: bytes):
         self.data = data
+        self.inflated = 0
         self.objs: Dict[int, Any] = {}
         self._scan()
         self.fonts: Dict[int, Font] = {}
+
+    def inflate_budget(self) -> int:
+        return max(0, min(MAX_STREAM_BYTES, MAX_DOCUMENT_BYTES - self.inflated))
 
     # ---- objects
     def _parse_at(self, pos: int):

@@ -307,6 +307,9 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
             params.guided = guide_for(req, tok)
         except (ValueError, KeyError) as e:  # SchemaError is a ValueError
             return _err(400, f"structured output: {e}")
+        if params.guided is not None and params.max_tokens < params.guided.min_tokens:
+            return _err(400, f"structured output: max_tokens={params.max_tokens} cannot hold the shortest valid "
+                             f"output ({params.guided.min_tokens} tokens)")
         # elastic re-queue (serving/router.py): the router asks for token ids in the stream and resumes a
         # completion a failed replica started by sending the ids it already delivered
         nv = req.nvext or {}

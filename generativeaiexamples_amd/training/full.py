@@ -177,10 +177,18 @@ class FullTrainer:
                       os.path.join(d, f"master.tp{r}.safetensors"))
             torch.save({"opt": self.opt.state_dict(), "step": self.step, "rng": torch.get_rng_state()},
                        os.path.join(d, f"trainer.tp{r}.pt"))
-            if r == 0:
-                with open(os.path.join(d, "meta.json"), "w") as f:
-                    json.dump({"step": self.step, "tp": self.ctx.tp_size, "dp": self.ctx.dp_size, "mode": "full",
-                               "params": self.num_params()}, f)
+        # meta.json is the "checkpoint complete" marker maybe_resume relies on: written only after every rank
+        # has flushed its files (barrier), and atomically (temp file + rename)
+        if self.ctx.is_distributed:
+            self.ctx.barrier()
+        if self.ctx.dp_rank == 0 and r == 0:
+            tmp = os.path.join(d, "meta.json.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"step": self.step, "tp": self.ctx.tp_size, "dp": self.ctx.dp_size, "mode": "full",
+                           "params": self.num_params()}, f)
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, os.path.join(d, "meta.json"))
         if self.ctx.is_distributed:
             self.ctx.barrier()
 

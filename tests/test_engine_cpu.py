@@ -190,3 +190,49 @@ def test_fp8_kv_cache_option():
     bf = KVCache.blocks_for_memory(1 << 24, c.num_layers, c.num_kv_heads, c.head_dim, torch.bfloat16)
     f8 = KVCache.blocks_for_memory(1 << 24, c.num_layers, c.num_kv_heads, c.head_dim, torch.float8_e4m3fn)
     assert f8 == 2 * bf
+
+
+def test_pipelined_decode_runs_chain_and_match_single_step():
+    """Run r+1 is enqueued before run r's tokens are read (device-side feedback of the last token): the
+    chained engine must produce the single-step tokens, including rows that stop inside a run (their next
+    run computes discarded tokens on the scratch page) and must return every KV page."""
+    m = _model(5)
+    tok = small_byte_tokenizer(512)
+    prompts = [list(range(40 + i, 40 + i + n)) for i, n in enumerate((5, 17, 31, 12, 44, 3))]
+    sps = [SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True) for n in (64, 50, 41, 64, 29, 57)]
+
+    def run(steps, sp):
+        eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=8, max_batched_tokens=512, num_blocks=96,
+                                             max_model_len=256, use_graphs=False, decode_steps=steps))
+        outs = eng.generate(prompts, sp)
+        assert eng.sched.num_free_blocks() == eng.sched.num_blocks() and not eng.has_work()
+        return eng, outs
+
+    e1, single = run(1, sps)
+    e8, multi = run(8, sps)
+    assert e8.stats["chained_runs"] >= 3, e8.stats
+    for a, b in zip(single, multi):
+        assert a.output_ids == b.output_ids and a.finish_reason == b.finish_reason
+    # stop tokens taken from the single-step outputs: rows stop at different points inside chained runs
+    stops = [[single[i].output_ids[k]] for i, k in enumerate((9, 30, 14, 3, 22, 40))]
+    sp_stop = [SamplingParams(temperature=0.0, max_tokens=64, stop_token_ids=st) for st in stops]
+    _, s1 = run(1, sp_stop)
+    e8, s8 = run(8, sp_stop)
+    for a, b in zip(s1, s8):
+        assert a.output_ids == b.output_ids and a.finish_reason == b.finish_reason
+
+
+def test_stager_overflow_within_a_step_keeps_earlier_regions():
+    """A step that stages more than the capacity (e.g. > 60 guided rows of 128K-vocabulary masks) continues
+    in a fresh region instead of failing; earlier regions of the step stay valid."""
+    import numpy as np
+
+    from generativeaiexamples_amd.engine.staging import HostStager
+
+    st = HostStager("cpu", capacity=64)
+    st.reset()
+    a = st.stage([np.arange(40, dtype=np.int32)])[0]
+    b = st.stage([np.arange(100, dtype=np.int32) * 3])[0]  # 40 + 100 > 64
+    assert a.tolist() == list(range(40)) and b.tolist() == [3 * i for i in range(100)]
+    st.reset()
+    assert st.capacity >= 140

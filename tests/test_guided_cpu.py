@@ -179,3 +179,19 @@ def test_engine_guided_generation_cpu():
     # unguided request in the same engine is unaffected
     r = eng.generate([tok.encode("x")], SamplingParams(temperature=0.0, max_tokens=5, ignore_eos=True))[0]
     assert len(r.output_ids) == 5
+
+
+def test_engine_guided_exhausted_budget_ends_with_length():
+    """Engine-level (no API admission check): once the grammar allows no token within the remaining budget
+    the request ends with finish_reason 'length' instead of sampling from an all -inf row."""
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+
+    tok = small_byte_tokenizer(512)
+    model = LlamaModel(LlamaConfig.tiny(), device=torch.device("cpu"), dtype=torch.float32).random_init(0)
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=2, num_blocks=64, max_model_len=256, use_graphs=False))
+    g = Guide.json_schema(PERSON, tok)
+    assert g.min_tokens > 3
+    r = eng.generate([tok.encode("p:")], SamplingParams(temperature=1.0, max_tokens=3, guided=g, seed=1))[0]
+    assert r.finished and r.finish_reason == "length"
+    assert eng.sched.num_free_blocks() == eng.sched.num_blocks()

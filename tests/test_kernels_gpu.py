@@ -8,7 +8,6 @@ from generativeaiexamples_amd import ops
 from generativeaiexamples_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
-ops.TUNER.mode = "native"  # these tests exercise the hand-written kernels themselves, never hipBLASLt
 
 
 def _close(a, b, atol, rtol=0.0, what=""):
@@ -386,3 +385,69 @@ def test_gemm_large_repeatable(cuda, M, N, K):
     for _ in range(20):
         assert torch.equal(ops.linear(x, w), y0)
     _close(y0, ref.linear(x.cpu(), w.cpu()), 3e-2, 2e-2, "gemm large")
+
+
+def test_sample_split_path_matches_whole_row(cuda):
+    """The split-row sampler (stats / candidate / resolve kernels, V >= 16K) must draw the whole-row
+    kernel's token for the same (seed, step): greedy, pure temperature, top-k, top-p, top-k + top-p,
+    masked rows and flat rows (candidate overflow -> whole-row fallback inside the resolve kernel)."""
+    from generativeaiexamples_amd.ops import native
+
+    torch.manual_seed(21)
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=cuda) * 1.28
+    logits[5:8] *= 0.01           # flat rows: > 4096 candidates
+    logits[9, 1000:] = float("-inf")  # heavily masked row
+    logits[10, 5] = 40.0          # one dominant token
+    temp = torch.full((B,), 0.2, device=cuda)
+    temp[:4] = 0.0
+    temp[20:28] = 0.9
+    top_p = torch.full((B,), 0.7, device=cuda)
+    top_p[20:24] = 1.0            # pure temperature rows
+    top_k = torch.zeros(B, dtype=torch.int32, device=cuda)
+    top_k[24:28] = 50
+    top_k[28:32] = 1
+    seeds = torch.arange(B, dtype=torch.int64, device=cuda) * 7 + 3
+    nat = native()
+    assert nat.sample_ws_bytes(B, V) > 0
+    agree, total = 0, 0
+    for step in range(6):
+        a = ops.sample(logits, temp, top_p, top_k, seeds, step)
+        b = torch.empty_like(a)
+        nat.sample(logits, temp, top_p, top_k, seeds, step, b)  # no workspace: whole-row kernel
+        assert torch.equal(a[:4], logits[:4].argmax(-1).int())
+        assert torch.equal(a[28:32], logits[28:32].argmax(-1).int())
+        assert int(a[10]) == 5
+        agree += int((a == b).sum())
+        total += B
+    assert agree >= 0.97 * total, (agree, total)
+
+
+def test_sample_split_is_faster(cuda):
+    from generativeaiexamples_amd.ops import native
+
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=cuda) * 1.28
+    temp = torch.full((B,), 0.2, device=cuda)
+    top_p = torch.full((B,), 0.7, device=cuda)
+    top_k = torch.zeros(B, dtype=torch.int32, device=cuda)
+    seeds = torch.arange(B, dtype=torch.int64, device=cuda)
+    out = torch.empty(B, dtype=torch.int32, device=cuda)
+    nat = native()
+    ws = torch.empty(nat.sample_ws_bytes(B, V), dtype=torch.uint8, device=cuda)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(20):
+            fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / 20 * 1000
+
+    t_split = timed(lambda: nat.sample(logits, temp, top_p, top_k, seeds, 1, out, ws))
+    t_row = timed(lambda: nat.sample(logits, temp, top_p, top_k, seeds, 1, out))
+    print(f"sampler B=64 V=128256: split {t_split:.1f} us, whole-row {t_row:.1f} us")
+    assert t_split < t_row

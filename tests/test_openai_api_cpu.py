@@ -161,3 +161,11 @@ def test_structured_output_bad_schema(client):
                                                    "response_format": {"type": "json_schema",
                                                                        "json_schema": {"schema": {"type": "tuple"}}}})
     assert r.status_code == 400
+
+
+def test_structured_output_budget_too_small_is_rejected(client):
+    """A max_tokens that cannot hold the shortest valid value is a 400, not an invalid 'stop' reply."""
+    r = client.post("/v1/chat/completions", json={
+        "max_tokens": 3, "messages": [{"role": "user", "content": "q"}],
+        "response_format": {"type": "json_schema", "json_schema": {"name": "Answer", "schema": SCHEMA}}})
+    assert r.status_code == 400 and "max_tokens" in r.text

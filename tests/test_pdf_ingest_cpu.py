@@ -203,3 +203,19 @@ def test_multimodal_example_ingests_pdf(tmp_path, monkeypatch):
         assert "QUARTERLY RESULTS" in blob and "North | 120" in blob and "This is an image" in blob
     finally:
         hub.shutdown()
+
+
+def test_flate_bomb_is_bounded(monkeypatch):
+    """A FlateDecode stream inflating past the per-stream budget is skipped, not inflated into memory."""
+    import zlib
+
+    from generativeaiexamples_amd.rag import pdf
+
+    monkeypatch.setattr(pdf, "MAX_STREAM_BYTES", 1 << 20)
+    bomb = zlib.compress(b"\0" * (8 << 20), 9)  # 8 MiB of zeros in ~8 KiB
+    s = pdf.Stream({"Filter": "FlateDecode", "Length": len(bomb)}, bomb)
+    doc = pdf.PdfDocument.__new__(pdf.PdfDocument)
+    doc.inflated, doc.objs = 0, {}
+    assert pdf.decode_stream(s, doc) is None
+    ok = pdf.Stream({"Filter": "FlateDecode"}, zlib.compress(b"BT (hi) Tj ET"))
+    assert pdf.decode_stream(ok, doc) == b"BT (hi) Tj ET"

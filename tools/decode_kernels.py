@@ -21,10 +21,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=2600)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-psw", action="store_true", help="plain-layout decode weights (no fragment copies)")
-    ap.add_argument("--policy", default=None, help="GEMM policy override: tune|native|hipblaslt")
     a = ap.parse_args()
-    if a.policy:
-        ops.TUNER.mode = a.policy
     m, tok, name = build_llm(a.model, device="cuda")
     if not a.no_psw:
         m.preshuffle_decode_weights()  # what LLMEngine does (EngineConfig.decode_preshuffle)
@@ -50,8 +47,6 @@ def main():
         torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
     print(f"{name} decode B={B} ctx={a.ctx}: {1000 * dt:.3f} ms/forward (eager, includes launch overhead)")
-    for r in ops.TUNER.log:
-        print("tuner", r)
 
 
 if __name__ == "__main__":

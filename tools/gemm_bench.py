@@ -13,7 +13,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from generativeaiexamples_amd import ops  # noqa: E402
+from generativeaiexamples_amd import ops
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from blas_ab import enable_tuned_blas  # noqa: E402  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "e5_ffn_up": (4096, 1024), "e5_qkv": (3072, 1024)}
@@ -69,7 +71,7 @@ def main():
         r["w4r_vs_blas"] = round(r["hipblaslt_ms"] / r["w4r_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
-    if ops.enable_tuned_blas():
+    if enable_tuned_blas():
         for r in rows:
             M, N, K = r["M"], r["N"], r["K"]
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)

@@ -1,0 +1,48 @@
+#!/usr/bin/env bash
+# One parameterised GPU job for gpurun (replaces the per-call scripts): every argument is one recipe,
+# run in order under its own time limit; the job stops at the first failure (abort, fault, timeout).
+#
+#   tools/gpu.sh <out-subdir> "<recipe> [args...]" ["<recipe> [args...]" ...]
+#
+# recipes (logs / results land in gpurun_out/<out-subdir>/):
+#   tests <name> <pytest args...>   python -m pytest -m gpu <args> (per-test timeout 120 s)
+#   bench <name> <bench.py args...> bench.py ... --json-out <name>.json
+#   prof  <name> <bench.py args...> rocprofv3 --kernel-trace --stats around bench.py, reduced to <name>_kernels.csv
+#   py    <name> <script args...>   python <script> <args>
+#   smoke                           __graft_entry__.smoke()
+# e.g. /usr/local/graft/bin/gpurun --timeout 900 -- tools/gpu.sh r3a "tests kern tests/test_kernels_gpu.py" \
+#        "bench b1 --steps 3 --warmup 1"
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export PYTHONPATH=$PWD
+export TMPDIR=/tmp
+O=$PWD/gpurun_out/$1; shift; mkdir -p "$O"
+
+step() {  # step SECONDS LOG cmd...
+  local secs=$1 log=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "[gpu.sh] rc=$rc cmd=$*" >> "$log"
+  tail -4 "$log"
+  return $rc
+}
+
+for spec in "$@"; do
+  read -r -a a <<< "$spec"
+  r=${a[0]}; n=${a[1]:-x}; rest=("${a[@]:2}")
+  echo "[gpu.sh] $(date +%T) $spec"
+  case $r in
+    tests) step 600 "$O/$n.log" python -u -m pytest -m gpu -q --timeout 120 --timeout-method thread \
+             -p no:cacheprovider "${rest[@]}" || exit $? ;;
+    bench) step 600 "$O/$n.log" python bench.py "${rest[@]}" --json-out "$O/$n.json" || exit $? ;;
+    prof)  rm -rf "/tmp/prof_$n"
+           step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
+             python3 "$PWD/bench.py" "${rest[@]}" --json-out "$O/$n.json" || exit $?
+           python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
+             > /dev/null || exit $? ;;
+    py)    step 600 "$O/$n.log" python "${rest[@]}" || exit $? ;;
+    smoke) step 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $? ;;
+    *) echo "unknown recipe $r"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] done"

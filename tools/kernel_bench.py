@@ -6,6 +6,8 @@ Interleaved rounds in one process (cdna_hip_programming §5.4 rule 24), random o
 from __future__ import annotations
 
 import argparse
+import sys
+import os
 import json
 import math
 import time
@@ -13,6 +15,8 @@ import time
 import torch
 
 from generativeaiexamples_amd import ops
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from blas_ab import blas_linear  # noqa: E402
 
 
 def timeit(fn, iters=20, warmup=3):
@@ -112,7 +116,7 @@ def bench_dec_hbm(rows, shapes, rounds=5):
             it[0] = (it[0] + 1) % ncopy
             return pool[it[0]]
         arms = {"native": lambda: nat.gemm_splitk(x, nxt(ws_), out, None, None, epi, wsp, False),
-                "blas": lambda: ops._blas_linear(x, nxt(ws_), None, act, odt)}
+                "blas": lambda: blas_linear(x, nxt(ws_), None, act, odt)}
         if sh_ is not None:
             arms["native_psw"] = lambda: nat.gemm_splitk(x, nxt(sh_), out, None, None, epi, wsp, True)
         ts = {k: [] for k in arms}
@@ -120,7 +124,7 @@ def bench_dec_hbm(rows, shapes, rounds=5):
             for k, f in arms.items():
                 ts[k].append(timeit(f, iters=30) * 1e3)
         nat.gemm_splitk(x, ws_[0], out, None, None, epi, wsp, False)
-        ref_ = ops._blas_linear(x, ws_[0], None, act, odt)
+        ref_ = blas_linear(x, ws_[0], None, act, odt)
         err = (out.float() - ref_.float()).abs().max().item()
         by = N * K * 2
         r = dict(op="dec_hbm", name=name, M=M, N=N, K=K, act=act, max_err_vs_blas=err)
