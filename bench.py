@@ -81,7 +81,11 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-plant", action="store_true", help="do not plant per-query relevant chunks")
     ap.add_argument("--no-probes", action="store_true", help="skip the untimed c1 / open-loop TTFT probes")
-    ap.add_argument("--probe-c1", type=int, default=8, help="queries of the concurrency-1 TTFT probe")
+    ap.add_argument("--probe-c1", type=int, default=4,
+                    help="queries of the concurrency-1 probe (each runs its full max_tokens: TTFT and TPOT)")
+    ap.add_argument("--served", action="store_true",
+                    help="drive the chain server instead of the engine: every query is a concurrent POST /generate "
+                         "SSE stream (basic_rag example, in-process engines), TTFT measured at the client")
     from generativeaiexamples_amd.benchmarks import CONFIGS, module
     for c in CONFIGS:
         module(c).add_args(ap)
@@ -113,8 +117,8 @@ def run_other_config(args):
 
 
 def run_probes(args, embedder, index, engine, build_requests, plant, unplant, new_phase, qps_per_rank):
-    """c1 TTFT and open-loop Poisson TTFT (untimed). Every query: embed -> local 1M scan -> prompt ->
-    engine; TTFT = scheduled arrival -> first token. c1 queries are aborted after their first token."""
+    """c1 TTFT / TPOT and open-loop Poisson TTFT (untimed). Every query: embed -> local 1M scan -> prompt ->
+    engine; TTFT = scheduled arrival -> first token; TPOT = (finish - first token) / (tokens - 1)."""
     rank = int(os.environ.get("RANK", "0"))
 
     def retrieve(qids):
@@ -123,8 +127,8 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
         _, rows = index.search_raw(e, args.top_k)
         return build_requests(qs, rows.cpu().tolist(), new_phase())
 
-    # concurrency 1
-    c1 = []
+    # concurrency 1: each query runs its full max_tokens (TTFT and per-token latency of a lone stream)
+    c1, tpot = [], []
     base = 900_000 + 1000 * rank
     for i in range(args.probe_c1):
         qid = base + i
@@ -132,12 +136,12 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         req = retrieve([qid])[0]
-        while req.first_token_time is None:
-            engine.step()
-        c1.append(req.first_token_time - t0)
-        engine.abort(req.request_id)
         while engine.has_work():
             engine.step()
+        c1.append(req.first_token_time - t0)
+        n = len(req.output_ids)
+        if n > 1:
+            tpot.append((req.finish_time - req.first_token_time) / (n - 1))
         unplant(planted)
     # open loop: Poisson arrivals at 0.8x the measured per-rank burst rate
     rate = 0.8 * qps_per_rank
@@ -168,7 +172,9 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
     span = time.perf_counter() - t0
     unplant(planted)
     tt = sorted(r.first_token_time - t0 - a for a, r in reqs)
+    tp = statistics.median(tpot) if tpot else float("nan")
     return {"p50_ttft_c1_s": round(statistics.median(c1), 4), "ttft_c1_s": [round(x, 4) for x in c1],
+            "tpot_c1_ms": round(1000 * tp, 3), "decode_tok_s_c1": round(1.0 / tp, 1) if tpot else None,
             "poisson": {"rate_qps_per_gpu": round(rate, 3), "queries": n, "achieved_qps_per_gpu": round(n / span, 3),
                         "p50_ttft_s": round(tt[len(tt) // 2], 4),
                         "p90_ttft_s": round(tt[min(len(tt) - 1, int(0.9 * len(tt)))], 4)}}
@@ -331,6 +337,21 @@ def main():
 
     def new_phase():
         return dict(embed=0.0, scan=0.0, prompt_build=0.0, tokenize=0.0, add_request=0.0)
+
+    if args.served:
+        from generativeaiexamples_amd.benchmarks.served import run_served
+
+        out = run_served(args, ctx, dict(lcfg=lcfg, bcfg=bcfg, embedder=embedder, index=index, engine=engine,
+                                         plant=plant, unplant=unplant, metric=METRIC, baseline_qps=BASELINE_QPS))
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    json.dump(out, f)
+        if world > 1:
+            torch.distributed.barrier()
+            torch.distributed.destroy_process_group()
+        return
 
     uniq = set()
     for w in range(args.warmup):

@@ -32,6 +32,8 @@ class LLMConfig(ConfigWizard):
                                     help_txt="mi355x (in-process) | nvidia-ai-endpoints | openai")
     model_name_pandas_ai: str = configfield("modelNamePandasAI", default="meta/llama3-8b-instruct",
                                             help_txt="model used by the structured-data (CSV) example")
+    ignore_eos: bool = configfield("ignoreEos", default=False,
+                                   help_txt="benchmarking only: every answer generates exactly max_tokens")
 
 
 @configclass

@@ -58,7 +58,30 @@ class ChatLLM:
         s.update({k: v for k, v in override.items() if v is not None})
         return SamplingParams(temperature=float(s.get("temperature", 0.2)), top_p=float(s.get("top_p", 0.7)),
                               max_tokens=int(s.get("max_tokens", 1024)), stop=list(s.get("stop") or []),
-                              seed=s.get("seed"))
+                              seed=s.get("seed"), ignore_eos=bool(s.get("ignore_eos", False)))
+
+
+class EngineStream:
+    """Token-text stream of one in-process generation. Iterated synchronously (a worker thread blocks per
+    chunk, e.g. an example that post-processes the stream) or asynchronously (``async for``: the
+    chain-server SSE route awaits the engine's asyncio queue and holds no thread while waiting). The
+    request is submitted to the engine when iteration starts."""
+
+    def __init__(self, engine, ids: List[int], params: SamplingParams):
+        self.engine, self.ids, self.params = engine, ids, params
+
+    def __iter__(self) -> Iterator[str]:
+        for it in self.engine.generate_sync(self.ids, self.params):
+            if it.delta:
+                yield it.delta
+
+    async def _agen(self):
+        async for it in self.engine.generate(self.ids, self.params):
+            if it.delta:
+                yield it.delta
+
+    def __aiter__(self):
+        return self._agen()
 
 
 class LocalChatLLM(ChatLLM):
@@ -66,11 +89,9 @@ class LocalChatLLM(ChatLLM):
         super().__init__(**settings)
         self.engine, self.model = engine, model
 
-    def stream(self, messages, **override) -> Iterator[str]:
+    def stream(self, messages, **override) -> EngineStream:
         ids = apply_chat_template(messages, self.engine.tokenizer)
-        for it in self.engine.generate_sync(ids, self._params(override)):
-            if it.delta:
-                yield it.delta
+        return EngineStream(self.engine, ids, self._params(override))
 
 
 class RemoteChatLLM(ChatLLM):
@@ -126,6 +147,9 @@ class LocalEmbeddings(Embeddings):
         self.dim = embedder.dim
 
     def embed_tensor(self, texts, input_type):
+        # concurrent callers (retrieval threads, ingest) coalesce into one encoder call (DynamicBatcher)
+        if hasattr(self.e, "embed_coalesced"):
+            return self.e.embed_coalesced(texts, input_type, self.truncate)
         return self.e.embed(texts, input_type, self.truncate)
 
     def embed_documents(self, texts):

@@ -236,13 +236,19 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
         if query is None:
             query = ""
         chain = ex.rag_chain if prompt.use_knowledge_base else ex.llm_chain
+        # retrieval + prompt building run in a worker thread (concurrent queries coalesce into one embed and
+        # one index scan there); the token stream is then awaited on the event loop when the chain returns
+        # an async-iterable stream (in-process engine), so no thread is held per open stream
         gen = await run_in_threadpool(chain, query, history, **settings)
-        gen = tracing.traced_stream("llm_stream", iter(gen))
+        if hasattr(gen, "__aiter__"):
+            chunks = tracing.traced_astream("llm_stream", gen)
+        else:
+            chunks = iterate_in_threadpool(tracing.traced_stream("llm_stream", iter(gen)))
 
         async def frames():
             rid = str(uuid.uuid4())
             try:
-                async for chunk in iterate_in_threadpool(gen):
+                async for chunk in chunks:
                     if chunk:
                         yield _frame(chunk, "", rid)
                 yield _frame("", "[DONE]", rid)

@@ -202,6 +202,23 @@ def traced(kind: str):
     return deco
 
 
+async def traced_astream(name: str, it, **attrs):
+    """Async twin of :func:`traced_stream` for streams iterated with ``async for``."""
+    if not ENABLED:
+        async for chunk in it:
+            yield chunk
+        return
+    with span(name, **attrs) as s:
+        t0, n = time.perf_counter(), 0
+        async for chunk in it:
+            if n == 0 and s is not None:
+                s.set_attribute("first_token_time_ms", (time.perf_counter() - t0) * 1000.0)
+            n += 1
+            yield chunk
+        if s is not None:
+            s.set_attribute("completion_chunks", n)
+
+
 def traced_stream(name: str, it: Iterator[str], **attrs) -> Iterator[str]:
     """Wraps a token stream; records first_token_time_ms (TTFT) and the token count."""
     if not ENABLED:

@@ -100,6 +100,8 @@ def set_hub(hub) -> None:
 def get_llm(**kwargs) -> ChatLLM:
     c = get_config().llm
     settings = {k: kwargs.get(k) for k in ("temperature", "top_p", "max_tokens", "stop") if k in kwargs}
+    if c.ignore_eos:
+        settings["ignore_eos"] = True
     eng = c.model_engine.lower()
     if eng in REMOTE_ENGINES or (c.server_url and eng not in LOCAL_ENGINES):
         if not c.server_url and eng == "nvidia-ai-endpoints":

@@ -55,6 +55,10 @@ class VectorStore:
                 if self.persist:
                     self.index.attach_wal(self.persist)
             rows = self.index.add(vecs, docs)
+            if self.index.device.type == "cuda":  # queries scan on the retrieval stream: writes land first
+                import torch
+
+                torch.cuda.current_stream(self.index.device).synchronize()
             if self.bm25 is not None:
                 self.bm25.add(rows, [d.page_content for d in docs])
             return rows
@@ -72,16 +76,39 @@ class VectorStore:
     add_texts = lambda self, texts, metadatas=None: self.add_documents(  # noqa: E731
         [Document(t, (metadatas or [{}] * len(texts))[i]) for i, t in enumerate(texts)])
 
+    # ---- query path: concurrent queries of this collection coalesce into ONE embed + ONE scan
+    @property
+    def batcher(self):
+        if getattr(self, "_batcher", None) is None:
+            from ..engine.embedder import DynamicBatcher
+
+            with self.lock:
+                if getattr(self, "_batcher", None) is None:
+                    self._batcher = DynamicBatcher(self._search_batch, max_batch=256, name=f"search-{self.name}")
+        return self._batcher
+
+    def _search_batch(self, items: List[Tuple[str, int, Optional[float]]]) -> List[List[Tuple[Document, float]]]:
+        """[(query, k, threshold)] -> hits per query: one query-embedding micro-batch and one exact scan of
+        the index for all of them (the scan streams the whole index once per batch, not once per query),
+        on the high-priority retrieval stream."""
+        from ..utils.streams import on_retrieval_stream
+
+        with on_retrieval_stream(self.index.device):
+            q = self.emb.embed_tensor([it[0] for it in items], "query")
+            kmax = max(it[1] for it in items)
+            hits = self.index.search(q.to(self.index.device), kmax, None)
+        return [[(h.document, h.score) for h in hs[:k] if thr is None or h.score >= thr]
+                for hs, (_, k, thr) in zip(hits, items)]
+
     @tracing.traced("retriever")
     def similarity_search_with_relevance_scores(self, query: str, k: int = 4,
                                                 score_threshold: Optional[float] = None) -> List[Tuple[Document, float]]:
         import time
 
         t0 = time.perf_counter()
-        q = self.emb.embed_tensor([query], "query")
-        hits = self.index.search(q, k, score_threshold)[0]
+        hits = self.batcher.submit((query, k, score_threshold)).result()
         METRICS.search.observe(time.perf_counter() - t0)
-        return [(h.document, h.score) for h in hits]
+        return hits
 
     @tracing.traced("retriever")
     def hybrid_search(self, query: str, k: int = 4, candidates: int = 40) -> List[Tuple[Document, float]]:

@@ -90,6 +90,47 @@ class Embedder:
         with roctx_range("embed"):
             return self.embed_ids([self.tokenize(t, input_type, truncate) for t in texts])
 
+    # ---- coalesced serving path (/v1/embeddings, chain-server queries)
+    @property
+    def batcher(self) -> DynamicBatcher:
+        """Concurrent embed requests -> one encoder call per batch, on the high-priority retrieval stream."""
+        if getattr(self, "_batcher", None) is None:
+            with self.lock:
+                if getattr(self, "_batcher", None) is None:
+                    self._batcher = DynamicBatcher(self._embed_requests, max_batch=256, name="embed-batcher")
+        return self._batcher
+
+    def _embed_requests(self, reqs: List[Tuple[Tuple[str, ...], str, str]]) -> List[torch.Tensor]:
+        from ..utils.streams import on_retrieval_stream
+
+        out: List = [None] * len(reqs)
+        groups: dict = {}
+        for i, (texts, itype, trunc) in enumerate(reqs):
+            groups.setdefault((itype, trunc), []).append(i)
+        with on_retrieval_stream(self.model.device):
+            for (itype, trunc), idx in groups.items():
+                seqs, spans = [], []
+                for i in idx:
+                    try:
+                        ids = [self.tokenize(t, itype, trunc) for t in reqs[i][0]]
+                    except TruncationError as e:  # this request fails alone
+                        out[i] = e
+                        continue
+                    spans.append((i, len(seqs), len(seqs) + len(ids)))
+                    seqs += ids
+                if not seqs:
+                    continue
+                e = self.embed_ids(seqs)
+                for i, a, b in spans:
+                    out[i] = e[a:b]
+        return out
+
+    def embed_coalesced(self, texts: Sequence[str], input_type: str = "passage", truncate: str = "END") -> torch.Tensor:
+        r = self.batcher.submit((tuple(texts), input_type, truncate)).result()
+        if isinstance(r, Exception):
+            raise r
+        return r
+
 
 class ClipEmbedder:
     """NV-CLIP-style multimodal embedder over :class:`~..models.clip.ClipModel` (BASELINE config 4,
@@ -198,44 +239,62 @@ class Reranker:
 
 
 class DynamicBatcher:
-    """Thread-safe request coalescer in front of a batch function ``fn(list[item]) -> list[result]``."""
+    """Thread-safe request coalescer in front of a batch function ``fn(list[item]) -> list[result]``
+    (Triton ``dynamic_batching`` semantics of the reference's embedding service,
+    all-MiniLM-L6-v2_config.pbtxt:19-29: preferred batch sizes up to 256, bounded queue delay).
 
-    def __init__(self, fn, max_batch: int = 256, max_delay_ms: float = 5.0):
+    One worker thread runs ``fn``. When it is free it takes everything queued (up to ``max_batch``) at
+    once, so an idle service adds no latency; while ``fn`` runs, new requests queue and form the next
+    batch. ``max_delay_ms`` > 0 additionally holds a batch that is not yet a preferred size for up to that
+    long to collect more. ``batch_sizes`` keeps the recent batch sizes (tests / metrics)."""
+
+    def __init__(self, fn, max_batch: int = 256, max_delay_ms: float = 0.0, preferred=None, name="dynamic-batcher"):
         self.fn, self.max_batch, self.max_delay = fn, max_batch, max_delay_ms / 1000.0
+        self.preferred = set(preferred or [1 << i for i in range(9) if (1 << i) <= max_batch])
         self.q: List[Tuple[object, Future]] = []
         self.cv = threading.Condition()
         self.stop = False
-        self.t = threading.Thread(target=self._loop, daemon=True, name="dynamic-batcher")
+        self.batch_sizes: List[int] = []
+        self.t = threading.Thread(target=self._loop, daemon=True, name=name)
         self.t.start()
 
     def submit(self, item) -> Future:
         f: Future = Future()
         with self.cv:
+            if self.stop:
+                raise RuntimeError("batcher closed")
             self.q.append((item, f))
             self.cv.notify()
         return f
 
+    def __call__(self, item):
+        return self.submit(item).result()
+
     def _loop(self):
-        while not self.stop:
+        while True:
             with self.cv:
                 while not self.q and not self.stop:
                     self.cv.wait()
-                deadline = time.perf_counter() + self.max_delay
-                while len(self.q) < self.max_batch and not self.stop:
-                    rem = deadline - time.perf_counter()
-                    if rem <= 0:
-                        break
-                    self.cv.wait(rem)
+                if self.stop and not self.q:
+                    return
+                if self.max_delay > 0 and len(self.q) not in self.preferred:
+                    deadline = time.perf_counter() + self.max_delay
+                    while len(self.q) < self.max_batch and len(self.q) not in self.preferred and not self.stop:
+                        rem = deadline - time.perf_counter()
+                        if rem <= 0:
+                            break
+                        self.cv.wait(rem)
                 batch, self.q = self.q[: self.max_batch], self.q[self.max_batch:]
-            if not batch:
-                continue
+            self.batch_sizes.append(len(batch))
+            del self.batch_sizes[:-1024]
             try:
                 res = self.fn([b[0] for b in batch])
                 for (_, f), r in zip(batch, res):
                     f.set_result(r)
             except Exception as e:  # propagate to every waiter
                 for _, f in batch:
-                    f.set_exception(e)
+                    if not f.done():
+                        f.set_exception(e)
 
     def close(self):
         with self.cv:

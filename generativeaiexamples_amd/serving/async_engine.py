@@ -9,6 +9,7 @@ disconnect aborts its request (frees its KV blocks) immediately.
 from __future__ import annotations
 
 import asyncio
+import collections
 import faulthandler
 import logging
 import os
@@ -49,6 +50,8 @@ class AsyncLLMEngine:
         self.error: Optional[BaseException] = None
         self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("GAI_WATCHDOG_S", "300"))
         self._step_started: Optional[float] = None
+        # (request id, generated tokens, finish reason) of recently finished requests (benchmarks, tests)
+        self.completed: collections.deque = collections.deque(maxlen=4096)
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
         self.thread.start()
@@ -133,6 +136,7 @@ class AsyncLLMEngine:
                 yield StreamItem(o.delta, o.token_id, o.finished, o.finish_reason)
                 if o.finished:
                     METRICS.e2e.observe(time.perf_counter() - t0)
+                    self.completed.append((rid, len(req.output_ids), o.finish_reason))
                     return
         finally:
             if rid in self.queues:  # client went away or error: free the sequence now
@@ -174,6 +178,7 @@ class AsyncLLMEngine:
                     first = False
                 yield StreamItem(o.delta, o.token_id, o.finished, o.finish_reason)
                 if o.finished:
+                    self.completed.append((rid, len(req.output_ids), o.finish_reason))
                     return
         finally:
             if rid in self.queues:

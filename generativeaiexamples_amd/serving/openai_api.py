@@ -426,7 +426,9 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
             return _err(400, "input_type must be 'query' or 'passage'")
         t0 = time.perf_counter()
         try:
-            vecs = await run_in_threadpool(lambda: emb.embed(texts, itype, req.truncate or "NONE"))
+            # concurrent /v1/embeddings calls coalesce into one encoder batch (Triton dynamic batching semantics)
+            fn = getattr(emb, "embed_coalesced", emb.embed)
+            vecs = await run_in_threadpool(lambda: fn(texts, itype, req.truncate or "NONE"))
         except ValueError as e:
             return _err(400, str(e))
         METRICS.embed.observe(time.perf_counter() - t0)
