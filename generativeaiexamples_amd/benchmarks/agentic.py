@@ -32,6 +32,10 @@ TOOL = {"type": "function", "function": {
 def add_args(ap):
     ap.add_argument("--agent-model", default="mixtral-8x7b", choices=["mixtral-8x7b", "tiny-moe"])
     ap.add_argument("--plan-tokens", type=int, default=64)
+    ap.add_argument("--ep", action="store_true",
+                    help="expert parallelism over the ranks: data-parallel attention + experts sharded with all-to-all "
+                         "token exchange and lockstep steps (default: one full Mixtral replica per GPU - it fits "
+                         "one 288 GB MI355X, so replicas need no collective at all)")
 
 
 def run(args, ctx) -> dict:
@@ -50,7 +54,11 @@ def run(args, ctx) -> dict:
     index_size = args.index_size or 1_000_000
     t_setup = time.perf_counter()
     mcfg = MixtralConfig.mixtral_8x7b() if args.agent_model == "mixtral-8x7b" else MixtralConfig.tiny_moe()
-    llm = MixtralModel(mcfg, device=dev).random_init(seed=21)
+    ep_group = None
+    if getattr(args, "ep", False) and world > 1:
+        import torch.distributed as dist
+        ep_group = dist.group.WORLD
+    llm = MixtralModel(mcfg, device=dev, ep_group=ep_group).random_init(seed=21)
     tok = _generic_tok(mcfg) if mcfg.vocab_size > 4096 else small_byte_tokenizer(mcfg.vocab_size)
     bcfg = BertConfig.e5_large_v2() if args.agent_model == "mixtral-8x7b" else BertConfig.tiny()
     emb = Embedder(BertModel(bcfg, device=dev).random_init(seed=22), bert_byte_tokenizer(bcfg.vocab_size))
@@ -119,7 +127,7 @@ def run(args, ctx) -> dict:
                 "EOS ignored; unparseable tool calls fall back to the question as the tool query)",
         "config": {"model": f"{mcfg.name} + {bcfg.name} + {index_size}-vector HBM index per GPU",
                    "global_batch": batch * world, "seq_len": int(median([s["prompt"] for s in stats])) + args.max_tokens,
-                   "parallelism": f"dp{world}", "turns": 2, "plan_tokens": args.plan_tokens,
+                   "parallelism": f"dp{world}-attention+ep{world}-experts" if ep_group is not None else f"dp{world}", "turns": 2, "plan_tokens": args.plan_tokens,
                    "max_tokens": args.max_tokens},
         "p50_ttft_s": round(percentile(ttft, 0.5), 4), "p50_answer_ttft_s": round(percentile(attft, 0.5), 4),
         "output_tokens_per_s": round(toks / total, 1),

@@ -215,6 +215,37 @@ void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p
              wp, wb, cur_stream());
 }
 
+void sample_tp_resolve(const Tensor& packets, int64_t C, int64_t V, const Tensor& temperature, const Tensor& top_p,
+                       const Tensor& top_k, const Tensor& seeds, int64_t step, Tensor& out, Tensor& flags) {
+  check_f32(packets, "packets");
+  TORCH_CHECK(packets.dim() == 3 && packets.is_contiguous(), "packets must be a contiguous [R, B, W] tensor");
+  check_f32(temperature, "temperature");
+  check_f32(top_p, "top_p");
+  check_i32(top_k, "top_k");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
+  check_i32(out, "out");
+  check_i32(flags, "flags");
+  const int R = packets.size(0), B = packets.size(1), W = packets.size(2);
+  TORCH_CHECK(out.numel() >= B, "out too small");
+  TORCH_CHECK(gai_sample_tp_resolve(packets.data_ptr<float>(), R, B, W, (int)C, (int)V, temperature.data_ptr<float>(),
+                                    top_p.data_ptr<float>(), top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), step,
+                                    out.data_ptr<int>(), flags.data_ptr<int>(), cur_stream()),
+              "sample_tp_resolve: R * C must be <= 1024 and W >= 4 + 2C");
+}
+
+void sample_tp_stats(const Tensor& logits, int64_t vstart, int64_t V, const Tensor& temperature, const Tensor& seeds,
+                     int64_t step, Tensor& out) {
+  check_f32(logits, "logits");
+  TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
+  check_f32(temperature, "temperature");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
+  check_f32(out, "out");
+  TORCH_CHECK(out.is_contiguous() && out.numel() >= logits.size(0) * 4, "out must hold [B, 4] floats");
+  gai_sample_tp_stats(logits.data_ptr<float>(), logits.stride(0), logits.size(0), logits.size(1), (int)vstart, (int)V,
+                      temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), step, out.data_ptr<float>(),
+                      cur_stream());
+}
+
 int64_t sample_ws_bytes(int64_t B, int64_t V) { return (int64_t)gai_sample_ws_bytes((int)B, (int)V);
 }
 
@@ -596,6 +627,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none());
   m.def("sample_ws_bytes", &sample_ws_bytes);
+  m.def("sample_tp_resolve", &sample_tp_resolve);
+  m.def("sample_tp_stats", &sample_tp_stats);
   m.def("apply_penalties", &apply_penalties);
   m.def("token_mask", &token_mask);
   m.def("sim_topk", &sim_topk);

@@ -676,6 +676,164 @@ __global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __
   if (tid == 0) out_tokens[row] = best.i < V ? best.i : am.i;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Vocab-parallel (TP) sampling without gathering the logits. Every TP rank reduces its logit shard to a
+// packet per row [max, sum exp((x - max) / T), Gumbel-max value, its id, C candidate values, C candidate
+// global ids (ids as exact floats)] (sample_tp_stats + its top-C, ops.sample_tp). The packets of all R ranks are gathered (one small peer-memory all-reduce of a
+// zero-padded [R, B, W] buffer) and every rank runs this kernel on the same bytes, so all ranks draw the
+// same token with no further collective. The candidate list holds every token above a cut K* when K* is
+// above every rank's C-th value; then the result is exactly the whole-row sampler's (same nucleus, same
+// Gumbel noise gumbel(seed, step, id)). Otherwise the draw is restricted to the R x C candidates and the
+// row is counted in flags[0] (diagnostics).
+constexpr int kTpThreads = 256;
+constexpr int kTpMaxCand = 1024;
+
+__global__ __launch_bounds__(kTpThreads) void sample_tp_resolve(const float* __restrict__ pk, int R, int B, int W, int C,
+                                                                int V, const float* __restrict__ temperature,
+                                                                const float* __restrict__ top_p,
+                                                                const int* __restrict__ top_k,
+                                                                const int64_t* __restrict__ seeds, int64_t step,
+                                                                int* __restrict__ out_tokens, int* __restrict__ flags) {
+  __shared__ float val[kTpMaxCand];
+  __shared__ int idx[kTpMaxCand];
+  __shared__ float wsum[kTpThreads / 64];
+  __shared__ float cutv;
+  __shared__ int cutj;
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = R * C;
+  int P = 1;
+  while (P < n) P <<= 1;
+  // candidates -> LDS (padding: -inf, id INT_MAX)
+  for (int j = tid; j < P; j += kTpThreads) {
+    if (j < n) {
+      const int r = j / C, c = j % C;
+      const float* q = pk + ((size_t)r * B + row) * W;
+      val[j] = q[4 + c];
+      idx[j] = (int)q[4 + C + c];
+    } else {
+      val[j] = -INFINITY;
+      idx[j] = 0x7fffffff;
+    }
+  }
+  const float T = temperature[row];
+  float M = -INFINITY, kth_max = -INFINITY;
+  for (int r = 0; r < R; ++r) {
+    const float* q = pk + ((size_t)r * B + row) * W;
+    M = fmaxf(M, q[0]);
+    kth_max = fmaxf(kth_max, q[4 + C - 1]);
+  }
+  __syncthreads();
+  // sort descending by value, ties: smaller id first
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < P / 2; t += kTpThreads) {
+        const int a = (t / j) * 2 * j + (t % j), b = a + j;
+        const float va = val[a], vb = val[b];
+        const int ia = idx[a], ib = idx[b];
+        const bool b_first = vb > va || (vb == va && ib < ia);
+        if (((a & k) == 0) ? b_first : !b_first) {
+          val[a] = vb, val[b] = va;
+          idx[a] = ib, idx[b] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (T <= 0.f) {  // greedy: the global max is every rank's first candidate
+    if (tid == 0) out_tokens[row] = idx[0];
+    return;
+  }
+  const float invT = 1.f / T;
+  float S = 0.f;
+  for (int r = 0; r < R; ++r) {
+    const float* q = pk + ((size_t)r * B + row) * W;
+    if (q[0] > -INFINITY) S += q[1] * __expf((q[0] - M) * invT);
+  }
+  const int k = top_k[row];
+  const float p = top_p[row];
+  if (p >= 1.f && (k <= 0 || k >= V)) {  // pure temperature: the max over the ranks' shard Gumbel-maxima (exact)
+    if (tid == 0) {
+      ArgMax g{-INFINITY, 0x7fffffff};
+      for (int r = 0; r < R; ++r) {
+        const float* q = pk + ((size_t)r * B + row) * W;
+        g = argmax_merge(g, ArgMax{q[2], (int)q[3]});
+      }
+      out_tokens[row] = g.i < V ? g.i : idx[0];
+    }
+    return;
+  }
+  int nk = n;            // candidates inside the top-k set
+  bool exact = true;
+  if (k > 0 && k < V) {
+    if (k > n) exact = false;
+    else nk = k;
+  }
+  // mass of the top-k set (or the whole row), then the first prefix reaching p of it
+  if (tid == 0) cutj = nk - 1;
+  float total = S;
+  if (k > 0 && k < V) {
+    float s = 0.f;
+    for (int j = tid; j < nk; j += kTpThreads) s += __expf((val[j] - M) * invT);
+    s = wave_sum(s);
+    if (lane == 0) wsum[wid] = s;
+    __syncthreads();
+    total = 0.f;
+    for (int w = 0; w < kTpThreads / 64; ++w) total += wsum[w];
+    __syncthreads();
+  }
+  if (p < 1.f) {
+    const float target = p * total;
+    // inclusive prefix over the sorted list in chunks of kTpThreads
+    float carry = 0.f;
+    for (int base = 0; base < nk; base += kTpThreads) {
+      const int j = base + tid;
+      const float w = j < nk ? __expf((val[j] - M) * invT) : 0.f;
+      float incl = w;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) wsum[wid] = incl;
+      __syncthreads();
+      float before = carry;
+      for (int w2 = 0; w2 < wid; ++w2) before += wsum[w2];
+      const bool hit = j < nk && before + incl >= target;
+      const unsigned long long m = __ballot(hit);
+      if (m && lane == __ffsll((long long)m) - 1) atomicMin(&cutj, j);
+      float tot = 0.f;
+      for (int w2 = 0; w2 < kTpThreads / 64; ++w2) tot += wsum[w2];
+      __syncthreads();
+      carry += tot;
+      if (cutj < nk - 1 || carry >= target) break;
+    }
+    if (carry < target && cutj == nk - 1 && (k <= 0 || k >= V)) exact = false;  // nucleus beyond the list
+  }
+  __syncthreads();
+  if (tid == 0) cutv = val[cutj];
+  __syncthreads();
+  const float K = cutv;
+  if ((k <= 0 || k >= V) && !(K > kth_max)) exact = false;  // a token outside every list could tie / pass K
+  const uint64_t seed = (uint64_t)seeds[row];
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int j = tid; j < n; j += kTpThreads) {
+    if (val[j] < K || idx[j] >= V) continue;
+    best = argmax_merge(best, ArgMax{(val[j] - M) * invT + gumbel(seed, (uint64_t)step, (uint32_t)idx[j]), idx[j]});
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) best = argmax_merge(best, ArgMax{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)});
+  if (lane == 0) sv[wid] = best.v, si[wid] = best.i;
+  __syncthreads();
+  if (tid == 0) {
+    ArgMax b{sv[0], si[0]};
+    for (int w = 1; w < kTpThreads / 64; ++w) b = argmax_merge(b, ArgMax{sv[w], si[w]});
+    out_tokens[row] = b.i < V ? b.i : idx[0];
+    if (!exact && flags) atomicAdd(flags, 1);
+  }
+}
+
 // logits[b, t] -= freq * count + presence * (count > 0) for the tokens generated so far.
 // counts is a sparse list per row: tok_ids[b, j], tok_cnt[b, j] for j < n[b] (unique ids).
 __global__ void penalty_kernel(float* logits, long ld, const int* __restrict__ tok_ids,
@@ -746,6 +904,74 @@ void gai_sample(const float* logits, int B, int V, long ld, const float* tempera
   sample_split_resolve<<<B, kThreads, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part, cands,
                                                S, out_tokens);
   GAI_LAUNCH_CHECK();
+}
+
+// Per-row stats of a vocab shard for sample_tp_resolve: out[b] = {max, sum exp((x - max) / T), Gumbel-max of
+// x / T + G(seed, step, vstart + i) over the shard, its global id}. Shard columns >= V - vstart (vocab padding)
+// are ignored.
+__global__ __launch_bounds__(kTpThreads) void sample_tp_stats(const float* __restrict__ x, long ld, int Vl, int vstart,
+                                                              int V, const float* __restrict__ temperature,
+                                                              const int64_t* __restrict__ seeds, int64_t step,
+                                                              float* __restrict__ out) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* xr = x + (size_t)row * ld;
+  const int n = min(Vl, V - vstart);
+  float m = -INFINITY;
+  for (int i = tid; i < n; i += kTpThreads) m = fmaxf(m, xr[i]);
+  m = wave_max(m);
+  if (lane == 0) sv[wid] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
+  __syncthreads();
+  const float T = temperature[row];
+  const float invT = T > 0.f ? 1.f / T : 1.f;
+  const uint64_t seed = (uint64_t)seeds[row];
+  float s = 0.f;
+  ArgMax g{-INFINITY, 0x7fffffff};
+  for (int i = tid; i < n; i += kTpThreads) {
+    const float v = xr[i];
+    if (m > -INFINITY) s += __expf((v - m) * invT);
+    if (T > 0.f && v > -INFINITY)
+      g = argmax_merge(g, ArgMax{v * invT + gumbel(seed, (uint64_t)step, (uint32_t)(vstart + i)), vstart + i});
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) g = argmax_merge(g, ArgMax{__shfl_xor(g.v, o, 64), __shfl_xor(g.i, o, 64)});
+  __syncthreads();
+  if (lane == 0) sv[wid] = s, si[wid] = 0;
+  __syncthreads();
+  float st = sv[0] + sv[1] + sv[2] + sv[3];
+  __syncthreads();
+  if (lane == 0) sv[wid] = g.v, si[wid] = g.i;
+  __syncthreads();
+  if (tid == 0) {
+    ArgMax b{sv[0], si[0]};
+    for (int w = 1; w < kTpThreads / 64; ++w) b = argmax_merge(b, ArgMax{sv[w], si[w]});
+    out[row * 4 + 0] = m;
+    out[row * 4 + 1] = st;
+    out[row * 4 + 2] = b.v;
+    out[row * 4 + 3] = (float)(b.i == 0x7fffffff ? vstart : b.i);
+  }
+}
+
+void gai_sample_tp_stats(const float* x, long ld, int B, int Vl, int vstart, int V, const float* temperature,
+                         const int64_t* seeds, int64_t step, float* out, hipStream_t st) {
+  if (B == 0) return;
+  sample_tp_stats<<<B, kTpThreads, 0, st>>>(x, ld, Vl, vstart, V, temperature, seeds, step, out);
+  GAI_LAUNCH_CHECK();
+}
+
+int gai_sample_tp_resolve(const float* packets, int R, int B, int W, int C, int V, const float* temperature,
+                          const float* top_p, const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens,
+                          int* flags, hipStream_t st) {
+  if (B == 0) return 1;
+  if (R * C > kTpMaxCand || W < 4 + 2 * C) return 0;
+  sample_tp_resolve<<<B, kTpThreads, 0, st>>>(packets, R, B, W, C, V, temperature, top_p, top_k, seeds, step, out_tokens,
+                                              flags);
+  GAI_LAUNCH_CHECK();
+  return 1;
 }
 
 void gai_apply_penalties(float* logits, int B, long ld, const int* tok_ids, const int* tok_cnt, const int* n,

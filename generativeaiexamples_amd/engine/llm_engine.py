@@ -138,6 +138,11 @@ class LLMEngine:
         ctx = getattr(model, "ctx", None)
         self.tp_size = ctx.tp_size if ctx is not None else 1
         self.leader = self.tp_size == 1 or ctx.tp_rank == 0
+        # multi-step decode graphs hold only peer-memory collectives when the TP group has the custom all-reduce
+        # (the embedding / block-boundary all-reduces and sample_tp's candidate exchange), so they are captured
+        # even over a gloo control plane (one-GPU TP rehearsal, GAI_SINGLE_DEVICE=1)
+        self.multi_graphs_ok = cfg.use_graphs and (self.tp_size == 1 or ctx.backend == "nccl"
+                                                   or getattr(ctx, "custom_ar", None) is not None)
         if self.tp_size > 1 and self.device.type == "cuda" and ctx.backend != "nccl":
             cfg.use_graphs = False  # host (gloo) collectives, e.g. a one-GPU TP rehearsal, are not capturable
         if self.tp_size > 1 and hasattr(model, "register_request"):
@@ -190,6 +195,15 @@ class LLMEngine:
         if self.tp_size > 1:
             from ..parallel.step_channel import StepChannel
             self.chan = StepChannel(ctx)
+        # expert parallelism with data-parallel attention (MixtralModel ep_group): every rank runs its own
+        # requests, but each MoE layer is an all-to-all over the group, so the ranks step in LOCKSTEP: one
+        # small all-reduce per step agrees on the largest token count (the padded exchange's capacity) and
+        # on whether anyone prefills; a rank with nothing scheduled runs a one-token dummy forward
+        self.ep_group = getattr(model, "ep_group", None)
+        if self.ep_group is not None:
+            cfg.use_graphs = False
+            self.multi_graphs_ok = False
+            cfg.decode_steps = 1
 
     # ------------------------------------------------------------------ memory
     def _kv_layers(self) -> int:
@@ -281,7 +295,30 @@ class LLMEngine:
             self.model.release_request(sid)
 
     def has_work(self) -> bool:
-        return self._pending is not None or self.sched.has_work()
+        """EP lockstep engines: a collective over the EP group (True while ANY rank has work), so every rank
+        calls it, and step(), the same number of times."""
+        local = self._pending is not None or self.sched.has_work()
+        if self.ep_group is None:
+            return local
+        return bool(self._ep_agree([int(local)])[0])
+
+    def _ep_agree(self, vals: List[int]) -> List[int]:
+        import torch.distributed as dist
+
+        dev = self.device if dist.get_backend(self.ep_group) == "nccl" else torch.device("cpu")
+        t = torch.tensor(vals, dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ep_group)
+        return [int(v) for v in t.tolist()]
+
+    def _ep_dummy_forward(self) -> None:
+        """One decode row on the scratch page: keeps this rank in the step's all-to-alls."""
+        d = self.device
+        i32 = dict(dtype=torch.int32, device=d)
+        fb = ForwardBatch(token_ids=torch.zeros(1, **i32), positions=torch.zeros(1, **i32),
+                          slots=torch.full((1,), self.pad_block * ops.BLOCK, **i32), num_prefill_tokens=0,
+                          decode_ctx=torch.ones(1, **i32), decode_block_tables=torch.full((1, 1), self.pad_block, **i32),
+                          max_decode_ctx=1, sample_rows=None)
+        self.model.forward(fb, self.kv, self.decode_ws)
 
     # ------------------------------------------------------------------ batch construction
     def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
@@ -399,11 +436,12 @@ class LLMEngine:
     def capture_graphs(self, max_bs: Optional[int] = None):
         """Capture the decode graphs of every batch bucket <= max_bs. With TP, every rank calls this at the
         same point (the captures contain the collectives)."""
-        if self.device.type != "cuda" or not self.cfg.use_graphs:
+        if self.device.type != "cuda" or not (self.cfg.use_graphs or self.multi_graphs_ok):
             return
         for bs in self.cfg.graph_batch_sizes:
             if bs <= (max_bs or self.cfg.max_num_seqs):
-                self._capture(bs)
+                if self.cfg.use_graphs:
+                    self._capture(bs)
                 if self._multi_step_capable():
                     self._capture_multi(bs)
 
@@ -427,7 +465,9 @@ class LLMEngine:
         n_valid = torch.zeros(1, dtype=torch.int32, device=d)
         toks = torch.zeros(K, bs, dtype=torch.int32, device=d)
         fb = ForwardBatch(token_ids=ids, positions=pos, slots=slots, num_prefill_tokens=0, decode_ctx=ctx,
-                          decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None)
+                          decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None,
+                          tp_local_logits=self.tp_size > 1 and getattr(self.model, "supports_tp_sampling", False))
+        dctx = getattr(self.model, "ctx", None)
 
         def run():
             # every step first advances rows < n_valid from the previous sampled token: at j = 0 that is
@@ -435,11 +475,15 @@ class LLMEngine:
             for j in range(K):
                 ops.decode_advance(toks[(j - 1) % K], ids, pos, ctx, slots, bt, n_valid)
                 logits = self.model.forward(fb, self.kv, self.decode_ws)
-                ops.sample(logits, samp["temperature"], samp["top_p"], samp["top_k"], samp["seeds"], j,
-                           out=toks[j])
+                if fb.tp_local_logits:  # vocab-parallel logits: candidate exchange instead of a logits all-gather
+                    ops.sample_tp(logits, dctx, self.model.vstart, self.model.cfg.vocab_size, samp["temperature"],
+                                  samp["top_p"], samp["top_k"], samp["seeds"], j, out=toks[j])
+                else:
+                    ops.sample(logits, samp["temperature"], samp["top_p"], samp["top_k"], samp["seeds"], j,
+                               out=toks[j])
 
         g = None
-        if d.type == "cuda" and self.cfg.use_graphs:
+        if d.type == "cuda" and self.multi_graphs_ok:
             s = torch.cuda.Stream(device=d)
             s.wait_stream(torch.cuda.current_stream(d))
             with torch.cuda.stream(s):
@@ -702,6 +746,14 @@ class LLMEngine:
             b = self.sched.schedule()
             self._mark("schedule")
             n_tok = b.num_tokens
+            if self.ep_group is not None:
+                t_max, any_prefill = self._ep_agree([n_tok, int(b.num_prefill_tokens > 0)])
+                if t_max == 0:
+                    return []
+                self.model.ep_capacity_tokens, self.model.ep_exact = t_max, bool(any_prefill)
+                if n_tok == 0:
+                    self._ep_dummy_forward()
+                    return []
             if n_tok == 0:
                 return []
             self.step_count += 1

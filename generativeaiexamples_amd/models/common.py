@@ -36,6 +36,9 @@ class ForwardBatch:
     seq_ids: Optional[list] = None
     extra: Optional[dict] = None
     lora_slots: Optional[torch.Tensor] = None  # [T] int32 adapter slot per token (multi-LoRA), None = none
+    # TP models: return this rank's vocab shard of the logits (no all-gather); the caller samples with
+    # ops.sample_tp
+    tp_local_logits: bool = False
 
     @property
     def num_tokens(self) -> int:

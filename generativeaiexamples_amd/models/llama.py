@@ -174,6 +174,8 @@ class LlamaModel:
 
     supports_fp8_kv = True  # the attention path passes the KV cache's per-layer scales (EngineConfig.kv_cache_dtype)
 
+    supports_tp_sampling = True  # forward honours ForwardBatch.tp_local_logits (engine: ops.sample_tp)
+
     def __init__(self, cfg: LlamaConfig, device=None, dtype=torch.bfloat16, dist_ctx: DistContext | None = None):
         self.cfg = cfg
         self.ctx = dist_ctx or get_context()
@@ -564,12 +566,16 @@ class LlamaModel:
                     ctx.tp_all_reduce(h)
         if xn is not None:  # the final norm already ran inside the last layer's down projection
             logits = ops.linear(xn, w["lm_head"], out_dtype=torch.float32)
+            if fb.tp_local_logits and ctx.tp_size > 1:
+                return logits
             return ctx.tp_all_gather_last(logits)[:, : c.vocab_size]
         if fb.sample_rows is not None:
             h = h.index_select(0, fb.sample_rows)
             res = res.index_select(0, fb.sample_rows)
         x = self._norm(h, "norm", residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
+        if fb.tp_local_logits and ctx.tp_size > 1:
+            return logits
         logits = ctx.tp_all_gather_last(logits)
         return logits[:, : c.vocab_size]
 

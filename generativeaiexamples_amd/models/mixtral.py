@@ -5,11 +5,18 @@ Attention is the Llama block. The MLP is a top-2-of-8 mixture: router GEMM (fp32
 host sync) -> grouped GEMM w1|w3 with the SwiGLU epilogue gathering token rows -> grouped GEMM w2
 -> weighted combine (+ residual). 47B parameters = 94 GB bf16: fits ONE 288 GB MI355X.
 
-Expert parallelism: experts are sharded over the TP group (rank r owns experts
-[r*E/tp, (r+1)*E/tp)); hidden states are replicated by the attention all-reduce, so each rank
-computes only the (token, expert) pairs it owns and the row-parallel all-reduce sums the expert
-outputs - no extra collective. :mod:`..parallel.ep` provides the all-to-all dispatch/combine for
-data-parallel attention + EP.
+Expert parallelism, two modes:
+
+* TP mode (``dist_ctx`` with tp > 1): experts are sharded over the TP group (rank r owns experts
+  [r*E/tp, (r+1)*E/tp)); hidden states are replicated by the attention all-reduce, so each rank
+  computes only the (token, expert) pairs it owns and the row-parallel all-reduce sums the expert
+  outputs - no extra collective.
+* EP mode (``ep_group``): data-parallel attention (every rank holds attention / embeddings and serves
+  its own requests) + experts sharded over the EP group, tokens exchanged with all-to-all
+  (:mod:`..parallel.ep`): decode-sized steps use the fixed-capacity, sync-free padded exchange (capacity =
+  the step's largest per-rank token count, agreed by the engine's EP lockstep, ``LLMEngine``), prefill
+  steps the exact-count exchange. Ranks step in lockstep; a rank without work runs a one-token dummy
+  forward so every all-to-all has all its peers.
 """
 from __future__ import annotations
 
@@ -46,11 +53,25 @@ class MixtralConfig(LlamaConfig):
 class MixtralModel(LlamaModel):
     supports_fp8_kv = False  # own attention call sites (no per-layer KV scales)
 
+    def __init__(self, cfg, device=None, dtype=torch.bfloat16, dist_ctx=None, ep_group=None):
+        import torch.distributed as dist
+
+        self.ep_group = ep_group
+        self.ep_size = dist.get_world_size(ep_group) if ep_group is not None else 1
+        self.ep_rank = dist.get_rank(ep_group) if ep_group is not None else 0
+        self.ep_capacity_tokens = 0   # EP lockstep: the step's largest per-rank token count (set by the engine)
+        self.ep_exact = False         # EP lockstep: some rank prefills this step -> exact-count exchange
+        super().__init__(cfg, device, dtype, dist_ctx)
+
     def _alloc(self):
         c = self.cfg
-        tp, r = self.ctx.tp_size, self.ctx.tp_rank
-        assert c.num_experts % tp == 0, "experts must divide the TP/EP group"
-        self.e_local = c.num_experts // tp
+        if self.ep_group is not None:
+            assert self.ctx.tp_size == 1, "EP mode runs data-parallel attention (tp = 1)"
+            shards, r = self.ep_size, self.ep_rank
+        else:
+            shards, r = self.ctx.tp_size, self.ctx.tp_rank
+        assert c.num_experts % shards == 0, "experts must divide the TP/EP group"
+        self.e_local = c.num_experts // shards
         self.e_start = r * self.e_local
         # the dense MLP of LlamaModel is replaced by experts: allocate attention etc. via the parent,
         # then drop its MLP weights
@@ -67,7 +88,7 @@ class MixtralModel(LlamaModel):
             self.w[p + "w2"] = torch.empty(self.e_local, D, I, device=d, dtype=dt)
 
     def random_init(self, seed: int = 0):
-        s = seed * 1000 + self.ctx.tp_rank
+        s = seed * 1000 + self.ctx.tp_rank + 100 * self.ep_rank
         for k, t in self.w.items():
             if k.endswith("norm"):
                 t.fill_(1.0)
@@ -93,6 +114,8 @@ class MixtralModel(LlamaModel):
         logits = ops.linear(x, w[p + "router"], out_dtype=torch.float32)
         ids, wts = ops.moe_route(logits, c.top_k, True)
         k = c.top_k
+        if self.ep_group is not None:
+            return self._moe_ep(x, ids, wts, w[p + "w13"], w[p + "w2"], residual)
         if self.e_local != c.num_experts:  # EP: keep only local experts; others -> sentinel bin, weight 0
             loc = ids - self.e_start
             mine = (loc >= 0) & (loc < self.e_local)
@@ -105,6 +128,24 @@ class MixtralModel(LlamaModel):
         y = ops.moe_gemm(h1, None, w[p + "w2"], offs, T * k, swiglu=False) if self.e_local == c.num_experts else \
             self._moe_down_ep(h1, w[p + "w2"], offs, T * k)
         return ops.moe_combine(y, pos, wts, residual)
+
+    def _moe_ep(self, x, ids, wts, w13, w2, residual):
+        """All-to-all expert parallelism: pairs go to the rank owning their expert and come back weighted."""
+        from ..parallel import ep
+
+        c = self.cfg
+        if self.ep_exact:  # prefill-sized step somewhere in the group: exact counts (one host sync)
+            rows, eid, plan = ep.dispatch(x, ids, wts, c.num_experts, group=self.ep_group)
+            y = ep.local_experts(rows, eid, w13, w2)
+            out = ep.combine(y, wts, plan, group=self.ep_group)
+        else:  # decode: fixed capacity agreed for this step, no host sync (graph-capturable)
+            cap = max(self.ep_capacity_tokens, x.shape[0]) * c.top_k
+            rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group)
+            y = ep.local_experts_padded(rows, eid, w13, w2)
+            out = ep.combine_padded(y, wts, plan, group=self.ep_group)
+        if residual is not None:
+            out = out + residual
+        return out
 
     def _moe_down_ep(self, h1, w2, offs, rows):
         y = ops.moe_gemm(h1, None, w2, offs, rows, swiglu=False)
@@ -144,6 +185,8 @@ class MixtralModel(LlamaModel):
             res = res.index_select(0, fb.sample_rows)
         x = ops.rms_norm(h, w["norm"], c.rms_eps, residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
+        if fb.tp_local_logits and ctx.tp_size > 1:
+            return logits
         logits = ctx.tp_all_gather_last(logits)
         return logits[:, : c.vocab_size]
 

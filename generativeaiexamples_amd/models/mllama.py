@@ -178,6 +178,7 @@ class CrossCache:
 
 
 class MllamaModel(LlamaModel):
+    supports_tp_sampling = False  # own forward (cross-attention layers) returns gathered logits
     """Vision encoder + projector + Llama decoder with cross-attention layers (TP = 1)."""
 
     supports_fp8_kv = False  # own attention call sites (no per-layer KV scales)

@@ -35,7 +35,14 @@ class EPPlan:
     top_k: int
 
 
+def _host_plane(x: torch.Tensor, group) -> bool:
+    """Device tensors over a gloo group (one-GPU multi-rank rehearsal): exchange through host memory."""
+    return x.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def _a2a(x: torch.Tensor, send: List[int], recv: List[int], group) -> torch.Tensor:
+    if _host_plane(x, group):
+        return _a2a(x.cpu(), send, recv, group).to(x.device)
     out = torch.empty(sum(recv), *x.shape[1:], dtype=x.dtype, device=x.device)
     if x.is_cuda or x.dtype in (torch.float32, torch.int64, torch.int32):
         dist.all_to_all_single(out, x.contiguous(), recv, send, group=group)
@@ -56,7 +63,12 @@ def dispatch(x: torch.Tensor, ids: torch.Tensor, weights: torch.Tensor, num_expe
     order = torch.argsort(dest, stable=True)
     send_counts = torch.bincount(dest, minlength=world)
     recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    if _host_plane(send_counts, group):
+        rc = torch.empty(world, dtype=send_counts.dtype)
+        dist.all_to_all_single(rc, send_counts.cpu(), group=group)
+        recv_counts = rc
+    else:
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
     sc, rc = send_counts.tolist(), recv_counts.tolist()
     rows = x[(order // k)]
     eid = (flat[order] % e_local).to(torch.int32)
@@ -103,6 +115,8 @@ class EPPaddedPlan:
 
 
 def _a2a_equal(x: torch.Tensor, group) -> torch.Tensor:
+    if _host_plane(x, group):
+        return _a2a_equal(x.cpu(), group).to(x.device)
     out = torch.empty_like(x)
     if x.is_cuda or x.dtype in (torch.float32, torch.int64, torch.int32):
         dist.all_to_all_single(out, x.contiguous(), group=group)

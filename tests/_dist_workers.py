@@ -659,3 +659,98 @@ def tp_linear_overlap_worker(rank, world, port, out_dir):
     torch.save(res, os.path.join(out_dir, f"ovl_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def tp_graph_rehearsal_worker(rank, world, port, out_dir):
+    """One-GPU rehearsal of a TP=world decode (every rank on cuda:0, gloo control plane): the multi-step
+    decode graph holds only peer-memory collectives (custom all-reduce for the embedding / block-boundary
+    reductions and ops.sample_tp's candidate exchange), is captured on every rank and replayed in lockstep
+    through pipelined (chained) runs. Rank 0 compares the greedy tokens with a TP=1 engine."""
+    import json
+
+    os.environ.update(GAI_SINGLE_DEVICE="1", GAI_CUSTOM_AR="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    from generativeaiexamples_amd.parallel import dist as gdist
+
+    ctx = gdist.init_distributed(tp_size=world, backend="gloo")
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd import ops
+
+    err = None
+    try:
+        assert ctx.custom_ar is not None, "custom all-reduce not created"
+        cfg = LlamaConfig.tiny(num_heads=8, num_kv_heads=8, head_dim=64, hidden_size=512, intermediate_size=1024,
+                               vocab_size=4096)
+        ref = LlamaModel(cfg, device="cuda", dist_ctx=DistContext()).random_init(17)
+        m = LlamaModel(cfg, device="cuda", dist_ctx=ctx).load_hf_state(ref.export_hf_state())
+        tok = small_byte_tokenizer(4096)
+        ecfg = dict(num_blocks=128, max_model_len=256, use_graphs=True, decode_steps=4, max_num_seqs=8,
+                    graph_batch_sizes=(1, 2, 4, 8), prefix_cache=False, kv_memory_fraction=0.02)
+        eng = LLMEngine(m, tok, EngineConfig(**ecfg))
+        eng.capture_graphs(max_bs=8)
+        if not eng.leader:
+            assert eng.follow() == "stop"
+        else:
+            prompts = [list(range(11 + 3 * i, 11 + 3 * i + n)) for i, n in enumerate((9, 23, 40, 5, 17))]
+            sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
+            tp = eng.generate(prompts, sp)
+            stats = dict(eng.stats)
+            eng.release_followers(stop=True)
+            r1 = LLMEngine(ref, tok, EngineConfig(**ecfg))
+            r1.capture_graphs(max_bs=8)
+            one = r1.generate(prompts, sp)
+            a = [r.output_ids for r in tp]
+            b = [r.output_ids for r in one]
+            same = sum(x == y for ra, rb in zip(a, b) for x, y in zip(ra, rb))
+            with open(os.path.join(out_dir, "tpg.json"), "w") as f:
+                json.dump({"tp": a, "ref": b, "same": same, "total": sum(len(x) for x in a), "stats": stats,
+                           "multi_graphs": sorted(eng.multi_graphs), "flags": int(ops.tp_sample_flags(m.device))}, f)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        err = traceback.format_exc()
+        with open(os.path.join(out_dir, f"tpg_err_{rank}.txt"), "w") as f:
+            f.write(err)
+    finally:
+        gdist.shutdown()
+    if err:
+        raise SystemExit(1)
+
+
+def ep_engine_worker(rank, world, port, out_dir):
+    """Data-parallel attention + expert parallelism (MixtralModel ep_group, all-to-all token exchange): each
+    rank serves its OWN requests (different counts and lengths, so ranks run dummy lockstep steps) with 8 / world
+    experts; its greedy tokens must equal a single-process Mixtral's on the same prompts (fp32)."""
+    import json
+
+    ctx = _init(rank, world, port, 1)
+    import torch.distributed as dist
+
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.mixtral import MixtralConfig, MixtralModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+
+    cfg = MixtralConfig.tiny_moe(num_experts=8)
+    ref = MixtralModel(cfg, device="cpu", dtype=torch.float32, dist_ctx=DistContext()).random_init(3)
+    m = MixtralModel(cfg, device="cpu", dtype=torch.float32, dist_ctx=ctx, ep_group=dist.group.WORLD)
+    with torch.no_grad():
+        for k, t in m.w.items():
+            src = ref.w[k]
+            if k.endswith("w13") or k.endswith("w2"):
+                src = src[m.e_start:m.e_start + m.e_local]
+            t.copy_(src)
+    tok = small_byte_tokenizer(512)
+    prompts = [list(range(5 + 7 * rank + 3 * i, 5 + 7 * rank + 3 * i + 6 + 9 * ((i + rank) % 3))) for i in range(rank + 1)]
+    sp = SamplingParams(temperature=0.0, max_tokens=5 + 3 * rank, ignore_eos=True)
+    ecfg = dict(num_blocks=96, max_model_len=256, use_graphs=False, max_num_seqs=8, max_batched_tokens=64,
+                prefill_chunk=32, prefix_cache=False)
+    eng = LLMEngine(m, tok, EngineConfig(**ecfg))
+    ep = [r.output_ids for r in eng.generate(prompts, sp)]
+    one = [r.output_ids for r in LLMEngine(ref, tok, EngineConfig(**ecfg)).generate(prompts, sp)]
+    with open(os.path.join(out_dir, f"ep_{rank}.json"), "w") as f:
+        json.dump({"ep": ep, "ref": one, "e_local": m.e_local, "steps": eng.stats["steps"]}, f)
+    dist.barrier()
+    dist.destroy_process_group()

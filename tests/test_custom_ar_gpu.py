@@ -1,5 +1,5 @@
 """One-shot peer-memory all-reduce (csrc/comm/custom_ar.hip, parallel/custom_ar.py) on a one-GPU
-box: 2 and 4 ranks share cuda:0 and exchange IPC handles over gloo; the result must equal the
+box: 2, 4 and 8 ranks (the Llama-3-70B TP8 instantiation) share cuda:0 and exchange IPC handles over gloo; the result must equal the
 fp32 sum of every rank's input (eager and HIP-graph replay). Multi-GPU xGMI runs go through the
 same kernel with peers on other devices."""
 import json
@@ -21,7 +21,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_matches_sum(tmp_path, world, cuda):
     ctx = mp.get_context("spawn")
     port = _port()

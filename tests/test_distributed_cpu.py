@@ -4,6 +4,7 @@
   all-reduces) reproduces the single-process logits;
 * the DP-sharded index (all-gather of queries and candidates + merge) equals a global exact top-k.
 """
+import json
 import socket
 
 import pytest
@@ -111,3 +112,14 @@ def test_tp_linear_all_reduce_overlap(tmp_path):
         d = torch.load(tmp_path / f"ovl_{r}.pt", weights_only=True)
         assert d["torch.float32"] < 1e-4
         assert d["torch.bfloat16"] < 1e-2
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ep_engine_matches_single_rank(tmp_path, world):
+    """Mixtral EP mode: DP attention + experts over the ranks with all-to-all exchange, lockstep steps (ranks
+    own different request sets): every rank's greedy tokens equal the single-process model's."""
+    mp.spawn(W.ep_engine_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        d = json.loads((tmp_path / f"ep_{r}.json").read_text())
+        assert d["e_local"] == 8 // world
+        assert d["ep"] == d["ref"], (r, d)

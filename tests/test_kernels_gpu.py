@@ -451,3 +451,47 @@ def test_sample_split_is_faster(cuda):
     t_row = timed(lambda: nat.sample(logits, temp, top_p, top_k, seeds, 1, out))
     print(f"sampler B=64 V=128256: split {t_split:.1f} us, whole-row {t_row:.1f} us")
     assert t_split < t_row
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_sample_tp_candidates_match_whole_row(cuda, R):
+    """Vocab-parallel sampling (ops.sample_tp): R shard packets (stats + top-64 candidates) resolved by
+    sample_tp_resolve must give the whole-row sampler's token for the same (seed, step): greedy, top-p,
+    top-k, top-k + top-p and pure temperature rows. The shards are simulated on one GPU (the gather is a
+    plain sum of zero-padded packets, what the TP all-reduce computes)."""
+    from generativeaiexamples_amd.ops import native
+
+    torch.manual_seed(31 + R)
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=cuda) * 1.28
+    logits[3, 77] = 30.0
+    temp = torch.full((B,), 0.2, device=cuda)
+    temp[:4] = 0.0
+    top_p = torch.full((B,), 0.7, device=cuda)
+    top_p[40:48] = 1.0  # pure temperature (exact via the shard Gumbel maxima)
+    temp[40:48] = 1.0
+    top_k = torch.zeros(B, dtype=torch.int32, device=cuda)
+    top_k[20:30] = 40
+    seeds = torch.arange(B, dtype=torch.int64, device=cuda) + 5
+    vl = -(-V // R)
+    pad = torch.full((B, vl * R - V), float("-inf"), device=cuda)
+    full = torch.cat([logits, pad], 1)
+    C = 64
+    W = (4 + 2 * C + 3) // 4 * 4
+    nat = native()
+    for step in range(4):
+        buf = torch.zeros(R, B, W, device=cuda)
+        for r in range(R):
+            sh = full[:, r * vl:(r + 1) * vl].contiguous()
+            n = min(vl, V - r * vl)
+            nat.sample_tp_stats(sh, r * vl, V, temp, seeds, step, buf[r, :, :4])
+            v, i = torch.topk(sh[:, :n], C, dim=-1)
+            buf[r, :, 4:4 + C] = v
+            buf[r, :, 4 + C:4 + 2 * C] = (i + r * vl).float()
+        got = torch.empty(B, dtype=torch.int32, device=cuda)
+        flags = torch.zeros(1, dtype=torch.int32, device=cuda)
+        nat.sample_tp_resolve(buf, C, V, temp, top_p, top_k, seeds, step, got, flags)
+        want = ops.sample(logits, temp, top_p, top_k, seeds, step)
+        assert torch.equal(got[:4], logits[:4].argmax(-1).int())
+        agree = int((got == want).sum())
+        assert agree >= B - 2, (step, agree, (got != want).nonzero().flatten().tolist(), int(flags))

@@ -1,0 +1,46 @@
+"""TP=2/4/8 decode captured in HIP graphs on ONE GPU: every rank shares
+cuda:0 over a gloo control plane; the only collectives inside the multi-step decode graph are the
+peer-memory custom all-reduce kernels (including ops.sample_tp's candidate exchange, which replaces the
+[B, vocab] logits all-gather). Greedy tokens must match a TP=1 engine (bf16 partial-sum order may flip a
+near-tie, so >= 95 % of positions must agree and every first token must)."""
+import json
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from tests import _dist_workers as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=W.tp_graph_rehearsal_worker, args=(r, world, port, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(110)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errs = [f.read_text() for f in tmp_path.glob("tpg_err_*.txt")]
+    assert not errs, errs[0]
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = json.loads((tmp_path / "tpg.json").read_text())
+    print(f"TP={world}: {res['same']}/{res['total']} tokens equal TP=1, stats {res['stats']}, flags {res['flags']}")
+    assert res["multi_graphs"], "no multi-step decode graph captured"
+    assert res["stats"]["graph_steps"] > 0 and res["stats"]["chained_runs"] > 0
+    assert all(a[0] == b[0] for a, b in zip(res["tp"], res["ref"]))
+    assert res["same"] >= 0.95 * res["total"]
