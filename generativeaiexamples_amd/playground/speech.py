@@ -12,9 +12,10 @@ built at import time from descriptors (google.protobuf, grpcio):
 * ``/nvidia.riva.tts.RivaSpeechSynthesis/SynthesizeOnline`` - server stream of int16 PCM chunks; long
   answers are split at ~300 characters on word boundaries (the reference's 400-character Riva limit).
 
-Field numbers follow the public Riva protos as remembered here: wire compatibility with a real Riva
-server is unverified offline (parity unpinned); the client / test server pair in tests/test_speech_cpu.py
-pins the behaviour. The backend is pluggable (:class:`SpeechBackend`): ``RIVA_API_URI`` selects
+The ASR messages are pinned field by field against the reference's riva_asr.proto
+(community/pdfspeak/.../riva_proto/riva_asr.proto, tests/test_speech_cpu.py); the reference ships no TTS
+proto, so the TTS field numbers remain parity-unpinned. The client / test server pair in
+tests/test_speech_cpu.py pins the behaviour. The backend is pluggable (:class:`SpeechBackend`): ``RIVA_API_URI`` selects
 :class:`RivaBackend`; without it the speech routes report that speech is unavailable, as the reference
 does when no Riva server answers.
 """

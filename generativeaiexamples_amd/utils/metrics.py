@@ -51,11 +51,16 @@ class Metrics:
             self.queue = Gauge("gai_waiting_requests", "requests waiting for admission", registry=r)
             self.collective = Histogram("gai_collective_seconds", "host-observed collective latency", ["op"],
                                         buckets=(1e-5, 1e-4, 1e-3, 1e-2, 0.1, 1.0), registry=r)
+            self.hbm_used = Gauge("gai_gpu_hbm_used_bytes", "HBM in use on the device (all processes)", ["gpu"],
+                                  registry=r)
+            self.hbm_total = Gauge("gai_gpu_hbm_total_bytes", "HBM capacity of the device", ["gpu"], registry=r)
+            self.hbm_allocated = Gauge("gai_gpu_hbm_allocated_bytes", "HBM held by this process's tensors", ["gpu"],
+                                       registry=r)
         else:  # pragma: no cover
             self.registry = None
             for n in ("requests_total", "prompt_tokens", "generation_tokens", "ttft", "e2e", "step", "batch",
                       "kv_usage", "embed", "search", "rerank", "api_requests", "tpot", "prefill_tokens",
-                      "decode_tokens", "queue", "collective"):
+                      "decode_tokens", "queue", "collective", "hbm_used", "hbm_total", "hbm_allocated"):
                 setattr(self, n, _Null())
 
     def observe_step(self, dt: float, n: int, engine=None):
@@ -79,7 +84,23 @@ class Metrics:
             except Exception:  # pragma: no cover - scheduler without counters
                 pass
 
+    def update_hbm(self) -> None:
+        """Per-GPU HBM gauges (used / total from the driver, allocated by this process's caching allocator)."""
+        try:
+            import torch
+
+            if not torch.cuda.is_available():
+                return
+            for i in range(torch.cuda.device_count()):
+                free, total = torch.cuda.mem_get_info(i)
+                self.hbm_used.labels(gpu=str(i)).set(total - free)
+                self.hbm_total.labels(gpu=str(i)).set(total)
+                self.hbm_allocated.labels(gpu=str(i)).set(torch.cuda.memory_allocated(i))
+        except Exception:  # pragma: no cover - device query failures never break /metrics
+            pass
+
     def render(self) -> bytes:
+        self.update_hbm()
         return generate_latest(self.registry) if self.registry is not None else b""
 
 

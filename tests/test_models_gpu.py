@@ -173,3 +173,12 @@ def test_fused_add_rmsnorm_decode_matches(cuda, monkeypatch):
         outs[flag] = g.forward(fb, eng2.kv, eng2.decode_ws).float().cpu()
     assert outs["1"].shape[0] == len(prompts)
     assert (outs["1"] - outs["0"]).abs().max().item() < 0.02 * outs["0"].abs().max().item() + 0.02
+
+
+def test_metrics_expose_per_gpu_hbm(cuda):
+    from generativeaiexamples_amd.utils.metrics import METRICS
+
+    txt = METRICS.render().decode()
+    line = next(ln for ln in txt.splitlines() if ln.startswith('gai_gpu_hbm_total_bytes{gpu="0"}'))
+    assert float(line.split()[-1]) > 1e11  # 288 GB HBM3E
+    assert 'gai_gpu_hbm_used_bytes{gpu="0"}' in txt and 'gai_gpu_hbm_allocated_bytes{gpu="0"}' in txt

@@ -120,3 +120,40 @@ def test_playground_speech_routes(riva):
     off = TestClient(create_app("http://x", "m", client=NoChain(), speech=S.SpeechBackend()))
     assert off.get("/api/speech/status").json()["asr"] is False
     assert off.post("/api/speech/tts", json={"text": "x"}).status_code == 503
+
+
+def test_asr_messages_match_reference_proto():
+    """Pin the hand-built Riva ASR messages against the reference's riva_asr.proto (field numbers by name):
+    every ASR field this client sends or reads must carry the proto's number."""
+    import os
+    import re
+
+    import pytest
+
+    from generativeaiexamples_amd.playground.speech import MSG
+
+    path = ("/root/reference/community/pdfspeak/webapp/src/main/ui/web/pdf-speak/server/modules/protos/src/"
+            "riva_proto/riva_asr.proto")
+    if not os.path.exists(path):
+        pytest.skip("reference proto not available")
+    src = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    fields = {}
+    for m in re.finditer(r"\bmessage\s+(\w+)\s*\{", src):
+        depth, i = 1, m.end()
+        while depth and i < len(src):
+            depth += {"{": 1, "}": -1}.get(src[i], 0)
+            i += 1
+        body = src[m.end():i - 1]
+        body = re.sub(r"\bmessage\s+\w+\s*\{.*?\}", "", body, flags=re.S)  # nested messages are their own entries
+        fields[m.group(1)] = {f: int(n) for f, n in re.findall(r"(\w+)\s*=\s*(\d+)\s*;", body)}
+    asr = ["RecognitionConfig", "StreamingRecognitionConfig", "StreamingRecognizeRequest",
+           "SpeechRecognitionAlternative", "StreamingRecognitionResult", "StreamingRecognizeResponse"]
+    checked = 0
+    for name in asr:
+        assert name in fields, name
+        for f in MSG[name].DESCRIPTOR.fields:
+            assert f.name in fields[name], (name, f.name)
+            assert fields[name][f.name] == f.number, (name, f.name, f.number, fields[name][f.name])
+            checked += 1
+    assert checked >= 15
