@@ -11,6 +11,7 @@
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from concurrent.futures import Future
@@ -50,6 +51,52 @@ class Embedder:
         self.sep_id = tokenizer.token_id("[SEP]") if tokenizer.token_id("[SEP]") is not None else (
             tokenizer.eos_ids[0] if tokenizer.eos_ids else None)
         self.lock = threading.Lock()
+        # query-sized batches (<= 64 sequences of <= 128 tokens) replay a captured HIP graph per (B, L) bucket:
+        # the 24-layer e5-large forward of one query is ~250 launches, launch-bound without the graph
+        self.use_graphs = model.device.type == "cuda" and os.environ.get("GAI_EMBED_GRAPHS", "1") == "1"
+        self._graphs: dict = {}
+
+    GRAPH_B = (1, 2, 4, 8, 16, 32, 64)
+    GRAPH_L = (32, 64, 128)
+
+    def _graph_for(self, B: int, L: int):
+        key = (B, L)
+        if key not in self._graphs:
+            from ..models.common import PackedAttention
+
+            m, dev = self.model, self.model.device
+            c = m.cfg
+            ids = torch.zeros(B * L, dtype=torch.int32, device=dev)
+            lens = torch.full((B,), L, dtype=torch.int32, device=dev)
+            attn = PackedAttention([L] * B, c.num_heads, c.head_dim_padded, dev, m.dtype)
+            attn.ctx = lens  # the key count per sequence IS the real length (keys past it are masked)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                m.embed_padded(ids, lens, attn, B, L)  # warm-up (allocator, kernel attributes)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                out = m.embed_padded(ids, lens, attn, B, L)
+            self._graphs[key] = (g, ids, lens, out)
+        return self._graphs[key]
+
+    def _embed_graphed(self, seqs: List[List[int]]) -> "torch.Tensor | None":
+        n, longest = len(seqs), max(len(x) for x in seqs)
+        B = next((b for b in self.GRAPH_B if b >= n), None)
+        L = next((x for x in self.GRAPH_L if x >= longest), None)
+        if B is None or L is None:
+            return None
+        g, ids, lens, out = self._graph_for(B, L)
+        flat = torch.zeros(B, L, dtype=torch.int32)
+        ln = torch.ones(B, dtype=torch.int32)
+        for i, x in enumerate(seqs):
+            flat[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
+            ln[i] = len(x)
+        ids.copy_(flat.view(-1), non_blocking=True)
+        lens.copy_(ln, non_blocking=True)
+        g.replay()
+        return out[:n].clone()
 
     def tokenize(self, text: str, input_type: str = "passage", truncate: str = "END") -> List[int]:
         body = self.tok.encode(self.prefix.get(input_type, "") + text)
@@ -65,6 +112,11 @@ class Embedder:
     def embed_ids(self, seqs: List[List[int]]) -> torch.Tensor:
         """Token id lists -> fp32 [B, D] on the model device (input order preserved)."""
         dev = self.model.device
+        if self.use_graphs and seqs:
+            with self.lock:
+                o = self._embed_graphed(seqs)
+            if o is not None:
+                return o
         order = sorted(range(len(seqs)), key=lambda i: len(seqs[i]))
         out = torch.empty(len(seqs), self.dim, dtype=torch.float32, device=dev)
         i = 0

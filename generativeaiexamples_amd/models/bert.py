@@ -230,12 +230,13 @@ class BertModel:
 
     # ---------------------------------------------------------------------------- forward
     def encode_hidden(self, ids: torch.Tensor, cu_seqlens: torch.Tensor, seq_lens: List[int],
-                      type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """ids [T] int32 (varlen packed), cu_seqlens [B+1] int32 (device), seq_lens host list -> hidden [T, D]."""
+                      type_ids: Optional[torch.Tensor] = None, attn: Optional[PackedAttention] = None) -> torch.Tensor:
+        """ids [T] int32 (varlen packed), cu_seqlens [B+1] int32 (device), seq_lens host list -> hidden [T, D].
+        ``attn``: a prebuilt attention plan (the padded HIP-graph path, :meth:`embed_padded`)."""
         c, w = self.cfg, self.w
         T, D, H, hp = ids.numel(), c.hidden_size, c.num_heads, c.head_dim_padded
         dev = ids.device
-        attn = PackedAttention(seq_lens, H, hp, dev, self.dtype)
+        attn = attn if attn is not None else PackedAttention(seq_lens, H, hp, dev, self.dtype)
         pos = attn.positions  # restart at 0 for every sequence
         h = ops.embedding(ids, w["word"])
         h = h + w["pos"][pos.long()]
@@ -257,6 +258,25 @@ class BertModel:
         """Pooled (and L2-normalised) sentence embeddings, fp32 [B, D]."""
         h = self.encode_hidden(ids, cu_seqlens, seq_lens)
         return ops.pool(h, cu_seqlens, self.cfg.pooling, self.cfg.normalize)
+
+    # ---- fixed-shape query encoder (HIP graphs): B sequences padded to L tokens each
+    def embed_padded(self, ids: torch.Tensor, lens: torch.Tensor, attn: PackedAttention, B: int, L: int) -> torch.Tensor:
+        """ids [B*L] (sequence b in rows [bL, bL + lens[b]), padding after), lens [B] int32 on the device,
+        ``attn`` built for q_lens = [L] * B whose ``ctx`` tensor holds ``lens``: every query row attends to the
+        real keys of its sequence only (the kernel masks keys >= ctx), so real rows equal the packed forward;
+        pooling runs over the real rows. All shapes are fixed: capturable once per (B, L) bucket."""
+        c = self.cfg
+        h = self.encode_hidden(ids, attn.cu_q, [L] * B, attn=attn).view(B, L, -1).float()
+        if c.pooling == "cls":
+            o = h[:, 0]
+        elif c.pooling == "last":
+            o = h[torch.arange(B, device=h.device), (lens.long() - 1).clamp_min(0)]
+        else:
+            m = (torch.arange(L, device=h.device)[None, :] < lens[:, None]).float()
+            o = (h * m[..., None]).sum(1) / lens.clamp_min(1)[:, None].float()
+        if c.normalize:
+            o = torch.nn.functional.normalize(o, dim=-1, eps=1e-12)
+        return o
 
     def score(self, ids, cu_seqlens, seq_lens, type_ids=None) -> torch.Tensor:
         """Cross-encoder relevance logits [B] (CLS -> dense+tanh -> classifier)."""

@@ -182,3 +182,20 @@ def test_metrics_expose_per_gpu_hbm(cuda):
     line = next(ln for ln in txt.splitlines() if ln.startswith('gai_gpu_hbm_total_bytes{gpu="0"}'))
     assert float(line.split()[-1]) > 1e11  # 288 GB HBM3E
     assert 'gai_gpu_hbm_used_bytes{gpu="0"}' in txt and 'gai_gpu_hbm_allocated_bytes{gpu="0"}' in txt
+
+
+def test_query_embed_graph_matches_packed(cuda):
+    """Query-sized batches replay a captured fixed-shape (B, L) encoder graph (padded rows, keys masked by the
+    real length): embeddings must equal the packed varlen path."""
+    cfg = BertConfig.tiny()
+    m = BertModel(cfg, device=cuda).random_init(4)
+    emb = Embedder(m, bert_byte_tokenizer(cfg.vocab_size))
+    qs = [f"what is question {i} about" + " x" * (3 * i) for i in range(5)]
+    assert emb.use_graphs
+    a = emb.embed(qs, "query")
+    assert emb._graphs, "graph path not taken"
+    emb.use_graphs = False
+    b = emb.embed(qs, "query")
+    assert torch.allclose(a, b, atol=2e-2), (a - b).abs().max()
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert bool((cos > 0.999).all()), cos
