@@ -240,10 +240,11 @@ void sample_tp_stats(const Tensor& logits, int64_t vstart, int64_t V, const Tens
   check_f32(temperature, "temperature");
   TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
   check_f32(out, "out");
-  TORCH_CHECK(out.is_contiguous() && out.numel() >= logits.size(0) * 4, "out must hold [B, 4] floats");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= logits.size(0) && out.size(1) >= 4 && out.stride(1) == 1,
+              "out must be a [B, >=4] float view with unit column stride");
   gai_sample_tp_stats(logits.data_ptr<float>(), logits.stride(0), logits.size(0), logits.size(1), (int)vstart, (int)V,
                       temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), step, out.data_ptr<float>(),
-                      cur_stream());
+                      out.stride(0), cur_stream());
 }
 
 int64_t sample_ws_bytes(int64_t B, int64_t V) { return (int64_t)gai_sample_ws_bytes((int)B, (int)V);

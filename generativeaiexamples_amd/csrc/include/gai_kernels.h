@@ -72,7 +72,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
 // sampling.hip
 size_t gai_sample_ws_bytes(int B, int V);
 void gai_sample_tp_stats(const float* x, long ld, int B, int Vl, int vstart, int V, const float* temperature,
-                         const int64_t* seeds, int64_t step, float* out, hipStream_t st);
+                         const int64_t* seeds, int64_t step, float* out, long ostride, hipStream_t st);
 int gai_sample_tp_resolve(const float* packets, int R, int B, int W, int C, int V, const float* temperature,
                           const float* top_p, const int* top_k, const int64_t* seeds, int64_t step, int* out_tokens,
                           int* flags, hipStream_t st);

@@ -356,20 +356,38 @@ bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, cons
 
 namespace {
 
-// K split for the partial-slab mode: the smallest KS (2..16) whose per-workgroup K range fits the
-// unrolled loop and that gives >= 192 workgroups (a K range per CU long enough to stream, few slabs).
+// K split for the partial-slab mode. Preferred: a KS giving EXACTLY a multiple of 256 workgroups (every CU
+// streams; down at N = 4096: NT = 4 x KS = 4 = 256), else the smallest KS (2..16) whose per-workgroup K range
+// fits the unrolled loop and that gives >= 192 workgroups (a K range per CU long enough to stream, few slabs;
+// NT = 8 x KS = 7 = 224, 1/8 of the CUs idle).
 template <int MB>
-int dec2_part_ks(int N, int K, int NT) {
+int dec2_part_ks(int N, int K, int NT, bool exact) {
   const int blocks = (N + 16 * NT - 1) / (16 * NT);
-  for (int KS = 2; KS <= 16; ++KS)
-    if (K % KS == 0 && (K / KS) % 32 == 0 && dec2_shape_ok<MB>(NT, K / KS) && blocks * KS >= 192) return KS;
+  for (int KS = 2; KS <= 16; ++KS) {
+    if (K % KS || (K / KS) % 32 || !dec2_shape_ok<MB>(NT, K / KS)) continue;
+    if (exact ? (blocks * KS) % 256 == 0 : blocks * KS >= 192) return KS;
+  }
   return 0;
+}
+
+// GAI_DEC2_PART_NT = 4 | 8 forces the column tile; default: the 256-exact NT = 4 split when it exists
+int dec2_part_nt_env() {
+  static const int v = getenv("GAI_DEC2_PART_NT") ? atoi(getenv("GAI_DEC2_PART_NT")) : 0;
+  return v;
 }
 
 template <int MB>
 int dec2_part_run(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
+  const int force = dec2_part_nt_env();
+  if (MB > 1 && force != 8) {
+    const int KS4 = dec2_part_ks<MB>(N, K, 4, force != 4);
+    if (KS4) {
+      if (launch) dec2_launch<MB, 4, EPI_NONE, true, true>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS4, ws);
+      return KS4;
+    }
+  }
   constexpr int NT = MB == 1 ? 4 : 8;
-  const int KS = dec2_part_ks<MB>(N, K, NT);
+  const int KS = dec2_part_ks<MB>(N, K, NT, false);
   if (KS && launch) dec2_launch<MB, NT, EPI_NONE, true, true>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS, ws);
   return KS;
 }

@@ -351,10 +351,11 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restric
 // Split-row sampler (V >= kSplitMinV). One workgroup per row leaves 3/4 of the chip idle at batch 64 and
 // streams each 513 KB row through one CU (~125 us per decode step at B = 64, V = 128256). Here:
 //  1. split_stats   grid (S, B), 256 threads, kChunk logits per workgroup held in registers: chunk max,
-//                   argmax, sum exp((x - max) / T); for pure-temperature rows also the chunk's Gumbel-max.
-//  2. split_cands   grid (S, B): the row max M from the S partials, then every element of the chunk with
-//                   (M - x) / T < kCut (the same candidate set as nucleus_fast) compacted to global slots.
-//  3. resolve       grid B, 1024 threads: the row's softmax mass from the partials, the candidates in LDS,
+//                   argmax, sum exp((x - max) / T); for pure-temperature rows the chunk's Gumbel-max, otherwise
+//                   every element within kCut temperatures of the CHUNK max compacted to global slots (one pass
+//                   over the logits: the row max is not known yet);
+//  2. resolve       grid B, 1024 threads: the row's softmax mass from the partials, the candidates within kCut
+//                   of the ROW max (nucleus_fast's set) gathered from the chunks that can hold any, in LDS,
 //                   count-radix top-k / mass-radix top-p cut on the candidates, Gumbel-max over the
 //                   survivors. Rows whose cut is not decidable on the candidates (top-k beyond them, a
 //                   nucleus reaching past kCut, > kSlot candidates in a chunk) take sample_row_full.
@@ -367,14 +368,20 @@ constexpr int kPartW = 8;      // words per (row, split) partial: max, sum, argm
 
 __device__ __forceinline__ int nsplit(int V) { return (V + kChunk - 1) / kChunk; }
 
+__device__ __forceinline__ bool split_needs_cands(float T, float p, int k, int V) {
+  return T > 0.f && (p < 1.f || (k > 0 && k < V));
+}
+
 __global__ __launch_bounds__(kSplitT) void sample_split_stats(const float* __restrict__ logits, int V, long ld,
                                                               const float* __restrict__ temperature,
                                                               const float* __restrict__ top_p,
                                                               const int* __restrict__ top_k,
                                                               const int64_t* __restrict__ seeds, int64_t step,
-                                                              float* __restrict__ part) {
+                                                              float* __restrict__ part,
+                                                              uint64_t* __restrict__ cands) {
   __shared__ float sv[8];
   __shared__ int si[8];
+  __shared__ int cnt;
   const int row = blockIdx.y, sp = blockIdx.x, S = gridDim.x, tid = threadIdx.x;
   const int c0 = sp * kChunk;
   const float* x = logits + (size_t)row * ld;
@@ -430,9 +437,35 @@ __global__ __launch_bounds__(kSplitT) void sample_split_stats(const float* __res
     float t = 0.f;
     for (int w = 0; w < kSplitT / 64; ++w) t += sv[w];
     pw[0] = m, pw[1] = t, pw[2] = __int_as_float(am.i);
+    cnt = 0;
   }
   const int k = top_k[row];
-  if (top_p[row] < 1.f || (k > 0 && k < V)) return;
+  if (split_needs_cands(T, top_p[row], k, V)) {
+    // candidates relative to THIS chunk's max (the values are still in registers: one pass over the logits);
+    // the resolve kernel keeps those within kCut temperatures of the row max, i.e. nucleus_fast's set
+    __syncthreads();
+    uint64_t* out = cands + ((size_t)row * S + sp) * kSlot;
+    const int lane = tid & 63;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = c0 + 4 * (u * kSplitT + tid);
+      const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool c = e[q] > -INFINITY && (m - e[q]) * invT < kCut;
+        const unsigned long long msk = __ballot(c);
+        if (msk == 0) continue;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&cnt, __popcll(msk));
+        base = __shfl(base, 0, 64);
+        const int pos = base + __popcll(msk & ((1ull << lane) - 1ull));
+        if (c && pos < kSlot) out[pos] = ((uint64_t)fkey(e[q]) << 32) | (uint32_t)(i + q);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) pw[5] = __int_as_float(cnt);
+    return;
+  }
   // pure temperature sampling: Gumbel-max over the whole row = max over chunks of x / T + G_i
   __syncthreads();
   const uint64_t seed = (uint64_t)seeds[row];
@@ -456,59 +489,6 @@ __global__ __launch_bounds__(kSplitT) void sample_split_stats(const float* __res
     pw[3] = g.v + m * invT;  // comparable across chunks: x / T + G
     pw[4] = __int_as_float(g.i);
   }
-}
-
-__device__ __forceinline__ bool split_needs_cands(float T, float p, int k, int V) {
-  return T > 0.f && (p < 1.f || (k > 0 && k < V));
-}
-
-__global__ __launch_bounds__(kSplitT) void sample_split_cands(const float* __restrict__ logits, int V, long ld,
-                                                              const float* __restrict__ temperature,
-                                                              const float* __restrict__ top_p,
-                                                              const int* __restrict__ top_k,
-                                                              float* __restrict__ part,
-                                                              uint64_t* __restrict__ cands) {
-  __shared__ int cnt;
-  const int row = blockIdx.y, sp = blockIdx.x, S = gridDim.x, tid = threadIdx.x, lane = tid & 63;
-  const float T = temperature[row];
-  if (!split_needs_cands(T, top_p[row], top_k[row], V)) return;
-  const float* pr = part + (size_t)row * S * kPartW;
-  float M = -INFINITY;
-  for (int j = 0; j < S; ++j) M = fmaxf(M, pr[j * kPartW]);
-  const float invT = 1.f / T;
-  if (tid == 0) cnt = 0;
-  __syncthreads();
-  const int c0 = sp * kChunk;
-  const float* x = logits + (size_t)row * ld;
-  uint64_t* out = cands + ((size_t)row * S + sp) * kSlot;
-  constexpr int U = kChunk / (4 * kSplitT);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = c0 + 4 * (u * kSplitT + tid);
-    float4 v;
-    if (i + 3 < V) {
-      v = *reinterpret_cast<const float4*>(x + i);
-    } else {
-      v.x = i < V ? x[i] : -INFINITY;
-      v.y = i + 1 < V ? x[i + 1] : -INFINITY;
-      v.z = i + 2 < V ? x[i + 2] : -INFINITY;
-      v.w = i + 3 < V ? x[i + 3] : -INFINITY;
-    }
-    const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool c = e[q] > -INFINITY && (M - e[q]) * invT < kCut;
-      const unsigned long long msk = __ballot(c);
-      if (msk == 0) continue;
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&cnt, __popcll(msk));
-      base = __shfl(base, 0, 64);
-      const int pos = base + __popcll(msk & ((1ull << lane) - 1ull));
-      if (c && pos < kSlot) out[pos] = ((uint64_t)fkey(e[q]) << 32) | (uint32_t)(i + q);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) part[((size_t)row * S + sp) * kPartW + 5] = __int_as_float(cnt);
 }
 
 // radix_select over the LDS candidate list (keys in the high words)
@@ -583,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __
                                                                  const uint64_t* __restrict__ cands, int S,
                                                                  int* __restrict__ out_tokens) {
   __shared__ SampleSmem sm;
-  __shared__ int offs[129];
+  __shared__ int cnt_sh;
   __shared__ int flag;
   const int row = blockIdx.x, tid = threadIdx.x;
   const float T = temperature[row];
@@ -605,29 +585,41 @@ __global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __
     if (tid == 0) out_tokens[row] = g.i < V ? g.i : am.i;
     return;
   }
-  // candidate list: per-chunk counts -> offsets (S <= 128 chunks)
-  if (tid == 0) {
-    int o = 0, bad = S > 128;
-    for (int j = 0; j < S && !bad; ++j) {
-      const int c = __float_as_int(pr[j * kPartW + 5]);
-      if (c > kSlot) bad = 1;
-      offs[j] = o;
-      o += c;
+  // candidate list: the chunks whose max lies within kCut of the row max contribute their candidates that do
+  // too (nucleus_fast's set); such a chunk that overflowed its slots may have dropped one -> whole-row path
+  if (tid == 0) cnt_sh = 0, flag = S > 128;
+  __syncthreads();
+  for (int j = 0; j < S && !flag; ++j) {
+    const float mj = pr[j * kPartW];
+    if (!(mj > -INFINITY) || (M - mj) * invT >= kCut) continue;
+    const int c = __float_as_int(pr[j * kPartW + 5]);
+    if (c > kSlot) {
+      if (tid == 0) flag = 1;
+      break;
     }
-    offs[S < 128 ? S : 128] = o;
-    flag = bad || o > kCap;
+    const uint64_t* src = cands + ((size_t)row * S + j) * kSlot;
+    for (int q0 = 0; q0 < c; q0 += kThreads) {
+      const int q = q0 + tid;
+      uint64_t e = 0;
+      bool keep = false;
+      if (q < c) {
+        e = src[q];
+        keep = (M - key_to_float((uint32_t)(e >> 32))) * invT < kCut;
+      }
+      const unsigned long long msk = __ballot(keep);
+      int base = 0;
+      if ((tid & 63) == 0 && msk) base = atomicAdd(&cnt_sh, __popcll(msk));
+      base = __shfl(base, 0, 64);
+      const int pos = base + __popcll(msk & ((1ull << (tid & 63)) - 1ull));
+      if (keep && pos < kCap) sm.cand[pos] = e;
+    }
   }
   __syncthreads();
-  if (flag) {
+  if (flag || cnt_sh > kCap) {
     sample_row_full(logits + (size_t)row * ld, V, T, k, p, seed, step, sm, out_tokens + row);
     return;
   }
-  const int n = offs[S];
-  for (int j = 0; j < S; ++j) {
-    const int c = offs[j + 1] - offs[j];
-    for (int q = tid; q < c; q += kThreads) sm.cand[offs[j] + q] = cands[((size_t)row * S + j) * kSlot + q];
-  }
-  __syncthreads();
+  const int n = cnt_sh;
   uint32_t floor_key = 0;
   int fallback = 0;
   if (k > 0 && k < V) {
@@ -897,9 +889,8 @@ void gai_sample(const float* logits, int B, int V, long ld, const float* tempera
   }
   uint64_t* cands = reinterpret_cast<uint64_t*>(ws);
   float* part = reinterpret_cast<float*>(cands + (size_t)B * S * kSlot);
-  sample_split_stats<<<dim3(S, B), kSplitT, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part);
-  GAI_LAUNCH_CHECK();
-  sample_split_cands<<<dim3(S, B), kSplitT, 0, st>>>(logits, V, ld, temperature, top_p, top_k, part, cands);
+  sample_split_stats<<<dim3(S, B), kSplitT, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part,
+                                                      cands);
   GAI_LAUNCH_CHECK();
   sample_split_resolve<<<B, kThreads, 0, st>>>(logits, V, ld, temperature, top_p, top_k, seeds, step, part, cands,
                                                S, out_tokens);
@@ -912,7 +903,7 @@ void gai_sample(const float* logits, int B, int V, long ld, const float* tempera
 __global__ __launch_bounds__(kTpThreads) void sample_tp_stats(const float* __restrict__ x, long ld, int Vl, int vstart,
                                                               int V, const float* __restrict__ temperature,
                                                               const int64_t* __restrict__ seeds, int64_t step,
-                                                              float* __restrict__ out) {
+                                                              float* __restrict__ out, long ostride) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -949,17 +940,18 @@ __global__ __launch_bounds__(kTpThreads) void sample_tp_stats(const float* __res
   if (tid == 0) {
     ArgMax b{sv[0], si[0]};
     for (int w = 1; w < kTpThreads / 64; ++w) b = argmax_merge(b, ArgMax{sv[w], si[w]});
-    out[row * 4 + 0] = m;
-    out[row * 4 + 1] = st;
-    out[row * 4 + 2] = b.v;
-    out[row * 4 + 3] = (float)(b.i == 0x7fffffff ? vstart : b.i);
+    float* o = out + (size_t)row * ostride;
+    o[0] = m;
+    o[1] = st;
+    o[2] = b.v;
+    o[3] = (float)(b.i == 0x7fffffff ? vstart : b.i);
   }
 }
 
 void gai_sample_tp_stats(const float* x, long ld, int B, int Vl, int vstart, int V, const float* temperature,
-                         const int64_t* seeds, int64_t step, float* out, hipStream_t st) {
+                         const int64_t* seeds, int64_t step, float* out, long ostride, hipStream_t st) {
   if (B == 0) return;
-  sample_tp_stats<<<B, kTpThreads, 0, st>>>(x, ld, Vl, vstart, V, temperature, seeds, step, out);
+  sample_tp_stats<<<B, kTpThreads, 0, st>>>(x, ld, Vl, vstart, V, temperature, seeds, step, out, ostride);
   GAI_LAUNCH_CHECK();
 }
 
