@@ -239,7 +239,7 @@ void sample_tp_stats(const Tensor& logits, int64_t vstart, int64_t V, const Tens
   TORCH_CHECK(logits.stride(1) == 1, "logits rows must be contiguous");
   check_f32(temperature, "temperature");
   TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
-  check_f32(out, "out");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat, "out must be a float32 GPU tensor");
   TORCH_CHECK(out.dim() == 2 && out.size(0) >= logits.size(0) && out.size(1) >= 4 && out.stride(1) == 1,
               "out must be a [B, >=4] float view with unit column stride");
   gai_sample_tp_stats(logits.data_ptr<float>(), logits.stride(0), logits.size(0), logits.size(1), (int)vstart, (int)V,

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restric
 // Same token as sample_kernel for a fixed (seed, step) up to float summation order at exact-cut ties.
 constexpr int kChunk = 8192;   // logits per split workgroup (32 per thread, 8 float4 registers)
 constexpr int kSplitT = 256;
-constexpr int kSlot = 256;     // candidate slots per chunk
+constexpr int kSlot = 1024;    // candidate slots per chunk (chunk-max relative: flat rows reach a few hundred)
 constexpr int kSplitMinV = 16384;
 constexpr int kPartW = 8;      // words per (row, split) partial: max, sum, argmax, gval, gidx, count
 

@@ -78,7 +78,8 @@ class Embedder:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 out = m.embed_padded(ids, lens, attn, B, L)
-            self._graphs[key] = (g, ids, lens, out)
+            # the graph reads and writes attn's buffers (KV scratch, index tensors) by address: keep them alive
+            self._graphs[key] = (g, ids, lens, out, attn)
         return self._graphs[key]
 
     def _embed_graphed(self, seqs: List[List[int]]) -> "torch.Tensor | None":
@@ -87,7 +88,7 @@ class Embedder:
         L = next((x for x in self.GRAPH_L if x >= longest), None)
         if B is None or L is None:
             return None
-        g, ids, lens, out = self._graph_for(B, L)
+        g, ids, lens, out, _ = self._graph_for(B, L)
         flat = torch.zeros(B, L, dtype=torch.int32)
         ln = torch.ones(B, dtype=torch.int32)
         for i, x in enumerate(seqs):

@@ -199,3 +199,19 @@ def test_query_embed_graph_matches_packed(cuda):
     assert torch.allclose(a, b, atol=2e-2), (a - b).abs().max()
     cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
     assert bool((cos > 0.999).all()), cos
+
+
+@pytest.mark.parametrize("L", [40, 100])
+def test_query_embed_graph_e5_large_batch64(cuda, L):
+    """The headline's query encoder (e5-large-v2 shape) through the graph path at batch 64."""
+    cfg = BertConfig.e5_large_v2()
+    m = BertModel(cfg, device=cuda).random_init(4)
+    emb = Embedder(m, bert_byte_tokenizer(cfg.vocab_size))
+    qs = [("q%d " % i) + "y" * (L - 12 - (i % 7)) for i in range(64)]
+    a = emb.embed(qs, "query")
+    torch.cuda.synchronize()
+    assert emb._graphs
+    emb.use_graphs = False
+    b = emb.embed(qs, "query")
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert bool((cos > 0.999).all()), cos.min()
