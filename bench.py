@@ -191,6 +191,10 @@ def main():
         from generativeaiexamples_amd.parallel.launch import spawn_ranks
 
         sys.exit(spawn_ranks(args.gpus))
+    if args.served:  # the HTTP clients run in their own process, spawned before this one touches the GPU
+        from generativeaiexamples_amd.benchmarks import served_client
+
+        served_client.start()
     if args.config != 2:
         return run_other_config(args)
     args.batch = args.batch or 64
@@ -327,6 +331,9 @@ def main():
         torch.cuda.synchronize()
         ctx.barrier()
         t1 = time.perf_counter()
+        t_first = max(r.first_token_time for r in reqs)  # every prompt prefilled (its first token sampled)
+        phase["prefill_wall"] += t_first - t_retrieved
+        phase["decode_wall"] += t1 - t_first
         unplant(planted)
         ttft = [r.first_token_time - t0 for r in reqs]
         ntok = sum(len(r.output_ids) for r in reqs)
@@ -336,7 +343,8 @@ def main():
         return t1 - t0, ttft, ntok, plen, t_retrieved - t0
 
     def new_phase():
-        return dict(embed=0.0, scan=0.0, prompt_build=0.0, tokenize=0.0, add_request=0.0)
+        return dict(embed=0.0, scan=0.0, prompt_build=0.0, tokenize=0.0, add_request=0.0, prefill_wall=0.0,
+                    decode_wall=0.0)
 
     if args.served:
         from generativeaiexamples_amd.benchmarks.served import run_served
@@ -420,7 +428,10 @@ def main():
         "unique_chunks_retrieved": len(uniq),
         "prefix_cache": bool(args.prefix_cache),
         "baseline_qps": round(BASELINE_QPS, 4),
-        "retrieval_breakdown_ms": {k: round(1000 * v / max(1, args.steps), 2) for k, v in phase.items()},
+        "retrieval_breakdown_ms": {k: round(1000 * v / max(1, args.steps), 2) for k, v in phase.items()
+                                   if not k.endswith("_wall")},
+        # wall time per step from retrieval done to the last prompt's first token, then to the last token
+        "phase_ms": {k[:-5]: round(1000 * v / max(1, args.steps), 1) for k, v in phase.items() if k.endswith("_wall")},
         "planted_chunks": not args.no_plant,
         **probes,
     }

@@ -12,7 +12,9 @@ bench.py behind a ServiceHub, the same 1M-vector HBM index shard as the vector s
   queries (DynamicBatcher) on the high-priority retrieval stream -> rag prompt -> AsyncLLMEngine ->
   SSE frames awaited on the event loop -> client.
 
-value = queries/s over all ranks; TTFT = client send -> first non-empty ``data:`` frame. The per-query
+The HTTP clients run in a separate process (``served_client``, spawned before the GPU is initialised),
+all streams of a wave on one asyncio loop. value = queries/s over all ranks; TTFT = client send -> first
+non-empty ``data:`` frame. The per-query
 relevant chunks are planted exactly as in the in-process bench (untimed), score_threshold is off and EOS
 is ignored (``APP_LLM_IGNOREEOS``, asserted: every answer has exactly max_tokens tokens). Untimed
 probes: a concurrency-1 run (TTFT, TPOT) and an open-loop Poisson run at 0.8x the measured rate.
@@ -134,38 +136,21 @@ def run_served(args, ctx, st: dict) -> dict:
         except httpx.HTTPError:
             time.sleep(0.05)
     B = args.batch
-    clients = [httpx.Client(timeout=600) for _ in range(B)]
+    from .served_client import start as start_clients
 
-    def wave(qids: List[int]) -> tuple:
-        """All clients released together; returns (wall seconds, per-request results)."""
+    clients = start_clients()  # spawned by bench.py before the GPU was initialised
+
+    def wave(qids: List[int], delays=None) -> tuple:
+        """All streams of the wave from the client process; (wall seconds, per-request results)."""
         qs = [synthetic.question(q) for q in qids]
-        res: List = [None] * len(qs)
-        errs: List[str] = []
-        go = threading.Event()
-
-        def worker(i):
-            go.wait()
-            try:
-                res[i] = _client_request(clients[i], url, qs[i], args.max_tokens)
-            except Exception as e:  # noqa: BLE001
-                errs.append(repr(e))
-
-        ths = [threading.Thread(target=worker, args=(i,)) for i in range(len(qs))]
-        for t in ths:
-            t.start()
-        time.sleep(0.05)  # every client thread parked on the start event
         n_done = len(aeng.completed)
         t0 = time.perf_counter()
-        go.set()
-        for t in ths:
-            t.join()
+        out = clients.wave(url, qs, args.max_tokens, delays)
         dt = time.perf_counter() - t0
-        if errs:
-            raise RuntimeError(f"{len(errs)} /generate requests failed: {errs[:2]}")
         done = list(aeng.completed)[n_done:]
         short = [n for _, n, _ in done if n != args.max_tokens]
         assert len(done) == len(qs) and not short, f"{len(short)} answers != max_tokens ({short[:4]}): work skipped"
-        return dt, res
+        return dt, out["results"]
 
     def step(i: int):
         qids = [(i * world + rank) * B + j for j in range(B)]
@@ -193,17 +178,19 @@ def run_served(args, ctx, st: dict) -> dict:
 
     probes = {}
     if not args.no_probes:
-        # concurrency 1 through the server: TTFT and per-chunk latency of a lone stream
+        # concurrency 1 through the server: TTFT and per-token latency of a lone stream
         c1, tpot = [], []
         for i in range(args.probe_c1):
             qid = 900_000 + 1000 * rank + i
             planted = st["plant"]([qid], [synthetic.question(qid)])
             _dev_sync()
-            r = _client_request(clients[0], url, synthetic.question(qid), args.max_tokens)
+            n0 = len(aeng.completed)
+            r = wave([qid])[1][0]
             st["unplant"](planted)
             c1.append(r["ttft"])
-            if r["chunks"] > 1:
-                tpot.append((r["e2e"] - r["ttft"]) / (r["chunks"] - 1))
+            ntok = aeng.completed[-1][1] if len(aeng.completed) > n0 else 0
+            if ntok > 1:
+                tpot.append((r["e2e"] - r["ttft"]) / (ntok - 1))
         # open loop: Poisson arrivals at 0.8x the measured per-rank rate
         rate = 0.8 * qps / world
         rng = random.Random(4242 + rank)
@@ -212,24 +199,9 @@ def run_served(args, ctx, st: dict) -> dict:
             t += rng.expovariate(rate)
             arr.append(t)
         qids = [900_000 + 1000 * rank + 500 + j for j in range(B)]
-        qs = [synthetic.question(q) for q in qids]
-        planted = st["plant"](qids, qs)
+        planted = st["plant"](qids, [synthetic.question(q) for q in qids])
         _dev_sync()
-        out: List = [None] * B
-        t0 = time.perf_counter()
-
-        def pworker(j):
-            d = arr[j] - (time.perf_counter() - t0)
-            if d > 0:
-                time.sleep(d)
-            out[j] = _client_request(clients[j], url, qs[j], args.max_tokens)
-
-        ths = [threading.Thread(target=pworker, args=(j,)) for j in range(B)]
-        for t_ in ths:
-            t_.start()
-        for t_ in ths:
-            t_.join()
-        span = time.perf_counter() - t0
+        span, out = wave(qids, delays=arr)
         st["unplant"](planted)
         pt = sorted(r["ttft"] for r in out)
         probes = {"p50_ttft_c1_s": round(statistics.median(c1), 4), "ttft_c1_s": [round(x, 4) for x in c1],
@@ -239,8 +211,6 @@ def run_served(args, ctx, st: dict) -> dict:
                               "achieved_qps_per_gpu": round(B / span, 3),
                               "p50_ttft_s": round(percentile(pt, 0.5), 4), "p90_ttft_s": round(percentile(pt, 0.9), 4)}}
         log(f"served probes: {probes}")
-    for c in clients:
-        c.close()
     srv.should_exit = True
     th.join(10)
     lcfg, bcfg = st["lcfg"], st["bcfg"]

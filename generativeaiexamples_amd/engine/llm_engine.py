@@ -123,6 +123,16 @@ class _Run:
     done: Any = None          # device event after the tokens' D2H copy (None: already synchronous)
 
 
+@dataclass
+class _Single:
+    """A one-token step enqueued on the device whose sampled tokens are not processed yet."""
+    seq_order: List[int]
+    reqs: List[Any]
+    n: int
+    host: Any                 # sampled tokens (pinned buffer view, valid once `done` completed) or a list
+    done: Any = None
+
+
 class LLMEngine:
     def __init__(self, model, tokenizer: Tokenizer, cfg: EngineConfig | None = None):
         self.model, self.tok = model, tokenizer
@@ -177,6 +187,11 @@ class LLMEngine:
         self._pending: Optional[_Run] = None  # multi-step run enqueued, tokens not processed yet
         self._launches = 0
         self._tok_host = None  # 2 pinned [K * max bucket] int32 token buffers (alternate launches)
+        self._single_host = None  # 2 pinned token buffers of one-token steps (alternate launches)
+        # schedule + enqueue the next batch while a one-token step is still on the device (prefill chunks
+        # back to back: the host's planning / launches overlap the GPU instead of following a sync)
+        self._lookahead = os.environ.get("GAI_LOOKAHEAD", "1") == "1"
+        self._pipeline = os.environ.get("GAI_PIPELINE", "1") == "1"  # chained multi-step runs (A/B switch)
         self._masks = None  # guided-decoding mask builder (lazy)
         self._timing = os.environ.get("GAI_STEP_TIMING") == "1"
         self.phase_ms: Dict[str, float] = {}
@@ -596,23 +611,22 @@ class LLMEngine:
         self._step_done()
         return out
 
-    def _launch_multi(self, b, reqs, K: int) -> bool:
+    def _launch_multi(self, b, reqs, K: int) -> Optional[_Run]:
         plan = self._plan_multi(b, reqs, K)
         if plan is None:
-            return False
+            return None
         self.step_count += K - 1
         self.stats["decode_tokens"] += plan["n"] * (K - 1)
         self._publish(plan)
         with roctx_range("decode_multi"):
             host, ev = self._exec_multi(plan)
         base = [int(p) for p in b.positions]
-        self._pending = _Run([int(x) for x in b.decode_seq_ids], reqs, K, plan["n"], False, base, host, ev)
-        return True
+        return _Run([int(x) for x in b.decode_seq_ids], reqs, K, plan["n"], False, base, host, ev)
 
     def _chain(self, run: _Run) -> Optional[_Run]:
         """Enqueue run r+1 of a pending run r (before r's tokens are read), or None when the batch should
         go back to the scheduler: requests waiting, the bucket shrank, too few tokens left, no KV pages."""
-        if self.sched.num_waiting() > 0:
+        if not self._pipeline or self.sched.num_waiting() > 0:
             return None
         alive = [i for i, r in enumerate(run.reqs) if not r.finished]
         if not alive or self._graph_bucket(len(alive)) != self._graph_bucket(run.n):
@@ -678,9 +692,10 @@ class LLMEngine:
         plan["step"] = self.step_count
         return plan, seq_order, reqs
 
-    def _exec_single(self, plan: dict, reqs=None) -> Optional[List[int]]:
+    def _exec_single(self, plan: dict, reqs=None, async_: bool = False):
         """Forward of a one-token step on this rank; the leader also samples (followers need no tokens:
-        the next plan carries them)."""
+        the next plan carries them). async_: return (pinned token buffer, completion event) instead of
+        waiting for the tokens (GPU only)."""
         st = self._bank()
         if plan["op"] == "graph":
             logits = self._run_graph(plan)
@@ -698,7 +713,18 @@ class LLMEngine:
             self._mark("penalize_pack")
             t = ops.sample(logits, temp, top_p, top_k, seeds, plan["step"])
             self._mark("sample")
-            toks = t.cpu().tolist()
+            if async_ and self.device.type == "cuda" and not self._timing:
+                n = t.shape[0]
+                cap = max(self.cfg.max_num_seqs, max(self.cfg.graph_batch_sizes), n)
+                if self._single_host is None or self._single_host[0].numel() < cap:
+                    self._single_host = [torch.empty(cap, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+                buf = self._single_host[self._launches & 1][:n]
+                buf.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                toks = (buf.numpy(), ev)
+            else:
+                toks = t.cpu().tolist()
         st.fence()
         self._step_done()
         return toks
@@ -731,6 +757,63 @@ class LLMEngine:
         return logits[:n]
 
     # ------------------------------------------------------------------ step
+    def _lookahead_ok(self) -> bool:
+        """Schedule the next batch while a one-token step is in flight only when schedule() cannot preempt: a
+        sequence whose token is still on the device must not be reset and re-admitted (its pending token would
+        then be appended twice). Every running sequence needs at most one new KV page per step."""
+        return (self._lookahead and self.ep_group is None and self.device.type == "cuda"
+                and self.sched.num_free_blocks() > self.sched.num_running() + 1)
+
+    def _schedule_and_launch(self):
+        """schedule() and enqueue the batch: a pending handle (_Run / _Single), None when nothing is scheduled
+        or nothing was sampled, or a list of outputs (synchronous paths: EP lockstep, CPU)."""
+        b = self.sched.schedule()
+        self._mark("schedule")
+        n_tok = b.num_tokens
+        if self.ep_group is not None:
+            t_max, any_prefill = self._ep_agree([n_tok, int(b.num_prefill_tokens > 0)])
+            if t_max == 0:
+                return None
+            self.model.ep_capacity_tokens, self.model.ep_exact = t_max, bool(any_prefill)
+            if n_tok == 0:
+                self._ep_dummy_forward()
+                return None
+        if n_tok == 0:
+            return None
+        self.step_count += 1
+        self.stats["steps"] += 1
+        P = b.num_prefill_tokens
+        self.stats["prefill_tokens"] += P
+        self.stats["decode_tokens"] += n_tok - P
+        nd = len(b.decode_seq_ids)
+        if P == 0 and nd and self.cfg.decode_steps > 1:
+            dreqs = [self.requests.get(s) for s in b.decode_seq_ids]
+            K = self._multi_steps_for(b, dreqs)
+            if K > 1:
+                run = self._launch_multi(b, dreqs, K)
+                if run is not None:
+                    return run  # its tokens are processed by the next step(), after run 2 is enqueued
+        plan, seq_order, reqs = self._plan_single(b)
+        self._publish(plan)
+        with roctx_range("prefill" if P else "decode"):
+            toks = self._exec_single(plan, reqs, async_=self._lookahead and self.ep_group is None)
+        if toks is None:
+            return None
+        if isinstance(toks, tuple):
+            host, ev = toks
+            return _Single(seq_order, reqs, len(seq_order), host, ev)
+        out = self._process(seq_order, reqs, toks)
+        self._mark("process")
+        return out
+
+    def _complete_single(self, p: _Single) -> List[RequestOutput]:
+        if p.done is not None:
+            p.done.synchronize()
+        toks = p.host[:p.n].tolist() if hasattr(p.host, "tolist") else list(p.host)
+        out = self._process(p.seq_order, p.reqs, toks)
+        self._mark("process")
+        return out
+
     @torch.inference_mode()
     def step(self) -> List[RequestOutput]:
         if not self.leader:
@@ -738,44 +821,26 @@ class LLMEngine:
         with self.lock:
             if self._timing:
                 self._t_mark = time.perf_counter()
-            if self._pending is not None:
+            p = self._pending
+            if isinstance(p, _Run):
                 # pipelined decode: enqueue run r+1, then process run r while r+1 executes
-                run = self._pending
-                self._pending = self._chain(run)
-                return self._complete(run)
-            b = self.sched.schedule()
-            self._mark("schedule")
-            n_tok = b.num_tokens
-            if self.ep_group is not None:
-                t_max, any_prefill = self._ep_agree([n_tok, int(b.num_prefill_tokens > 0)])
-                if t_max == 0:
-                    return []
-                self.model.ep_capacity_tokens, self.model.ep_exact = t_max, bool(any_prefill)
-                if n_tok == 0:
-                    self._ep_dummy_forward()
-                    return []
-            if n_tok == 0:
-                return []
-            self.step_count += 1
-            self.stats["steps"] += 1
-            P = b.num_prefill_tokens
-            self.stats["prefill_tokens"] += P
-            self.stats["decode_tokens"] += n_tok - P
-            nd = len(b.decode_seq_ids)
-            if P == 0 and nd and self.cfg.decode_steps > 1:
-                dreqs = [self.requests.get(s) for s in b.decode_seq_ids]
-                K = self._multi_steps_for(b, dreqs)
-                if K > 1 and self._launch_multi(b, dreqs, K):
-                    return []  # its tokens are processed by the next step(), after run 2 is enqueued
-            plan, seq_order, reqs = self._plan_single(b)
-            self._publish(plan)
-            with roctx_range("prefill" if P else "decode"):
-                toks = self._exec_single(plan, reqs)
-            if toks is None:
-                return []
-            out = self._process(seq_order, reqs, toks)
-            self._mark("process")
-            return out
+                self._pending = self._chain(p)
+                return self._complete(p)
+            if isinstance(p, _Single):
+                # the next batch goes to the device before this step's tokens are read (its sequences are not
+                # schedulable until they are: schedule() sees no uncomputed token for them)
+                nxt = self._schedule_and_launch() if self._lookahead_ok() else None
+                self._pending = None
+                outs = self._complete_single(p)
+                if isinstance(nxt, list):
+                    return outs + nxt
+                self._pending = nxt
+                return outs
+            nxt = self._schedule_and_launch()
+            if isinstance(nxt, list):
+                return nxt
+            self._pending = nxt
+            return []
 
     # ------------------------------------------------------------------ tensor-parallel followers
     @torch.inference_mode()
