@@ -233,6 +233,7 @@ def main():
         bcfg = BertConfig.tiny()
     enc = BertModel(bcfg, device=dev).random_init(seed=2)
     embedder = Embedder(enc, bert_byte_tokenizer(bcfg.vocab_size))
+    embedder.capture_graphs()  # every query-encoder bucket before any timed or served work
     log(f"models ready: {lcfg.name} {llm.num_params() / 1e9:.2f}B params, {bcfg.name}")
 
     # ---------------- index shard (1M x dim per GPU, synthetic documents on demand)

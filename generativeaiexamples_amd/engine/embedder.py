@@ -76,11 +76,23 @@ class Embedder:
                 m.embed_padded(ids, lens, attn, B, L)  # warm-up (allocator, kernel attributes)
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 out = m.embed_padded(ids, lens, attn, B, L)
             # the graph reads and writes attn's buffers (KV scratch, index tensors) by address: keep them alive
             self._graphs[key] = (g, ids, lens, out, attn)
         return self._graphs[key]
+
+    def capture_graphs(self, max_batch: int = 64, max_len: int = 128) -> int:
+        """Capture every (batch, length) bucket up front (service start-up): a capture while the engine thread
+        runs would otherwise happen on the first query of each new shape. Returns the number captured."""
+        if not self.use_graphs:
+            return 0
+        with self.lock:
+            for B in self.GRAPH_B:
+                for L in self.GRAPH_L:
+                    if B <= max_batch and L <= max_len:
+                        self._graph_for(B, L)
+        return len(self._graphs)
 
     def _embed_graphed(self, seqs: List[List[int]]) -> "torch.Tensor | None":
         n, longest = len(seqs), max(len(x) for x in seqs)

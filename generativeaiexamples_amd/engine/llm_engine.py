@@ -444,7 +444,7 @@ class LLMEngine:
                 self.model.forward(fb, self.kv, self.decode_ws)
         torch.cuda.current_stream(d).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             logits = self.model.forward(fb, self.kv, self.decode_ws)
         self.graphs[bs] = (g, fb, logits)
 
@@ -505,7 +505,7 @@ class LLMEngine:
                 run()  # warm-up (n_valid = 0: the advance kernel touches no row)
             torch.cuda.current_stream(d).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 run()
         self.multi_graphs[bs] = (g, run, fb, samp, n_valid, toks)
 
@@ -630,6 +630,8 @@ class LLMEngine:
             return None
         alive = [i for i, r in enumerate(run.reqs) if not r.finished]
         if not alive or self._graph_bucket(len(alive)) != self._graph_bucket(run.n):
+            return None
+        if self.sched.num_running() != len(alive):  # other running sequences must join the next batch
             return None
         K = run.K
         if not self._worth_multi([run.reqs[i] for i in alive], extra=K):
@@ -761,7 +763,11 @@ class LLMEngine:
         """Schedule the next batch while a one-token step is in flight only when schedule() cannot preempt: a
         sequence whose token is still on the device must not be reset and re-admitted (its pending token would
         then be appended twice). Every running sequence needs at most one new KV page per step."""
+        # only while prompts are still waiting for prefill: with none waiting the look-ahead batch would be the
+        # decode of every running sequence EXCEPT the in-flight ones, splitting the decode batch in two (a
+        # second, small-batch pass over all the decode steps)
         return (self._lookahead and self.ep_group is None and self.device.type == "cuda"
+                and self.sched.num_waiting() > 0
                 and self.sched.num_free_blocks() > self.sched.num_running() + 1)
 
     def _schedule_and_launch(self):

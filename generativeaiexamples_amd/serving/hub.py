@@ -83,6 +83,8 @@ class ServiceHub:
         self.default_llm_name = self.default_llm_name or name
 
     def add_embedder(self, name: str, emb: Embedder):
+        if hasattr(emb, "capture_graphs"):
+            emb.capture_graphs()  # before serving: no graph capture beside the running engine thread
         self.embedders[name] = emb
         self.default_embedder_name = self.default_embedder_name or name
 

@@ -665,7 +665,9 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
     """One-GPU rehearsal of a TP=world decode (every rank on cuda:0, gloo control plane): the multi-step
     decode graph holds only peer-memory collectives (custom all-reduce for the embedding / block-boundary
     reductions and ops.sample_tp's candidate exchange), is captured on every rank and replayed in lockstep
-    through pipelined (chained) runs. Rank 0 compares the greedy tokens with a TP=1 engine."""
+    through pipelined (chained) runs. Rank 0 checks every greedy token against the fp32 reference forward of
+    the same weights (bf16 TP partial sums may flip a near-tie, after which the sequences legitimately
+    diverge, so token-by-token equality with a TP=1 engine is not the criterion)."""
     import json
 
     os.environ.update(GAI_SINGLE_DEVICE="1", GAI_CUSTOM_AR="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
@@ -673,11 +675,11 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
     from generativeaiexamples_amd.parallel import dist as gdist
 
     ctx = gdist.init_distributed(tp_size=world, backend="gloo")
+    from generativeaiexamples_amd import ops
     from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
     from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
     from generativeaiexamples_amd.parallel.dist import DistContext
-    from generativeaiexamples_amd import ops
 
     err = None
     try:
@@ -688,27 +690,29 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
         m = LlamaModel(cfg, device="cuda", dist_ctx=ctx).load_hf_state(ref.export_hf_state())
         tok = small_byte_tokenizer(4096)
         ecfg = dict(num_blocks=128, max_model_len=256, use_graphs=True, decode_steps=4, max_num_seqs=8,
-                    graph_batch_sizes=(1, 2, 4, 8), prefix_cache=False, kv_memory_fraction=0.02)
+                    graph_batch_sizes=(4, 8), prefix_cache=False, kv_memory_fraction=0.02)
         eng = LLMEngine(m, tok, EngineConfig(**ecfg))
         eng.capture_graphs(max_bs=8)
         if not eng.leader:
             assert eng.follow() == "stop"
         else:
             prompts = [list(range(11 + 3 * i, 11 + 3 * i + n)) for i, n in enumerate((9, 23, 40, 5, 17))]
-            sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
+            sp = SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
             tp = eng.generate(prompts, sp)
             stats = dict(eng.stats)
             eng.release_followers(stop=True)
-            r1 = LLMEngine(ref, tok, EngineConfig(**ecfg))
-            r1.capture_graphs(max_bs=8)
-            one = r1.generate(prompts, sp)
-            a = [r.output_ids for r in tp]
-            b = [r.output_ids for r in one]
-            same = sum(x == y for ra, rb in zip(a, b) for x, y in zip(ra, rb))
+            bad, total = [], 0
+            for p, r in zip(prompts, tp):
+                lg = ref.reference_forward(torch.tensor(p + r.output_ids[:-1]))[len(p) - 1:]
+                for i, t in enumerate(r.output_ids):
+                    total += 1
+                    row = lg[i]
+                    if float(row[t]) < float(row.max()) - 0.02 * max(1.0, float(row.abs().max())):
+                        bad.append((i, t, int(row.argmax())))
             with open(os.path.join(out_dir, "tpg.json"), "w") as f:
-                json.dump({"tp": a, "ref": b, "same": same, "total": sum(len(x) for x in a), "stats": stats,
-                           "multi_graphs": sorted(eng.multi_graphs), "flags": int(ops.tp_sample_flags(m.device))}, f)
-    except Exception as e:  # noqa: BLE001
+                json.dump({"bad": bad, "total": total, "stats": stats, "multi_graphs": sorted(eng.multi_graphs),
+                           "flags": int(ops.tp_sample_flags(m.device))}, f)
+    except Exception:  # noqa: BLE001
         import traceback
         err = traceback.format_exc()
         with open(os.path.join(out_dir, f"tpg_err_{rank}.txt"), "w") as f:

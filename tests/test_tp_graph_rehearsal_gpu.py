@@ -1,8 +1,8 @@
 """TP=2/4/8 decode captured in HIP graphs on ONE GPU: every rank shares
 cuda:0 over a gloo control plane; the only collectives inside the multi-step decode graph are the
 peer-memory custom all-reduce kernels (including ops.sample_tp's candidate exchange, which replaces the
-[B, vocab] logits all-gather). Greedy tokens must match a TP=1 engine (bf16 partial-sum order may flip a
-near-tie, so >= 95 % of positions must agree and every first token must)."""
+[B, vocab] logits all-gather). Every greedy token must be the fp32 reference argmax of its prefix up to a
+bf16 near-tie (the criterion of the CPU engine tests)."""
 import json
 import socket
 
@@ -22,6 +22,7 @@ def _port():
     return p
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
     ctx = mp.get_context("spawn")
@@ -31,7 +32,7 @@ def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
     for p in procs:
         p.start()
     for p in procs:
-        p.join(110)
+        p.join(280)
     for p in procs:
         if p.is_alive():
             p.kill()
@@ -39,8 +40,8 @@ def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
     assert not errs, errs[0]
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = json.loads((tmp_path / "tpg.json").read_text())
-    print(f"TP={world}: {res['same']}/{res['total']} tokens equal TP=1, stats {res['stats']}, flags {res['flags']}")
+    print(f"TP={world}: {res['total'] - len(res['bad'])}/{res['total']} tokens fp32-consistent, stats {res['stats']}, "
+          f"flags {res['flags']}")
     assert res["multi_graphs"], "no multi-step decode graph captured"
     assert res["stats"]["graph_steps"] > 0 and res["stats"]["chained_runs"] > 0
-    assert all(a[0] == b[0] for a, b in zip(res["tp"], res["ref"]))
-    assert res["same"] >= 0.95 * res["total"]
+    assert not res["bad"], res["bad"][:5]
