@@ -21,8 +21,14 @@ O=$PWD/gpurun_out/$1; shift; mkdir -p "$O"
 
 step() {  # step SECONDS LOG cmd...
   local secs=$1 log=$2; shift 2
-  env "${envs[@]}" timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  # heartbeat into the log: a long quiet step (multi-rank tests, pytest -q) is not mistaken for a hang;
+  # the step's own timeout still bounds it
+  : > "$log"
+  ( while sleep 50; do echo "[gpu.sh] heartbeat $(date +%T)" >> "$log"; done ) &
+  local hb=$!
+  env "${envs[@]}" timeout -k 10 "$secs" "$@" >> "$log" 2>&1
   local rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "[gpu.sh] rc=$rc cmd=$*" >> "$log"
   tail -4 "$log"
   return $rc
