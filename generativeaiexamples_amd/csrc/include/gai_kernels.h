@@ -53,10 +53,11 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
                             int D, int kv_fp8, float k_scale, float v_scale, float* ws, int psw, hipStream_t st,
                             int K);
 bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                   int epi, int out_f32, hipStream_t st);
+                   int epi, int out_f32, hipStream_t st, int psw = 0);
 // deep-K decode projections: K split over workgroups into fp32 slabs ws[KS][M][N]; returns KS (0: not handled)
 int gai_gemm_dec2_partials_ks(int M, int N, int K);
-int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st);
+int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st,
+                           int psw = 0);
 
 // attention.hip
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,

@@ -80,7 +80,10 @@ __device__ __forceinline__ void dec_store8(void* C, size_t off, const float (&v)
 
 // PART: K is also split over gridDim.y workgroups (deep-K projections: down); each writes its fp32 partial
 // slab [ks][M][N] instead of the epilogue, reduced by the split-K tail kernels (gemm_splitk.hip).
-template <int MB, int NT, int EPI, bool OUTF32, bool PART = false>
+// PSW: W is the fragment-shuffled copy [N/16][K/32][64 lanes][8] (ops.shuffle_fragments): a wave's k32 step
+// is ONE contiguous KiB (8 full 128-B lines) instead of 16 half lines, loaded non-temporally (read once;
+// profiles/r2/dec_stream_microbench.jsonl: 5.8-6.5 TB/s shuffled + nt vs 5.0-5.4 on the natural layout).
+template <int MB, int NT, int EPI, bool OUTF32, bool PART = false, bool PSW = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                                 void* C, const bf16* __restrict__ bias, const bf16* R,
                                                                 int M, int N, int K, int ldc, float* __restrict__ part) {
@@ -99,7 +102,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
   const int nstages = nsteps / SPS;
 
   // ---- weight stream: rows nb + 16 ntl + (lane & 15), k = kq KW + 32 s + 8 (lane >> 4)
-  const bf16* wp = W + (size_t)min(nb + 16 * ntl + (lane & 15), N - 1) * K + kbase + (size_t)kq * KW + 8 * (lane >> 4);
+  constexpr int WSTEP = PSW ? 512 : 32;  // elements per k32 step of one wave's stream
+  const bf16* wp = PSW ? W + ((size_t)min((nb >> 4) + ntl, (N >> 4) - 1) * (K >> 5) + ((kbase + kq * KW) >> 5)) * 512 +
+                             8 * lane
+                       : W + (size_t)min(nb + 16 * ntl + (lane & 15), N - 1) * K + kbase + (size_t)kq * KW +
+                             8 * (lane >> 4);
+  auto wload = [&](int s) -> bf16x8 {
+    const bf16x8* p = reinterpret_cast<const bf16x8*>(wp + (size_t)WSTEP * s);
+    if constexpr (PSW) return __builtin_nontemporal_load(p);
+    else return *p;
+  };
 
   // ---- activation staging: chunk p = (4 wid + j) 64 + lane of a stage's [KQ][ROWS][CPR] chunks
   const bf16* asrc[4];
@@ -140,7 +152,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
   a_write(0, ast[0]);
   a_load(1, ast[1]);
 #pragma unroll
-  for (int d = 0; d < kD; ++d) rw[d] = load8(wp + 32 * min(d, nsteps - 1));
+  for (int d = 0; d < kD; ++d) rw[d] = wload(min(d, nsteps - 1));
   __syncthreads();
 
   // Stage st: at its first step issue the loads of stage st + 2 (register set st & 1); at its last
@@ -152,7 +164,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
       const int s = s0 + u;
       const int st = s / SPS;
       if (u % SPS == 0) a_load(st + 2, ast[(u / SPS) & 1]);
-      rw[(u + kD) % kSets] = load8(wp + 32 * min(s + kD, nsteps - 1));
+      rw[(u + kD) % kSets] = wload(min(s + kD, nsteps - 1));
       const char* sb = smem + (st & 1) * kStage;
       const int c = 4 * (u % SPS) + cq;
 #pragma unroll
@@ -239,10 +251,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
 template <int MB, int NT>
 constexpr int dec2_steps_multiple() { return DecCfg<MB, 8 / NT>::L; }
 
-template <int MB, int NT, int EPI, bool OUTF32, bool PART = false>
+template <int MB, int NT, int EPI, bool OUTF32, bool PART = false, bool PSW = false>
 void dec2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
                  hipStream_t st, int KS = 1, float* part = nullptr) {
-  auto kern = gemm_dec2_kernel<MB, NT, EPI, OUTF32, PART>;
+  auto kern = gemm_dec2_kernel<MB, NT, EPI, OUTF32, PART, PSW>;
   constexpr int lds = 2 * kStage;
   static bool once = false;
   if (!once) {
@@ -255,15 +267,15 @@ void dec2_launch(const void* A, const void* W, void* C, const void* bias, const 
   GAI_LAUNCH_CHECK();
 }
 
-template <int MB, int NT>
+template <int MB, int NT, bool PSW>
 bool dec2_dispatch_epi(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K,
                        int ldc, int epi, int out_f32, hipStream_t st) {
 #define GAI_D2(E)                                                                    \
   case E:                                                                            \
     if (out_f32)                                                                     \
-      dec2_launch<MB, NT, E, true>(A, W, C, bias, R, M, N, K, ldc, st);              \
+      dec2_launch<MB, NT, E, true, false, PSW>(A, W, C, bias, R, M, N, K, ldc, st);  \
     else                                                                             \
-      dec2_launch<MB, NT, E, false>(A, W, C, bias, R, M, N, K, ldc, st);             \
+      dec2_launch<MB, NT, E, false, false, PSW>(A, W, C, bias, R, M, N, K, ldc, st); \
     return true;
   switch (epi) {
     GAI_D2(EPI_NONE)
@@ -276,9 +288,9 @@ bool dec2_dispatch_epi(const void* A, const void* W, void* C, const void* bias, 
     case EPI_SWIGLU:
       if constexpr (NT >= 2) {
         if (out_f32)
-          dec2_launch<MB, NT, EPI_SWIGLU, true>(A, W, C, bias, R, M, N, K, ldc, st);
+          dec2_launch<MB, NT, EPI_SWIGLU, true, false, PSW>(A, W, C, bias, R, M, N, K, ldc, st);
         else
-          dec2_launch<MB, NT, EPI_SWIGLU, false>(A, W, C, bias, R, M, N, K, ldc, st);
+          dec2_launch<MB, NT, EPI_SWIGLU, false, false, PSW>(A, W, C, bias, R, M, N, K, ldc, st);
         return true;
       }
       return false;
@@ -316,15 +328,15 @@ int dec2_pick_nt(int N, int K, bool swiglu) {
   return 0;
 }
 
-template <int MB>
+template <int MB, bool PSW>
 bool dec2_run(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
               int epi, int out_f32, hipStream_t st) {
   const int NT = dec2_pick_nt<MB>(N, K, epi == EPI_SWIGLU);
   switch (NT) {
-    case 8: return dec2_dispatch_epi<MB, 8>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-    case 4: return dec2_dispatch_epi<MB, 4>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-    case 2: return dec2_dispatch_epi<MB, 2>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-    case 1: return dec2_dispatch_epi<MB, 1>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    case 8: return dec2_dispatch_epi<MB, 8, PSW>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    case 4: return dec2_dispatch_epi<MB, 4, PSW>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    case 2: return dec2_dispatch_epi<MB, 2, PSW>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    case 1: return dec2_dispatch_epi<MB, 1, PSW>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
     default: return false;
   }
 }
@@ -347,11 +359,16 @@ int gai_gemm_dec2_ok(int M, int N, int K, int epi) {
 }
 
 bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                   int epi, int out_f32, hipStream_t st) {
+                   int epi, int out_f32, hipStream_t st, int psw) {
   if (!gai_gemm_dec2_ok(M, N, K, epi)) return false;
-  if (M <= 16) return dec2_run<1>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-  if (M <= 32) return dec2_run<2>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
-  return dec2_run<4>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+  if (psw) {
+    if (M <= 16) return dec2_run<1, true>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    if (M <= 32) return dec2_run<2, true>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+    return dec2_run<4, true>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+  }
+  if (M <= 16) return dec2_run<1, false>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+  if (M <= 32) return dec2_run<2, false>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
+  return dec2_run<4, false>(A, W, C, bias, R, M, N, K, ldc, epi, out_f32, st);
 }
 
 namespace {
@@ -376,29 +393,34 @@ int dec2_part_nt_env() {
   return v;
 }
 
-template <int MB>
+template <int MB, bool PSW>
 int dec2_part_run(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
   const int force = dec2_part_nt_env();
   if (MB > 1 && force != 8) {
     const int KS4 = dec2_part_ks<MB>(N, K, 4, force != 4);
     if (KS4) {
-      if (launch) dec2_launch<MB, 4, EPI_NONE, true, true>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS4, ws);
+      if (launch)
+        dec2_launch<MB, 4, EPI_NONE, true, true, PSW>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS4, ws);
       return KS4;
     }
   }
   constexpr int NT = MB == 1 ? 4 : 8;
   const int KS = dec2_part_ks<MB>(N, K, NT, false);
-  if (KS && launch) dec2_launch<MB, NT, EPI_NONE, true, true>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS, ws);
+  if (KS && launch)
+    dec2_launch<MB, NT, EPI_NONE, true, true, PSW>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS, ws);
   return KS;
 }
 
-int dec2_part_dispatch(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
+int dec2_part_dispatch(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch,
+                       bool psw = false) {
   static const int min_k = getenv("GAI_DEC2_PART_MINK") ? atoi(getenv("GAI_DEC2_PART_MINK")) : 8192;
   static const bool off = getenv("GAI_DEC2") && atoi(getenv("GAI_DEC2")) == 0;
   // M <= 16: the register-streamed split-K kernel is faster (down at M = 1: 30 vs 34 us)
   if (off || M <= 16 || M > 64 || N % 16 || K < min_k) return 0;
-  if (M <= 32) return dec2_part_run<2>(A, W, M, N, K, ws, st, launch);
-  return dec2_part_run<4>(A, W, M, N, K, ws, st, launch);
+  if (psw) return M <= 32 ? dec2_part_run<2, true>(A, W, M, N, K, ws, st, launch)
+                          : dec2_part_run<4, true>(A, W, M, N, K, ws, st, launch);
+  if (M <= 32) return dec2_part_run<2, false>(A, W, M, N, K, ws, st, launch);
+  return dec2_part_run<4, false>(A, W, M, N, K, ws, st, launch);
 }
 
 }  // namespace
@@ -407,6 +429,6 @@ int dec2_part_dispatch(const void* A, const void* W, int M, int N, int K, float*
 // KS workgroups writing fp32 slabs ws[KS][M][N] for the split-K tail kernels. Returns KS (0: shape not
 // handled, nothing launched).
 int gai_gemm_dec2_partials_ks(int M, int N, int K) { return dec2_part_dispatch(nullptr, nullptr, M, N, K, nullptr, 0, false); }
-int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st) {
-  return dec2_part_dispatch(A, W, M, N, K, ws, st, true);
+int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, int psw) {
+  return dec2_part_dispatch(A, W, M, N, K, ws, st, true, psw != 0);
 }

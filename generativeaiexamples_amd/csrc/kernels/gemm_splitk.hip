@@ -595,16 +595,16 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
                                  int M, int N, int K, float eps, float* ws, int psw, hipStream_t st) {
   if (M == 0) return;
   if (!gai_gemm_splitk_fusable_norm(M, N, K)) gai_launch_error(__FILE__, __LINE__, "gemm_splitk_add_rmsnorm: shape");
-  if (!psw && gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) {
-    // decode GEMM on the natural layout into a bf16 scratch h (the workspace), then the residual-add
-    // RMSNorm kernel: res = bf16(h + res), out = rmsnorm(res) * g - the same roundings as the fused tail
+  if (gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) {
+    // decode GEMM into a bf16 scratch h (the workspace), then the residual-add RMSNorm kernel:
+    // res = bf16(h + res), out = rmsnorm(res) * g - the same roundings as the fused tail
     bf16* h = reinterpret_cast<bf16*>(ws);
-    gai_gemm_dec2(A, B, h, bias, nullptr, M, N, K, N, bias ? EPI_BIAS : EPI_NONE, 0, st);
+    gai_gemm_dec2(A, B, h, bias, nullptr, M, N, K, N, bias ? EPI_BIAS : EPI_NONE, 0, st, psw);
     gai_rmsnorm(h, res, res, g, out, M, N, eps, st);
     return;
   }
-  // deep K (down): LDS-staged decode kernel writing K-split slabs on the natural layout
-  const int ks2 = psw ? 0 : gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+  // deep K (down): LDS-staged decode kernel writing K-split slabs
+  const int ks2 = gai_gemm_dec2_partials(A, B, M, N, K, ws, st, psw);
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (!ks2) launch_partials(A, B, M, N, K, KS, ws, psw, st);
   if (N <= 4096 && N % 4 == 0 && getenv("GAI_NORM_TAIL_256") == nullptr) {
@@ -668,12 +668,12 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
                             int K) {
   const int N = (Hq + 2 * Hkv) * D;
   if (M < 1 || M > 64 || (D != 64 && D != 128 && D != 256) || N % 16) return 0;
-  if (!psw && gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) return 0;  // single-pass kernel owns it
-  const int ks2 = psw ? 0 : gai_gemm_dec2_partials_ks(M, N, K);
+  if (gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) return 0;  // single-pass kernel owns it
+  const int ks2 = gai_gemm_dec2_partials_ks(M, N, K);
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (KS <= 1) return 0;
   if (ks2)
-    gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+    gai_gemm_dec2_partials(A, B, M, N, K, ws, st, psw);
   else
     launch_partials(A, B, M, N, K, KS, ws, psw, st);
   const long items = (long)M * (Hq + 2 * Hkv);
@@ -707,8 +707,8 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
   if (M > 64) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: M must be <= 64");
   // natural weight layout: the LDS-staged decode kernel (gemm_decode.hip) when the shape fits - single
   // pass for the wide projections, K-split slabs for the deep ones
-  if (!psw && gai_gemm_dec2(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st)) return;
-  const int ks2 = psw ? 0 : gai_gemm_dec2_partials(A, B, M, N, K, ws, st);
+  if (gai_gemm_dec2(A, B, C, bias, R, M, N, K, ldc, epi, out_f32, st, psw)) return;
+  const int ks2 = gai_gemm_dec2_partials(A, B, M, N, K, ws, st, psw);
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (KS == 0) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: K must be a multiple of 512");
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;

@@ -58,9 +58,10 @@ class EngineConfig:
     prefix_cache: bool = True
     use_graphs: bool = True
     # keep MFMA-fragment-shuffled copies of the decode projections (ops.preshuffle_weight, see
-    # LlamaModel.DECODE_PROJECTIONS): a second copy of those weights in HBM for <= 4 % faster decode
-    # GEMMs; off by default (one weight layout, all HBM beyond the weights goes to the KV cache)
-    decode_preshuffle: bool = False
+    # LlamaModel.DECODE_PROJECTIONS): every decode weight stream then reads whole 128-B lines
+    # (non-temporal), +9 % decode / +4.9 % headline on the same box (profiles/r3/psw_ab) for a second copy of
+    # the projection weights (17 GB for Llama-3-8B: 6 % of one MI355X's 288 GB)
+    decode_preshuffle: bool = True
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     # multi-step decode: when every running sequence is decoding (nothing waiting), run this many
     # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)
@@ -141,7 +142,8 @@ class LLMEngine:
         mc = model.cfg
         cfg.max_model_len = min(cfg.max_model_len, mc.max_position)
         self.max_blocks_per_seq = (cfg.max_model_len + ops.BLOCK - 1) // ops.BLOCK
-        if (self.device.type == "cuda" and cfg.decode_preshuffle and os.environ.get("GAI_DECODE_PSW", "1") == "1"
+        psw = os.environ.get("GAI_DECODE_PSW")  # "1" / "0" overrides the config (same-box A/B)
+        if (self.device.type == "cuda" and (cfg.decode_preshuffle if psw is None else psw == "1")
                 and hasattr(model, "preshuffle_decode_weights")):
             model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
         # tensor parallel: rank 0 of the TP group plans every step, the other members execute its plans

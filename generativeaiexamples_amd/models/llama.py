@@ -234,11 +234,10 @@ class LlamaModel:
             self.w["norm_b"] = e(D)
         self.w["lm_head"] = self.w["embed"] if c.tie_embeddings else e(self.vocab_local, D)
 
-    # Projections that may keep a fragment-shuffled decode copy (ops.preshuffle_weight, opt-in through
-    # EngineConfig.decode_preshuffle). Off by default: every decode GEMM runs from the single natural
-    # layout - the down projection on the LDS-staged K-split kernel at 38.9 us vs 37.5 us from a 3.8 GB
-    # copy at M = 64 (profiles/r2/dec_gemm_hbm_part.jsonl), QKV / O within 1 us.
-    DECODE_PROJECTIONS = ("qkv", "o", "down", "proj")
+    # Projections that keep a fragment-shuffled decode copy (ops.preshuffle_weight, EngineConfig.decode_preshuffle,
+    # on by default): HBM-cold at M = 64 (profiles/r3/psw_ab/dec_hbm.jsonl) gate_up + SwiGLU 56.1 -> 44.3 us,
+    # down 36.0 -> 29.3, LM head 238 -> 208, QKV 23.8 -> 21.4, O 17.2 -> 16.4 us.
+    DECODE_PROJECTIONS = ("qkv", "o", "gate_up", "down", "proj", "lm_head")
 
     def preshuffle_decode_weights(self) -> int:
         """Attach fragment-shuffled copies of the per-layer projection weights for the decode GEMM

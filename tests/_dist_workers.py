@@ -672,6 +672,10 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
 
     os.environ.update(GAI_SINGLE_DEVICE="1", GAI_CUSTOM_AR="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    # every rank's spin-waiting all-reduce kernel must be resident at once on the ONE shared GPU: one hardware
+    # queue per process keeps 8 processes within the device's mapped queues (no time-sliced queue, whose
+    # kernel would never meet its peers)
+    os.environ["GPU_MAX_HW_QUEUES"] = "1"
     from generativeaiexamples_amd.parallel import dist as gdist
 
     ctx = gdist.init_distributed(tp_size=world, backend="gloo")

@@ -164,6 +164,8 @@ def test_fused_add_rmsnorm_decode_matches(cuda, monkeypatch):
     for p in prompts:
         eng2.add_request(p, SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
     eng2.step()
+    while eng2._pending is not None:  # the prefill step's tokens are read by the next step() (async launch)
+        eng2.step()
     b = eng2.sched.schedule()
     assert b.num_prefill_tokens == 0 if hasattr(b, "num_prefill_tokens") else True
     fb, _ = eng2._make_batch(b)

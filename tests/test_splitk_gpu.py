@@ -135,9 +135,11 @@ def test_linear_add_rmsnorm_decode_tail(cuda, M, K, bias, psw):
 @pytest.mark.parametrize("M", [1, 2, 16, 31, 64])
 @pytest.mark.parametrize("N,K,act", [(28672, 4096, "swiglu"), (32000, 4096, None), (16384, 14336, "residual"),
                                      (18432, 4096, "bias"), (16384, 2048, "gelu")])
-def test_decode_gemm_natural_layout(cuda, M, N, K, act):
+@pytest.mark.parametrize("psw", [False, True])
+def test_decode_gemm_natural_layout(cuda, M, N, K, act, psw):
     """The LDS-staged decode GEMM (gemm_decode.hip, wide projections) vs the fp32 reference: Llama-3-8B
-    gate_up+SwiGLU, a 32K-vocab LM head (fp32 logits), deep K + residual, bias, bias+GELU."""
+    gate_up+SwiGLU, a 32K-vocab LM head (fp32 logits), deep K + residual, bias, bias+GELU; on the natural
+    [N, K] layout and on the fragment-shuffled copy (full-line non-temporal weight stream)."""
     torch.manual_seed(M * 3 + N)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
@@ -146,7 +148,12 @@ def test_decode_gemm_natural_layout(cuda, M, N, K, act):
     epi = ops.EPI[act]
     assert ops.native().gemm_dec2_ok(M, N, K, epi), "shape should take the LDS-staged decode kernel"
     out_dtype = torch.float32 if act is None else torch.bfloat16
-    y = _run(x, w, b, r, epi, out_dtype)
+    if psw:
+        assert ops.preshuffle_weight(w)
+        y = ops.linear(x, w, bias=b, residual=r, act=act if act in ("swiglu", "gelu") else None,
+                       out_dtype=out_dtype)
+    else:
+        y = _run(x, w, b, r, epi, out_dtype)
     want = ref.linear(x.cpu(), w.cpu(), None if b is None else b.cpu(), None if r is None else r.cpu(),
                       act if act in ("swiglu", "gelu") else None, torch.float32)
     tol = 2e-3 if out_dtype == torch.float32 else 2e-2

@@ -5,6 +5,7 @@ peer-memory custom all-reduce kernels (including ops.sample_tp's candidate excha
 bf16 near-tie (the criterion of the CPU engine tests)."""
 import json
 import socket
+import time
 
 import pytest
 import torch.multiprocessing as mp
@@ -22,7 +23,7 @@ def _port():
     return p
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(200)
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
     ctx = mp.get_context("spawn")
@@ -31,8 +32,9 @@ def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
              for r in range(world)]
     for p in procs:
         p.start()
+    deadline = time.monotonic() + 170
     for p in procs:
-        p.join(280)
+        p.join(max(1.0, deadline - time.monotonic()))
     for p in procs:
         if p.is_alive():
             p.kill()

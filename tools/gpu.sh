@@ -9,6 +9,7 @@
 #   bench <name> <bench.py args...> bench.py ... --json-out <name>.json
 #   prof  <name> <bench.py args...> rocprofv3 --kernel-trace --stats around bench.py, reduced to <name>_kernels.csv
 #   py    <name> <script args...>   python <script> <args>
+#   pyprof <name> <script args...>  rocprofv3 --kernel-trace --stats around python3 <script> <args>
 #   smoke                           __graft_entry__.smoke()
 # Leading KEY=VALUE tokens after <name> are exported for that step only, e.g. "bench b2 GAI_X=1 --steps 2".
 # e.g. /usr/local/graft/bin/gpurun --timeout 900 -- tools/gpu.sh r3a "tests kern tests/test_kernels_gpu.py" \
@@ -51,6 +52,11 @@ for spec in "$@"; do
            python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
              > /dev/null || exit $? ;;
     py)    step 600 "$O/$n.log" python "${rest[@]}" || exit $? ;;
+    pyprof) rm -rf "/tmp/prof_$n"
+           step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
+             python3 "${rest[@]}" || exit $?
+           python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
+             > /dev/null || exit $? ;;
     smoke) step 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $? ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac
