@@ -145,7 +145,9 @@ class LLMEngine:
         psw = os.environ.get("GAI_DECODE_PSW")  # "1" / "0" overrides the config (same-box A/B)
         if (self.device.type == "cuda" and (cfg.decode_preshuffle if psw is None else psw == "1")
                 and hasattr(model, "preshuffle_decode_weights")):
-            model.preshuffle_decode_weights()  # before KV sizing: the fragment copies are resident
+            # before KV sizing: the fragment copies are resident; at most 20 % of the device's HBM
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            model.preshuffle_decode_weights(budget_bytes=int(0.2 * total))
         # tensor parallel: rank 0 of the TP group plans every step, the other members execute its plans
         ctx = getattr(model, "ctx", None)
         self.tp_size = ctx.tp_size if ctx is not None else 1

@@ -207,10 +207,21 @@ class IncrementalDetokenizer:
                 self.text = self.text[:k]
                 self.stopped = True
                 break
-        limit = len(self.text) if self.stopped else max(self.sent, len(self.text) - self.hold)
+        limit = len(self.text) if self.stopped else max(self.sent, len(self.text) - self._partial_stop())
         delta = self.text[self.sent:limit]
         self.sent = limit
         return delta
+
+    def _partial_stop(self) -> int:
+        """Characters to hold back: the longest unsent suffix of the text that begins a stop string (a stop
+        string may still complete there). Everything before it streams now - a fixed hold of the longest
+        stop string's length would delay the first frame by several tokens (behind a whole prefill wave)."""
+        t, lo = self.text, self.sent
+        for k in range(min(self.hold, len(t) - lo), 0, -1):
+            tail = t[len(t) - k:]
+            if any(s.startswith(tail) for s in self.stop):
+                return k
+        return 0
 
     def flush(self) -> str:
         delta = self.text[self.sent:]

@@ -239,13 +239,20 @@ class LlamaModel:
     # down 36.0 -> 29.3, LM head 238 -> 208, QKV 23.8 -> 21.4, O 17.2 -> 16.4 us.
     DECODE_PROJECTIONS = ("qkv", "o", "gate_up", "down", "proj", "lm_head")
 
-    def preshuffle_decode_weights(self) -> int:
+    def preshuffle_decode_weights(self, budget_bytes: Optional[int] = None) -> int:
         """Attach fragment-shuffled copies of the per-layer projection weights for the decode GEMM
-        (ops.preshuffle_weight); returns the bytes added. Call after the weights are final."""
-        added = 0
-        for k, v in self.w.items():
-            if k.rsplit(".", 1)[-1] in self.DECODE_PROJECTIONS and isinstance(v, torch.Tensor) \
-                    and getattr(v, "_gai_psw", None) is None and ops.preshuffle_weight(v):
+        (ops.preshuffle_weight); returns the bytes added. Call after the weights are final. With
+        ``budget_bytes`` nothing is copied unless every candidate fits (a 70B model on ONE GPU keeps its HBM
+        for the KV cache)."""
+        cand = [v for k, v in self.w.items() if k.rsplit(".", 1)[-1] in self.DECODE_PROJECTIONS
+                and isinstance(v, torch.Tensor) and getattr(v, "_gai_psw", None) is None]
+        need = sum(v.numel() * v.element_size() for v in {id(v): v for v in cand}.values())
+        if budget_bytes is not None and need > budget_bytes:
+            return 0
+        added, seen = 0, set()
+        for v in cand:
+            if id(v) not in seen and ops.preshuffle_weight(v):
+                seen.add(id(v))
                 added += v.numel() * v.element_size()
         return added
 

@@ -236,3 +236,19 @@ def test_stager_overflow_within_a_step_keeps_earlier_regions():
     assert a.tolist() == list(range(40)) and b.tolist() == [3 * i for i in range(100)]
     st.reset()
     assert st.capacity >= 140
+
+
+def test_detokenizer_holds_only_partial_stop_matches():
+    """Streaming holds back only a suffix that may still become a stop string: the first token's text reaches
+    the client at once (served TTFT), a completed stop string is never emitted."""
+    from generativeaiexamples_amd.engine.tokenizer import IncrementalDetokenizer, small_byte_tokenizer
+
+    t = small_byte_tokenizer(512)
+    d = IncrementalDetokenizer(t, stop=["<|eot_id|>", "STOP"])
+    assert d.add(t.encode("H")[0]) == "H"
+    got = "".join(d.add(i) for i in t.encode("i <|eo"))
+    assert got == "i "  # '<|eo' may still become '<|eot_id|>'
+    got += "".join(d.add(i) for i in t.encode("x S"))
+    assert got == "i <|eox "  # no longer a stop prefix: released; 'S' held
+    got += "".join(d.add(i) for i in t.encode("TOP tail"))
+    assert d.stopped and d.text == "Hi <|eox " and got == "i <|eox "
