@@ -56,7 +56,9 @@ for spec in "$@"; do
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
              python3 "${rest[@]}" || exit $?
            python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
-             > /dev/null || exit $? ;;
+             > /dev/null || exit $?
+           python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_trace.csv" --by-grid -o "$O/${n}_grid.csv" \
+             --top 80 > /dev/null || exit $? ;;
     smoke) step 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $? ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac

@@ -14,6 +14,9 @@ def main():
     ap.add_argument("path", help="kernel_stats.csv (a glob is accepted)")
     ap.add_argument("-o", "--out", default=None)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--by-grid", action="store_true",
+                    help="path is a kernel_trace.csv: one row per (kernel, grid size) - tells apart the shapes "
+                         "one template serves (e.g. QKV vs O projections)")
     a = ap.parse_args()
     files = sorted(glob.glob(a.path, recursive=True))
     if not files:
@@ -22,9 +25,14 @@ def main():
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                name = r.get("Name") or r.get("KernelName")
-                calls = int(r.get("Calls", 0))
-                tot = float(r.get("TotalDurationNs", 0))
+                if a.by_grid:
+                    grid = "x".join(r.get(f"Grid_Size_{d}", "?") for d in "XYZ")
+                    name = f"{r.get('Kernel_Name', '?')} grid={grid}"
+                    calls, tot = 1, float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                else:
+                    name = r.get("Name") or r.get("KernelName")
+                    calls = int(r.get("Calls", 0))
+                    tot = float(r.get("TotalDurationNs", 0))
                 c, t = rows.get(name, (0, 0.0))
                 rows[name] = (c + calls, t + tot)
     total = sum(t for _, t in rows.values()) or 1.0
@@ -33,7 +41,7 @@ def main():
     w = csv.writer(open(a.out, "w", newline="") if a.out else sys.stdout)
     w.writerow(["kernel", "calls", "total_ms", "avg_us", "pct"])
     for n, c, t, avg, pct in out[: a.top]:
-        w.writerow([n[:200], c, round(t, 3), round(avg, 2), round(pct, 2)])
+        w.writerow([n[:120] + (n[n.rfind(' grid='):] if ' grid=' in n[120:] else ''), c, round(t, 3), round(avg, 2), round(pct, 2)])
     print(f"# total GPU kernel time {total / 1e6:.1f} ms over {sum(c for _, (c, _) in rows.items())} launches",
           file=sys.stderr)
 

@@ -1,0 +1,73 @@
+"""Cost of the prefill QKV GEMM's RoPE + paged-KV epilogue (gemm_w4d_kernel<EPI_ROPE_KV>) at a headline chunk:
+M tokens packed from prompts of --plen tokens, Llama-3-8B QKV (N = 6144, K = 4096). Arms, interleaved rounds:
+  plain    - the same GEMM writing bf16 qkv (no epilogue work)
+  fused    - GEMM + RoPE + q store + paged K / V^T cache stores (the engine path)
+  fused_nokv - the fused kernel with every slot = -1 (q stores only: isolates the K / V^T cache stores)
+python tools/rope_epi_bench.py [--m 16384] [--plen 2406]
+"""
+import argparse
+import json
+import math
+import time
+
+import torch
+
+from generativeaiexamples_amd import ops
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=16384)
+    ap.add_argument("--plen", type=int, default=2406)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    Hq, Hkv, D, K = 32, 8, 128, 4096
+    N = (Hq + 2 * Hkv) * D
+    M = a.m
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    # packed prompts: positions restart per prompt, each prompt's tokens on its own pages
+    pos = torch.arange(M, device="cuda", dtype=torch.int32) % a.plen
+    seq = torch.arange(M, device="cuda", dtype=torch.int32) // a.plen
+    pages_per_seq = (a.plen + 15) // 16
+    slots = ((seq * pages_per_seq + pos // 16) * 16 + pos % 16).to(torch.int32)
+    nblk = int(slots.max()) // 16 + 1
+    kc = torch.zeros(nblk, Hkv, 16, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.zeros(nblk, Hkv, D, 16, device="cuda", dtype=torch.bfloat16)
+    q = torch.empty(M, Hq, D, device="cuda", dtype=torch.bfloat16)
+    cs = ops.rope_cos_sin(8192, D, 500000.0, device="cuda")
+    nos = torch.full_like(slots, -1)
+    nat = ops.native()
+    ws = torch.empty(0, dtype=torch.float32, device="cuda")
+    arms = {
+        "plain": lambda: nat.gemm(x, w, out, None, None, 0, 0),
+        "fused": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False),
+        "fused_nokv": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, nos, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False),
+    }
+    ts = {k: [] for k in arms}
+    for _ in range(a.rounds):
+        for k, f in arms.items():
+            ts[k].append(timeit(f))
+    flops = 2.0 * M * N * K
+    res = {"M": M, "N": N, "K": K, "plen": a.plen}
+    for k, v in ts.items():
+        v.sort()
+        res[f"{k}_us"] = round(v[len(v) // 2], 1)
+        res[f"{k}_pfs"] = round(flops / (v[len(v) // 2] * 1e-6) / 1e15, 3)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
