@@ -9,7 +9,10 @@
 from __future__ import annotations
 
 import os
+import re
 from typing import Dict, List, Optional, Sequence
+
+import numpy as np
 
 
 class Tokenizer:
@@ -44,26 +47,33 @@ class ByteTokenizer(Tokenizer):
         self.eos_ids = tuple(self.special[e] for e in eos if e in self.special)
         self.pad_id = self.special.get(pad, 0) if pad else 0
 
+    _SPECIAL_START = re.compile(r"[<\[]")
+
+    def _bytes_ids(self, piece: str) -> List[int]:
+        raw = piece.encode("utf-8")
+        if self.offset == 0:
+            return list(raw)
+        return (np.frombuffer(raw, np.uint8).astype(np.int32) + self.offset).tolist()
+
     def encode(self, text: str, add_special: bool = False) -> List[int]:
         ids: List[int] = []
-        i = 0
+        i, n = 0, len(text)
         if self.special:
-            # split on special-token literals present in the text
+            # split on special-token literals present in the text (runs between candidates in one C-level call)
             names = sorted(self.special, key=len, reverse=True)
-            while i < len(text):
+            while i < n:
                 if text[i] == "<" or text[i] == "[":
-                    hit = next((n for n in names if text.startswith(n, i)), None)
+                    hit = next((nm for nm in names if text.startswith(nm, i)), None)
                     if hit is not None:
                         ids.append(self.special[hit])
                         i += len(hit)
                         continue
-                j = i + 1
-                while j < len(text) and text[j] not in "<[":
-                    j += 1
-                ids.extend(b + self.offset for b in text[i:j].encode("utf-8"))
+                m = self._SPECIAL_START.search(text, i + 1)
+                j = m.start() if m else n
+                ids.extend(self._bytes_ids(text[i:j]))
                 i = j
         else:
-            ids = [b + self.offset for b in text.encode("utf-8")]
+            ids = self._bytes_ids(text)
         if add_special and self.bos_id is not None:
             ids = [self.bos_id] + ids
         return ids
