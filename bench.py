@@ -368,6 +368,8 @@ def main():
         log(f"warmup {w}: {dt:.2f}s")
     uniq = set()
     phase = new_phase()
+    engine.phase_ms.clear()  # GAI_STEP_TIMING=1: synchronised per-phase engine wall time of the timed steps
+    stats0 = dict(engine.stats)
     times, ttfts, toks, plens, rtimes = [], [], 0, [], []
     for s in range(args.steps):
         dt, ttft, ntok, plen, rt = run_step(s, phase)
@@ -378,6 +380,7 @@ def main():
         rtimes.append(rt)
         log(f"step {s}: {dt:.3f}s  p50 TTFT {statistics.median(ttft):.3f}s  retrieval {rt * 1000:.1f} ms")
 
+    stats1, phase1 = dict(engine.stats), dict(engine.phase_ms)  # the timed steps only (before the probes)
     # ---------------- untimed TTFT probes on the rank-local shard (no collectives: ranks run them freely)
     probes = {}
     if not args.no_probes:
@@ -434,8 +437,13 @@ def main():
         # wall time per step from retrieval done to the last prompt's first token, then to the last token
         "phase_ms": {k[:-5]: round(1000 * v / max(1, args.steps), 1) for k, v in phase.items() if k.endswith("_wall")},
         "planted_chunks": not args.no_plant,
+        "engine_steps_per_step": {k: round((stats1[k] - stats0.get(k, 0)) / max(1, args.steps), 1)
+                                  for k in ("steps", "multi_step_runs", "chained_runs", "graph_steps")
+                                  if k in stats1},
         **probes,
     }
+    if phase1:
+        out["engine_phase_ms_per_step"] = {k: round(v / max(1, args.steps), 1) for k, v in phase1.items()}
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.json_out:

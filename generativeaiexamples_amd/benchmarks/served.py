@@ -165,10 +165,23 @@ def run_served(args, ctx, st: dict) -> dict:
         dt, _ = step(10_000 + w)
         log(f"served warmup {w}: {dt:.2f}s")
     times, ttfts = [], []
+    # client TTFT split (medians over the timed waves, ms): send -> engine submit (HTTP + retrieval + prompt),
+    # submit -> first token sampled (queue + prefill), first token -> first SSE frame read by the client
+    split = {"send_to_submit": [], "submit_to_first_token": [], "first_token_to_client": []}
     for s_ in range(args.steps):
+        n_t = len(aeng.timings)
         dt, res = step(s_)
         times.append(dt)
         ttfts += [r["ttft"] for r in res]
+        srv = list(aeng.timings)[n_t:]
+        t_send = min(r["t0"] for r in res)
+        for tm in srv:
+            if tm["first_token"] is not None:
+                split["submit_to_first_token"].append(tm["first_token"] - tm["submit"])
+        split["send_to_submit"] += [tm["submit"] - t_send for tm in srv]
+        firsts = sorted(r["t_first"] for r in res if r.get("t_first"))
+        toks = sorted(tm["first_token"] for tm in srv if tm["first_token"] is not None)
+        split["first_token_to_client"] += [a - b for a, b in zip(firsts, toks)]  # k-th first frame vs k-th token
         log(f"served step {s_}: {dt:.3f}s p50 TTFT {statistics.median(r['ttft'] for r in res):.3f}s")
     total = sum(times)
     if world > 1:
@@ -227,5 +240,6 @@ def run_served(args, ctx, st: dict) -> dict:
                    "kv_cache_dtype": "bf16" if args.kv_cache_dtype == "auto" else "fp8_e4m3"},
         "p50_ttft_s": round(percentile(ttfts, 0.5), 4), "p90_ttft_s": round(percentile(ttfts, 0.9), 4),
         "served": True, "tokens_per_query": args.max_tokens, "planted_chunks": not args.no_plant,
+        "ttft_split_p50_ms": {k: round(1000 * statistics.median(v), 1) for k, v in split.items() if v},
         "baseline_qps": round(st["baseline_qps"], 4), **probes,
     }

@@ -36,7 +36,7 @@ async def _one(client, url: str, question: str, max_tokens: int, delay: float = 
             if ch.get("finish_reason") == "[DONE]":
                 break
     t1 = time.perf_counter()
-    return {"ttft": (first or t1) - t0, "e2e": t1 - t0, "chunks": n}
+    return {"ttft": (first or t1) - t0, "e2e": t1 - t0, "chunks": n, "t0": t0, "t_first": first}
 
 
 async def _wave(url: str, questions: List[str], max_tokens: int, delays: List[float]) -> Dict:

@@ -174,7 +174,7 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                  const Tensor& ctx_lens, Tensor& out, Tensor& ws_o, Tensor& ws_ml, double scale, int64_t split_keys,
-                 int64_t max_splits, double k_scale, double v_scale) {
+                 int64_t max_splits, double k_scale, double v_scale, const c10::optional<Tensor>& split_cnt) {
   check_bf16(q, "q");
   const int f8 = kv_cache_fp8(k_cache, v_cache);
   check_i32(block_tables, "block_tables");
@@ -186,10 +186,16 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   const int Hkv = k_cache.size(1);
   TORCH_CHECK(ws_o.numel() >= (int64_t)max_splits * B * Hq * D, "attn_decode: ws_o too small");
   TORCH_CHECK(ws_ml.numel() >= (int64_t)max_splits * B * Hq * 2, "attn_decode: ws_ml too small");
+  int* cnt = nullptr;
+  if (split_cnt.has_value() && split_cnt->defined()) {
+    check_i32(*split_cnt, "split_cnt");
+    TORCH_CHECK(split_cnt->numel() >= (int64_t)B * Hkv, "attn_decode: split_cnt too small");
+    cnt = split_cnt->data_ptr<int>();
+  }
   gai_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                   block_tables.size(1), ctx_lens.data_ptr<int>(), out.data_ptr(), ws_o.data_ptr<float>(),
                   ws_ml.data_ptr<float>(), B, Hq, Hkv, D, (float)scale, split_keys, max_splits, f8, (float)k_scale,
-                  (float)v_scale, cur_stream());
+                  (float)v_scale, cur_stream(), cnt);
 }
 
 void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p, const Tensor& top_k,

@@ -68,7 +68,7 @@ int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
                      int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
-                     float v_scale, hipStream_t st);
+                     float v_scale, hipStream_t st, int* split_cnt = nullptr);
 
 // sampling.hip
 size_t gai_sample_ws_bytes(int B, int V);

@@ -300,15 +300,21 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
 // ----------------------------------------------------------------------------------------------
 // Decode
 // ----------------------------------------------------------------------------------------------
-template <int D, bool PIPE, int H, bool V16, typename KV>
+// FUSE (split_cnt != nullptr): the splits of a (sequence, kv head) are merged in the same launch by the split
+// that finishes last (cdna_hip_programming §Projection GEMM at M = 256, item 2: plain partial stores -> every
+// wave vmcnt(0) -> barrier -> lane-0 agent release -> ticket fetch_add; the last arriver acquires and reads
+// every split with plain loads), instead of a separate attn_decode_reduce launch. cnt[seq * Hkv + g] starts at
+// 0 (zeroed at allocation) and the last arriver resets it for the next launch (graph replays).
+template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int Hq, int Hkv, float scale, int split_keys,
-    int max_splits, float k_scale, float v_scale) {
+    int max_splits, float k_scale, float v_scale, int* __restrict__ cnt) {
   static_assert(sizeof(KV) == 2 || V16, "fp8 KV decode uses the 16-key V^T loads");
   __shared__ __attribute__((aligned(16))) float red_o[4][D][16];
   __shared__ float red_m[4][16], red_l[4][16];
+  __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, gq = lane >> 4;
   const int split = blockIdx.x, g = blockIdx.y, seq = blockIdx.z;
   const int ratio = Hq / Hkv;
@@ -502,6 +508,38 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       }
     }
   }
+  if constexpr (FUSE) {
+    if (nsplit == 1) return;  // wave-uniform for the whole workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores issued and complete
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 may drop the fence's own wait
+      const int t = __hip_atomic_fetch_add(cnt + seq * Hkv + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == nsplit - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int e = tid; e < ratio * D; e += 256) {
+      const int qq = e / D, d = e % D, hq = g * ratio + qq;
+      float M = kNeg;
+      for (int s2 = 0; s2 < nsplit; ++s2) M = fmaxf(M, ws_ml[(((size_t)s2 * B + seq) * Hq + hq) * 2]);
+      float L = 0.f, O = 0.f;
+      for (int s2 = 0; s2 < nsplit; ++s2) {
+        const size_t i = ((size_t)s2 * B + seq) * Hq + hq;
+        const float f = fexp2(ws_ml[i * 2] - M);
+        L += ws_ml[i * 2 + 1] * f;
+        O += ws_o[i * D + d] * f;
+      }
+      out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+    }
+    if (tid == 0) __hip_atomic_store(cnt + seq * Hkv + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int D>
@@ -583,7 +621,7 @@ int gai_attn_prefill_rows_per_tile(int Hq, int Hkv) {
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
                      int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
-                     float v_scale, hipStream_t st) {
+                     float v_scale, hipStream_t st, int* split_cnt) {
   if (B == 0) return;
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
   if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
@@ -591,7 +629,21 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   // GAI_DECODE_VARIANT: 0 = 8-B V^T pieces, 1 = 16-B V^T loads (default), 2 = 16-B + 64 keys per wave step,
   // 3 = 16-B + register double buffer (software pipelined)
   static const int variant = getenv("GAI_DECODE_VARIANT") ? atoi(getenv("GAI_DECODE_VARIANT")) : 1;
+  // in-launch split merge (no attn_decode_reduce launch) when the caller passes the ticket counters
+  const bool fuse = split_cnt != nullptr && max_splits > 1 && variant == 1;
 #define GAI_DEC(DD)                                                                                             \
+  if (D == DD && fuse) {                                                                                        \
+    if (kv_fp8)                                                                                                 \
+      attn_decode_kernel<DD, false, 1, true, fp8, true><<<grid, 256, 0, st>>>(                                  \
+          (const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache, block_tables, max_blocks, ctx_lens,         \
+          (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys, max_splits, k_scale, v_scale, split_cnt);     \
+    else                                                                                                        \
+      attn_decode_kernel<DD, false, 1, true, bf16, true><<<grid, 256, 0, st>>>(                                 \
+          (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, max_blocks, ctx_lens,       \
+          (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys, max_splits, k_scale, v_scale, split_cnt);     \
+    GAI_LAUNCH_CHECK();                                                                                         \
+    return;                                                                                                     \
+  }                                                                                                             \
   if (D == DD) {                                                                                                \
     if (kv_fp8) {                                                                                               \
       auto kern = variant == 2   ? attn_decode_kernel<DD, false, 2, true, fp8>                                  \
@@ -599,7 +651,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                                  : attn_decode_kernel<DD, false, 1, true, fp8>;                                 \
       kern<<<grid, 256, 0, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache, block_tables,        \
                                  max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
-                                 max_splits, k_scale, v_scale);                                                  \
+                                 max_splits, k_scale, v_scale, nullptr);                                         \
     } else {                                                                                                    \
       auto kern = variant == 0   ? attn_decode_kernel<DD, false, 1, false, bf16>                                \
                   : variant == 2 ? attn_decode_kernel<DD, false, 2, true, bf16>                                 \
@@ -607,7 +659,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                                  : attn_decode_kernel<DD, false, 1, true, bf16>;                                \
       kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables,      \
                                  max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
-                                 max_splits, k_scale, v_scale);                                                  \
+                                 max_splits, k_scale, v_scale, nullptr);                                         \
     }                                                                                                           \
     GAI_LAUNCH_CHECK();                                                                                         \
     if (max_splits > 1) {                                                                                       \

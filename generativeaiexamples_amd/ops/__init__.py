@@ -375,6 +375,9 @@ class DecodeWorkspace:
         self.max_splits = max(1, (max_ctx + self.MIN_SPLIT - 1) // self.MIN_SPLIT)
         self.o = torch.empty(self.max_splits * max_batch * Hq * D, dtype=torch.float32, device=device)
         self.ml = torch.empty(self.max_splits * max_batch * Hq * 2, dtype=torch.float32, device=device)
+        # split tickets of the in-launch merge (one per (sequence, kv head) <= max_batch * Hq): zero at
+        # allocation, reset by each merge's last split
+        self.cnt = torch.zeros(max_batch * Hq, dtype=torch.int32, device=device)
 
     @property
     def split_keys(self) -> int:
@@ -412,8 +415,14 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
     assert nsplit <= ws.max_splits, "decode workspace too small for this context"
     out = torch.empty_like(q) if out is None else out
     native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, split, nsplit, k_scale,
-                         v_scale)
+                         v_scale, ws.cnt if _ATTN_FUSE else None)
     return out
+
+
+# GAI_ATTN_FUSE=1: merge decode-attention splits inside the attention launch (ticket + agent release / acquire per
+# split) instead of the separate attn_decode_reduce launch. Off: measured 192.6 vs 117.4 us per Llama-3-8B layer at
+# B = 64, ctx 2600 (the per-workgroup release fence), profiles/r3/attn_fused_merge_ab
+_ATTN_FUSE = os.environ.get("GAI_ATTN_FUSE", "0") == "1"
 
 
 # ---------------------------------------------------------------------------------------------

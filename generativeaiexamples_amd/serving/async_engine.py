@@ -52,6 +52,10 @@ class AsyncLLMEngine:
         self._step_started: Optional[float] = None
         # (request id, generated tokens, finish reason) of recently finished requests (benchmarks, tests)
         self.completed: collections.deque = collections.deque(maxlen=4096)
+        # per finished streamed request, perf_counter timestamps (CLOCK_MONOTONIC: comparable across processes):
+        # submit (generate() entered), first_token (engine sampled it), first_yield (first item handed to the
+        # caller); the served benchmark splits client TTFT into retrieval / queue+prefill / delivery
+        self.timings: collections.deque = collections.deque(maxlen=4096)
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
         self.thread.start()
@@ -123,6 +127,7 @@ class AsyncLLMEngine:
             self.queues.pop(rid, None)
             yield StreamItem("", -1, True, req.finish_reason)
             return
+        t_yield = None
         try:
             while True:
                 o = await q.get()
@@ -130,13 +135,15 @@ class AsyncLLMEngine:
                     raise RuntimeError(f"engine failure: {o!r}")
                 assert isinstance(o, RequestOutput)
                 if first:
-                    METRICS.ttft.observe(time.perf_counter() - t0)
+                    t_yield = time.perf_counter()
+                    METRICS.ttft.observe(t_yield - t0)
                     first = False
                 METRICS.generation_tokens.inc()
                 yield StreamItem(o.delta, o.token_id, o.finished, o.finish_reason)
                 if o.finished:
                     METRICS.e2e.observe(time.perf_counter() - t0)
                     self.completed.append((rid, len(req.output_ids), o.finish_reason))
+                    self.timings.append({"submit": t0, "first_token": req.first_token_time, "first_yield": t_yield})
                     return
         finally:
             if rid in self.queues:  # client went away or error: free the sequence now

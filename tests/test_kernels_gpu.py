@@ -174,6 +174,51 @@ def test_attention_decode(cuda, D, Hq, Hkv):
         _close(o, o_ref, 2e-2, 2e-2, f"decode split={ws.split_keys}")
 
 
+def test_attention_decode_fused_merge_reuse(cuda):
+    """In-launch split merge (ticket counters, last split combines): equal to the separate reduce launch, and
+    the counters reset themselves - many back-to-back launches and graph replays on one workspace, with the
+    number of splits changing between calls, stay exact."""
+    torch.manual_seed(7)
+    D, Hq, Hkv = 128, 32, 8
+    ctx = [5, 130, 700, 1500, 2600, 33, 4000, 257]
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, cuda, seed=2)
+    q = torch.randn(len(ctx), Hq, D, device=cuda, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    ws = ops.DecodeWorkspace(len(ctx), Hq, D, max(ctx), cuda, split_keys=128)
+    nat = ops.native()
+    for trial in range(6):
+        c = torch.tensor([max(1, x - 97 * trial) for x in ctx], dtype=torch.int32, device=cuda)
+        o_f = torch.empty_like(q)
+        o_u = torch.empty_like(q)
+        nsplit = (int(c.max()) + 127) // 128
+        nat.attn_decode(q, kc, vc, bt, c, o_f, ws.o, ws.ml, scale, 128, nsplit, 1.0, 1.0, ws.cnt)
+        nat.attn_decode(q, kc, vc, bt, c, o_u, ws.o, ws.ml, scale, 128, nsplit, 1.0, 1.0, None)
+        assert torch.equal(o_f, o_u), f"trial {trial}"
+        assert int(ws.cnt.abs().sum()) == 0
+    o_ref = ref.attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), c.cpu(), scale)
+    _close(o_f, o_ref, 2e-2, 2e-2, "fused merge")
+    # graph replays
+    c = torch.tensor(ctx, dtype=torch.int32, device=cuda)
+    out = torch.empty_like(q)
+    nsplit = (max(ctx) + 127) // 128
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        nat.attn_decode(q, kc, vc, bt, c, out, ws.o, ws.ml, scale, 128, nsplit, 1.0, 1.0, ws.cnt)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nat.attn_decode(q, kc, vc, bt, c, out, ws.o, ws.ml, scale, 128, nsplit, 1.0, 1.0, ws.cnt)
+    want = torch.empty_like(q)
+    nat.attn_decode(q, kc, vc, bt, c, want, ws.o, ws.ml, scale, 128, nsplit, 1.0, 1.0, None)
+    for _ in range(20):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
+    assert int(ws.cnt.abs().sum()) == 0
+
+
 F8 = torch.float8_e4m3fn
 
 
