@@ -173,14 +173,14 @@ def run_served(args, ctx, st: dict) -> dict:
         dt, res = step(s_)
         times.append(dt)
         ttfts += [r["ttft"] for r in res]
-        srv = list(aeng.timings)[n_t:]
+        tms = list(aeng.timings)[n_t:]
         t_send = min(r["t0"] for r in res)
-        for tm in srv:
+        for tm in tms:
             if tm["first_token"] is not None:
                 split["submit_to_first_token"].append(tm["first_token"] - tm["submit"])
-        split["send_to_submit"] += [tm["submit"] - t_send for tm in srv]
+        split["send_to_submit"] += [tm["submit"] - t_send for tm in tms]
         firsts = sorted(r["t_first"] for r in res if r.get("t_first"))
-        toks = sorted(tm["first_token"] for tm in srv if tm["first_token"] is not None)
+        toks = sorted(tm["first_token"] for tm in tms if tm["first_token"] is not None)
         split["first_token_to_client"] += [a - b for a, b in zip(firsts, toks)]  # k-th first frame vs k-th token
         log(f"served step {s_}: {dt:.3f}s p50 TTFT {statistics.median(r['ttft'] for r in res):.3f}s")
     total = sum(times)

@@ -82,9 +82,12 @@ class VectorStore:
         if getattr(self, "_batcher", None) is None:
             from ..engine.embedder import DynamicBatcher
 
+            from ..utils.streams import RETRIEVAL_GATE
+
             with self.lock:
                 if getattr(self, "_batcher", None) is None:
-                    self._batcher = DynamicBatcher(self._search_batch, max_batch=256, name=f"search-{self.name}")
+                    self._batcher = DynamicBatcher(self._search_batch, max_batch=256, name=f"search-{self.name}",
+                                                   gate=RETRIEVAL_GATE)
         return self._batcher
 
     def _search_batch(self, items: List[Tuple[str, int, Optional[float]]]) -> List[List[Tuple[Document, float]]]:

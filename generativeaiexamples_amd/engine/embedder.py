@@ -162,7 +162,10 @@ class Embedder:
         if getattr(self, "_batcher", None) is None:
             with self.lock:
                 if getattr(self, "_batcher", None) is None:
-                    self._batcher = DynamicBatcher(self._embed_requests, max_batch=256, name="embed-batcher")
+                    from ..utils.streams import RETRIEVAL_GATE
+
+                    self._batcher = DynamicBatcher(self._embed_requests, max_batch=256, name="embed-batcher",
+                                                   gate=RETRIEVAL_GATE)
         return self._batcher
 
     def _embed_requests(self, reqs: List[Tuple[Tuple[str, ...], str, str]]) -> List[torch.Tensor]:
@@ -313,8 +316,10 @@ class DynamicBatcher:
     batch. ``max_delay_ms`` > 0 additionally holds a batch that is not yet a preferred size for up to that
     long to collect more. ``batch_sizes`` keeps the recent batch sizes (tests / metrics)."""
 
-    def __init__(self, fn, max_batch: int = 256, max_delay_ms: float = 0.0, preferred=None, name="dynamic-batcher"):
+    def __init__(self, fn, max_batch: int = 256, max_delay_ms: float = 0.0, preferred=None, name="dynamic-batcher",
+                 gate=None):
         self.fn, self.max_batch, self.max_delay = fn, max_batch, max_delay_ms / 1000.0
+        self.gate = gate  # utils.streams.RetrievalGate: a request counts as pending from submit to result
         self.preferred = set(preferred or [1 << i for i in range(9) if (1 << i) <= max_batch])
         self.q: List[Tuple[object, Future]] = []
         self.cv = threading.Condition()
@@ -328,6 +333,9 @@ class DynamicBatcher:
         with self.cv:
             if self.stop:
                 raise RuntimeError("batcher closed")
+            if self.gate is not None:
+                self.gate.enter()
+                f.add_done_callback(lambda _f: self.gate.exit())
             self.q.append((item, f))
             self.cv.notify()
         return f

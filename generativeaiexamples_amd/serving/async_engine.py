@@ -23,6 +23,7 @@ from typing import AsyncIterator, Dict, Iterator, List, Optional
 from ..engine.llm_engine import LLMEngine, RequestOutput
 from ..engine.sampling import SamplingParams
 from ..utils.metrics import METRICS
+from ..utils.streams import RETRIEVAL_GATE
 
 
 @dataclass
@@ -49,6 +50,7 @@ class AsyncLLMEngine:
         self.healthy = True
         self.error: Optional[BaseException] = None
         self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("GAI_WATCHDOG_S", "300"))
+        self.admission_wait_s = float(os.environ.get("GAI_ADMISSION_WAIT_MS", "25")) / 1000.0
         self._step_started: Optional[float] = None
         # (request id, generated tokens, finish reason) of recently finished requests (benchmarks, tests)
         self.completed: collections.deque = collections.deque(maxlen=4096)
@@ -90,6 +92,7 @@ class AsyncLLMEngine:
                     self.cv.wait(0.05)
             if not self.running:
                 break
+            self._admission_wait(eng)
             try:
                 t0 = self._step_started = time.perf_counter()
                 outs = eng.step()
@@ -108,6 +111,18 @@ class AsyncLLMEngine:
                 loop.call_soon_threadsafe(q.put_nowait, o)
                 if o.finished:
                     self.queues.pop(o.request_id, None)
+
+    def _admission_wait(self, eng) -> None:
+        """Before a step that would only start prefill for newly queued prompts (nothing running, nothing in
+        flight), give query-path work still pending in this process (utils.streams.RETRIEVAL_GATE) up to
+        ``admission_wait_s`` (env GAI_ADMISSION_WAIT_MS, default 25) to finish, so concurrent arrivals share
+        that prefill. Never delays decode steps of running sequences."""
+        if self.admission_wait_s <= 0 or not RETRIEVAL_GATE.busy():
+            return
+        sched = getattr(eng, "sched", None)
+        if sched is None or getattr(eng, "_pending", None) is not None or sched.num_running() > 0:
+            return
+        RETRIEVAL_GATE.wait_idle(self.admission_wait_s)
 
     async def generate(self, prompt_ids: List[int], params: SamplingParams,
                        request_id: Optional[str] = None, images: Optional[list] = None,

@@ -108,3 +108,28 @@ def test_64_concurrent_generate_streams_with_8_threads(served):
     emb = utils.get_hub().embedder(utils.get_config().embeddings.model_name)
     assert sum(store.batcher.batch_sizes[-n:]) >= n
     assert max(emb.batcher.batch_sizes) > 1 or max(store.batcher.batch_sizes) > 1
+
+
+def test_retrieval_gate_counts_pending_batcher_requests():
+    """Query-path requests count as pending from submit until their result (RetrievalGate), so the serving
+    loop can let a burst of concurrent retrievals join one prefill."""
+    import threading
+
+    from generativeaiexamples_amd.engine.embedder import DynamicBatcher
+    from generativeaiexamples_amd.utils.streams import RetrievalGate
+
+    gate = RetrievalGate()
+    release = threading.Event()
+
+    def fn(items):
+        release.wait(5)
+        return [x * 2 for x in items]
+
+    b = DynamicBatcher(fn, max_batch=8, gate=gate)
+    futs = [b.submit(i) for i in range(5)]
+    assert gate.busy() and gate.n == 5
+    assert not gate.wait_idle(0.05)
+    release.set()
+    assert [f.result(5) for f in futs] == [0, 2, 4, 6, 8]
+    assert gate.wait_idle(5) and not gate.busy()
+    b.close()
