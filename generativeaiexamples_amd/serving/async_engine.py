@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import concurrent.futures
 import faulthandler
 import logging
 import os
@@ -58,6 +59,7 @@ class AsyncLLMEngine:
         # submit (generate() entered), first_token (engine sampled it), first_yield (first item handed to the
         # caller); the served benchmark splits client TTFT into retrieval / queue+prefill / delivery
         self.timings: collections.deque = collections.deque(maxlen=4096)
+        self.inbox: collections.deque = collections.deque()  # (fn, args, kwargs, future) run between steps
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="llm-engine")
         self.thread.start()
@@ -84,15 +86,40 @@ class AsyncLLMEngine:
     def tokenizer(self):
         return self.engine.tok
 
+    def _call(self, fn, *args, **kw) -> concurrent.futures.Future:
+        """Run ``fn`` on the engine thread between steps. Request admission and aborts go through here: the
+        engine holds its lock for a whole step (a prefill chunk waits ~0.2 s on the GPU), and an event-loop
+        thread blocked on that lock stalls every open SSE stream (served first-frame delay 0.5 s p50)."""
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        with self.cv:
+            self.inbox.append((fn, args, kw, fut))
+            self.cv.notify()
+        return fut
+
+    def _drain(self):
+        while True:
+            with self.cv:
+                if not self.inbox:
+                    return
+                fn, args, kw, fut = self.inbox.popleft()
+            try:
+                fut.set_result(fn(*args, **kw))
+            except BaseException as e:  # noqa: BLE001 - delivered to the caller
+                fut.set_exception(e)
+
     def _loop(self):
         eng = self.engine
         while self.running:
             with self.cv:
-                while self.running and not eng.has_work():
+                while self.running and not self.inbox and not eng.has_work():
                     self.cv.wait(0.05)
             if not self.running:
                 break
+            self._drain()
+            if not eng.has_work():
+                continue
             self._admission_wait(eng)
+            self._drain()  # requests that arrived during the wait join this step
             try:
                 t0 = self._step_started = time.perf_counter()
                 outs = eng.step()
@@ -133,9 +160,12 @@ class AsyncLLMEngine:
         self.queues[rid] = (loop, q)
         t0 = time.perf_counter()
         first = True
-        with self.cv:
-            req = self.engine.add_request(prompt_ids, params, rid, images=images, lora=lora)
-            self.cv.notify()
+        try:
+            req = await asyncio.wrap_future(self._call(self.engine.add_request, prompt_ids, params, rid, images=images,
+                                                       lora=lora))
+        except BaseException:
+            self.queues.pop(rid, None)
+            raise
         METRICS.requests_total.inc()
         METRICS.prompt_tokens.inc(len(prompt_ids))
         if req.finished:  # zero-budget request
@@ -161,10 +191,9 @@ class AsyncLLMEngine:
                     self.timings.append({"submit": t0, "first_token": req.first_token_time, "first_yield": t_yield})
                     return
         finally:
-            if rid in self.queues:  # client went away or error: free the sequence now
+            if rid in self.queues:  # client went away or error: free the sequence now (on the engine thread)
                 self.queues.pop(rid, None)
-                with self.cv:
-                    self.engine.abort(rid)
+                self._call(self.engine.abort, rid)
 
     def generate_sync(self, prompt_ids: List[int], params: SamplingParams,
                       request_id: Optional[str] = None, images: Optional[list] = None) -> Iterator[StreamItem]:
@@ -181,9 +210,11 @@ class AsyncLLMEngine:
 
         self.queues[rid] = (_Shim, q)
         t0 = time.perf_counter()
-        with self.cv:
-            req = self.engine.add_request(prompt_ids, params, rid, images=images)
-            self.cv.notify()
+        try:
+            req = self._call(self.engine.add_request, prompt_ids, params, rid, images=images).result()
+        except BaseException:
+            self.queues.pop(rid, None)
+            raise
         METRICS.requests_total.inc()
         if req.finished:
             self.queues.pop(rid, None)
@@ -205,8 +236,7 @@ class AsyncLLMEngine:
         finally:
             if rid in self.queues:
                 self.queues.pop(rid, None)
-                with self.cv:
-                    self.engine.abort(rid)
+                self._call(self.engine.abort, rid)
 
     async def complete(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None,
                        images: Optional[list] = None, lora: Optional[str] = None):
@@ -220,6 +250,11 @@ class AsyncLLMEngine:
 
     def shutdown(self):
         self.running = False
+        with self.cv:
+            pending, self.inbox = list(self.inbox), collections.deque()
+            self.cv.notify_all()
+        for _, _, _, fut in pending:
+            fut.set_exception(RuntimeError("engine shut down"))
         self._stop.set()
         with self.cv:
             self.cv.notify_all()
