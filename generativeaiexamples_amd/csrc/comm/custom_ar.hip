@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "gai_common.h"
 #include "gai_kernels.h"
 
@@ -57,7 +59,19 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 struct ArPtrs {
   char* data[GAI_AR_MAX_WORLD];
   uint32_t* sig[GAI_AR_MAX_WORLD];
+  uint32_t spin_limit;  // bounded peer wait (s_sleep polls) before the error flag is raised
 };
+
+// 2^26 polls (~2 s) by default; GAI_AR_SPIN_LOG2 raises it where ranks legitimately lag by seconds (every
+// rank of a TP rehearsal time-slicing ONE GPU and a few CPU cores)
+static uint32_t ar_spin_limit() {
+  static const uint32_t v = [] {
+    const char* e = getenv("GAI_AR_SPIN_LOG2");
+    const int l = e ? atoi(e) : 26;
+    return 1u << (l < 20 ? 20 : l > 31 ? 31 : l);
+  }();
+  return v;
+}
 
 template <int W, bool F32>
 __global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in, uint4* out,
@@ -90,7 +104,7 @@ __global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in,
     uint32_t spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26)) {  // ~seconds: a peer died or diverged; never hang the GPU
+      if (++spins > p.spin_limit) {  // ~seconds: a peer died or diverged; never hang the GPU
         atomicOr(err, 1);
         break;
       }
@@ -155,7 +169,7 @@ __global__ __launch_bounds__(kArThreads) void ar_rmsnorm_kernel(const uint4* in,
     uint32_t spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26)) {
+      if (++spins > p.spin_limit) {
         atomicOr(err, 1);
         break;
       }
@@ -235,7 +249,7 @@ __global__ __launch_bounds__(kArThreads) void ar_twoshot_kernel(const uint4* in,
       uint32_t spins = 0;
       while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 26)) {
+        if (++spins > p.spin_limit) {
           atomicOr(err, 1);
           break;
         }
@@ -303,6 +317,7 @@ void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, voi
   const int64_t nblk = (bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
   if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "custom_allreduce: message too large");
   ArPtrs p{};
+  p.spin_limit = ar_spin_limit();
   for (int q = 0; q < world; ++q) {
     p.data[q] = static_cast<char*>(peer_data[q]);
     p.sig[q] = peer_sig[q];
@@ -340,6 +355,7 @@ void gai_custom_allreduce_twoshot(const void* in, void* out, int64_t bytes, int 
   const int64_t nblk = (seg + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
   if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "allreduce two-shot: too many blocks");
   ArPtrs p{};
+  p.spin_limit = ar_spin_limit();
   for (int q = 0; q < world; ++q) {
     p.data[q] = static_cast<char*>(peer_data[q]);
     p.sig[q] = peer_sig[q];
@@ -376,6 +392,7 @@ void gai_custom_allreduce_rmsnorm(const void* in, void* out, void* residual, con
   const int64_t nblk = (bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
   if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "allreduce_rmsnorm: message too large");
   ArPtrs p{};
+  p.spin_limit = ar_spin_limit();
   for (int q = 0; q < world; ++q) {
     p.data[q] = static_cast<char*>(peer_data[q]);
     p.sig[q] = peer_sig[q];

@@ -380,6 +380,9 @@ namespace {
 template <int MB>
 int dec2_part_ks(int N, int K, int NT, bool exact) {
   const int blocks = (N + 16 * NT - 1) / (16 * NT);
+  static const int force_ks = getenv("GAI_DEC2_PART_KS") ? atoi(getenv("GAI_DEC2_PART_KS")) : 0;  // A/B sweeps
+  if (force_ks > 1)
+    return K % force_ks == 0 && (K / force_ks) % 32 == 0 && dec2_shape_ok<MB>(NT, K / force_ks) ? force_ks : 0;
   for (int KS = 2; KS <= 16; ++KS) {
     if (K % KS || (K / KS) % 32 || !dec2_shape_ok<MB>(NT, K / KS)) continue;
     if (exact ? (blocks * KS) % 256 == 0 : blocks * KS >= 192) return KS;

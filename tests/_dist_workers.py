@@ -676,6 +676,8 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
     # queue per process keeps 8 processes within the device's mapped queues (no time-sliced queue, whose
     # kernel would never meet its peers)
     os.environ["GPU_MAX_HW_QUEUES"] = "1"
+    # ranks share a few CPU cores too: a peer can reach a collective seconds late without being dead
+    os.environ["GAI_AR_SPIN_LOG2"] = "29"
     from generativeaiexamples_amd.parallel import dist as gdist
 
     ctx = gdist.init_distributed(tp_size=world, backend="gloo")
