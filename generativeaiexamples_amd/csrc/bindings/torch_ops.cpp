@@ -99,7 +99,8 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, 
 // epilogue for M >= 1024. False: nothing launched, the caller runs linear + rope_kv_write.
 bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias, const Tensor& pos,
                   const Tensor& cos_sin, const Tensor& slots, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
-                  int64_t Hq, int64_t Hkv, int64_t D, double k_scale, double v_scale, Tensor& ws, bool psw) {
+                  int64_t Hq, int64_t Hkv, int64_t D, double k_scale, double v_scale, Tensor& ws, bool psw,
+                  const optional<Tensor>& tail_cnt) {
   check_bf16(A, "A");
   check_bf16(B, "B");
   check_i32(pos, "positions");
@@ -120,10 +121,16 @@ bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias
                                     k_cache.data_ptr(), v_cache.data_ptr(), M, K, Hq, Hkv, D, f8, cur_stream()) != 0;
   TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
               "gemm_rope_kv: workspace too small");
+  int* cnt = nullptr;
+  if (tail_cnt && tail_cnt->defined()) {
+    check_i32(*tail_cnt, "tail_cnt");
+    TORCH_CHECK(tail_cnt->numel() >= (N + 127) / 128, "gemm_rope_kv: tail_cnt too small");
+    cnt = tail_cnt->data_ptr<int>();
+  }
   return gai_gemm_splitk_rope_kv(A.data_ptr(), B.data_ptr(), opt_ptr(bias), pos.data_ptr<int>(),
                                  cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
                                  k_cache.data_ptr(), v_cache.data_ptr(), M, Hq, Hkv, D, f8, (float)k_scale,
-                                 (float)v_scale, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream(), K) != 0;
+                                 (float)v_scale, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream(), K, cnt) != 0;
 }
 
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,

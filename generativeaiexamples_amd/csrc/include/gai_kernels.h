@@ -47,11 +47,12 @@ void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, co
 int gai_gemm_dec2_ok(int M, int N, int K, int epi);
 // gemm_splitk.hip fused decode QKV tail: split-K QKV projection, then ONE kernel sums the partials (+ bias),
 // applies RoPE and writes q / the paged K, V^T caches (as gai_rope_kv_write). Returns 0 (nothing launched)
-// when the shape does not take the split-K path; ws as gai_gemm_splitk.
+// when the shape does not take the split-K path; ws as gai_gemm_splitk. tail_cnt (zeroed int32 ticket counters,
+// >= N / 128, left zeroed): at head_dim 128 the sum + RoPE + KV write runs inside the GEMM launch instead.
 int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
                             const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int Hq, int Hkv,
                             int D, int kv_fp8, float k_scale, float v_scale, float* ws, int psw, hipStream_t st,
-                            int K);
+                            int K, int* tail_cnt = nullptr);
 bool gai_gemm_dec2(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
                    int epi, int out_f32, hipStream_t st, int psw = 0);
 // deep-K decode projections: K split over workgroups into fp32 slabs ws[KS][M][N]; returns KS (0: not handled)

@@ -301,10 +301,58 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
 // Decode
 // ----------------------------------------------------------------------------------------------
 // FUSE (split_cnt != nullptr): the splits of a (sequence, kv head) are merged in the same launch by the split
-// that finishes last (cdna_hip_programming §Projection GEMM at M = 256, item 2: plain partial stores -> every
-// wave vmcnt(0) -> barrier -> lane-0 agent release -> ticket fetch_add; the last arriver acquires and reads
-// every split with plain loads), instead of a separate attn_decode_reduce launch. cnt[seq * Hkv + g] starts at
-// 0 (zeroed at allocation) and the last arriver resets it for the next launch (graph replays).
+// that finishes last, instead of a separate attn_decode_reduce launch. Hand-off without any fence
+// (cdna_hip_programming Guideline 16, R1 form): the partials are stored write-through (sc1, relaxed agent-scope
+// stores, so nothing is left dirty in this XCD's L2) -> every wave vmcnt(0) -> barrier -> lane 0 relaxed agent
+// ticket fetch_add; the last arriver reads every split with sc1 loads (they bypass the CU's L1, so no acquire
+// is needed). The first version published with a per-workgroup agent release (buffer_wbl2: 192.6 vs 117.4 us
+// per layer). cnt[seq * Hkv + g] starts at 0 (zeroed at allocation) and the last arriver resets it for the next
+// launch (graph replays).
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store((gu32_t*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load((gu32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Merge the flash-decoding partials (O, max, sum) of ns splits for one (sequence, q head, dim): groups of
+// kMergeGroup splits, every load of a group issued before its math, running-max rescale between groups. The
+// separate reduce launch and the in-launch merge (SC1: write-through partials read with sc1 loads) share it,
+// so both round identically.
+constexpr int kMergeGroup = 8;
+template <bool SC1>
+__device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_ml, int B, int Hq, int D, int seq,
+                                             int hq, int d, int ns, float& L, float& O) {
+  float M = kNeg;
+  L = 0.f;
+  O = 0.f;
+  for (int s0 = 0; s0 < ns; s0 += kMergeGroup) {
+    float m[kMergeGroup], l[kMergeGroup], o[kMergeGroup];
+#pragma unroll
+    for (int j = 0; j < kMergeGroup; ++j) {
+      const size_t i = ((size_t)min(s0 + j, ns - 1) * B + seq) * Hq + hq;
+      m[j] = SC1 ? ld_sc1(ws_ml + i * 2) : ws_ml[i * 2];
+      l[j] = SC1 ? ld_sc1(ws_ml + i * 2 + 1) : ws_ml[i * 2 + 1];
+      o[j] = SC1 ? ld_sc1(ws_o + i * D + d) : ws_o[i * D + d];
+    }
+    float Mn = M;
+#pragma unroll
+    for (int j = 0; j < kMergeGroup; ++j) Mn = s0 + j < ns ? fmaxf(Mn, m[j]) : Mn;
+    if (s0 > 0) {
+      const float a = fexp2(M - Mn);
+      L *= a;
+      O *= a;
+    }
+#pragma unroll
+    for (int j = 0; j < kMergeGroup; ++j) {
+      const float f = s0 + j < ns ? fexp2(m[j] - Mn) : 0.f;
+      L += l[j] * f;
+      O += o[j] * f;
+    }
+    M = Mn;
+  }
+}
+
 template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
@@ -500,6 +548,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const int hq = g * ratio + qq;
     if (nsplit == 1) {
       out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+    } else if constexpr (FUSE) {
+      st_sc1(ws_o + (((size_t)split * B + seq) * Hq + hq) * D + d, O);
+      if (d == 0) {
+        st_sc1(ws_ml + (((size_t)split * B + seq) * Hq + hq) * 2, M);
+        st_sc1(ws_ml + (((size_t)split * B + seq) * Hq + hq) * 2 + 1, L);
+      }
     } else {
       ws_o[(((size_t)split * B + seq) * Hq + hq) * D + d] = O;
       if (d == 0) {
@@ -510,32 +564,17 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
   if constexpr (FUSE) {
     if (nsplit == 1) return;  // wave-uniform for the whole workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores issued and complete
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partials have landed
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 may drop the fence's own wait
-      const int t = __hip_atomic_fetch_add(cnt + seq * Hkv + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == nsplit - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_last = last;
-    }
+    if (tid == 0) s_last = __hip_atomic_fetch_add(cnt + seq * Hkv + g, 1, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
     __syncthreads();
     if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
     for (int e = tid; e < ratio * D; e += 256) {
       const int qq = e / D, d = e % D, hq = g * ratio + qq;
-      float M = kNeg;
-      for (int s2 = 0; s2 < nsplit; ++s2) M = fmaxf(M, ws_ml[(((size_t)s2 * B + seq) * Hq + hq) * 2]);
-      float L = 0.f, O = 0.f;
-      for (int s2 = 0; s2 < nsplit; ++s2) {
-        const size_t i = ((size_t)s2 * B + seq) * Hq + hq;
-        const float f = fexp2(ws_ml[i * 2] - M);
-        L += ws_ml[i * 2 + 1] * f;
-        O += ws_o[i * D + d] * f;
-      }
+      float L, O;
+      merge_splits<true>(ws_o, ws_ml, B, Hq, D, seq, hq, d, nsplit, L, O);
       out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
     }
     if (tid == 0) __hip_atomic_store(cnt + seq * Hkv + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -550,15 +589,8 @@ __global__ void attn_decode_reduce_kernel(const float* __restrict__ ws_o, const 
   const int ctx = ctx_lens[seq];
   const int ns = (ctx + split_keys - 1) / split_keys;
   if (ns <= 1) return;
-  float M = kNeg;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, ws_ml[(((size_t)s * B + seq) * Hq + hq) * 2]);
-  float L = 0.f, O = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const size_t i = ((size_t)s * B + seq) * Hq + hq;
-    const float f = fexp2(ws_ml[i * 2] - M);
-    L += ws_ml[i * 2 + 1] * f;
-    O += ws_o[i * D + d] * f;
-  }
+  float L, O;
+  merge_splits<false>(ws_o, ws_ml, B, Hq, D, seq, hq, d, ns, L, O);
   out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 

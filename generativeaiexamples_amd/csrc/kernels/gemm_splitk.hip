@@ -13,6 +13,8 @@
 //  * K is split over gridDim.y so every projection launches >= ~512 workgroups; fp32 partials land
 //    in a workspace [KS, M, N] and a reduce kernel sums them and applies the fused epilogue
 //    (bias / GELU / ReLU / quick-GELU / residual / interleaved SwiGLU), writing bf16 or fp32.
+#include <type_traits>
+
 #include "gai_common.h"
 #include "gai_epilogue.h"
 #include "gai_kernels.h"
@@ -31,9 +33,69 @@ __device__ __forceinline__ size_t psw_offset(int nt, int kt, int K, int lane) {
   return (((size_t)nt * (K / 32) + kt) * 64 + lane) * 8;
 }
 
-template <int MB, bool PSW, int WPG>
+// In-launch decode QKV tail (RopeTail): the K-slices of a 128-column tile (= one head at head_dim 128) hand their
+// partials to the slice that finishes last, which sums them (+ bias), rounds to bf16, applies RoPE and writes q /
+// the paged K, V^T caches - the work of splitk_rope_kv_kernel without its launch. Hand-off as the decode-attention
+// split merge (cdna_hip_programming Guideline 16, R1): write-through (sc1) partial stores, every wave vmcnt(0),
+// barrier, lane 0 relaxed agent ticket; the last arriver reads the slabs with sc1 loads. cnt[tile] is zero between
+// launches (zeroed at allocation, reset by the last arriver).
+struct RopeTail {
+  int* cnt;
+  const bf16* bias;
+  const int* pos;
+  const float* cos_sin;
+  const int* slots;
+  bf16* q_out;
+  void* k_cache;
+  void* v_cache;
+  int Hq, Hkv;
+  float inv_ks, inv_vs;
+};
+constexpr int kTailMaxKS = 8;  // K-slices one last arriver sums (legacy_ks never exceeds 8 at K <= 4096)
+
+// Reducer of one 128-column tile = head h: 16 threads per token row, each owning rotation pairs (i0..i0+3,
+// i0+64..i0+67), slabs summed in slice order from 0 (the rounding of sum_slabs / splitk_rope_kv_kernel).
+template <typename KV>
+__device__ void rope_tail_reduce(const float* part, int KS, int M, int N, int h, const RopeTail& t, int tid,
+                                 int nthreads) {
+  constexpr int D = 128, LPH = D / 8;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part), (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  for (int e = tid; e < M * LPH; e += nthreads) {
+    const int row = e / LPH, i0 = (e % LPH) * 4;
+    const int c1 = h * D + i0, c2 = c1 + D / 2;
+    float4 x[kTailMaxKS][2];
+#pragma unroll
+    for (int k = 0; k < kTailMaxKS; ++k) {  // every slab load issued before the sums (sc1: past this CU's L1)
+      const unsigned base = (unsigned)((((size_t)min(k, KS - 1) * M + row) * N) * 4);
+      x[k][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, base + c1 * 4, 0, 16));
+      x[k][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, base + c2 * 4, 0, 16));
+    }
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kTailMaxKS; ++k) {
+      if (k < KS) {
+        a[0] += x[k][0].x; a[1] += x[k][0].y; a[2] += x[k][0].z; a[3] += x[k][0].w;  // NOLINT
+        b[0] += x[k][1].x; b[1] += x[k][1].y; b[2] += x[k][1].z; b[3] += x[k][1].w;  // NOLINT
+      }
+    }
+    bf16x4 x1, x2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x1[j] = (bf16)(t.bias ? a[j] + (float)t.bias[c1 + j] : a[j]);
+      x2[j] = (bf16)(t.bias ? b[j] + (float)t.bias[c2 + j] : b[j]);
+    }
+    rope_kv_store<D>(x1, x2, row, h, i0, t.pos, t.cos_sin, t.slots, t.q_out, reinterpret_cast<KV*>(t.k_cache),
+                     reinterpret_cast<KV*>(t.v_cache), t.Hq, t.Hkv, 1, t.inv_ks, t.inv_vs);
+  }
+}
+
+template <int MB, bool PSW, int WPG, typename TAILKV = void>
 __global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                               float* __restrict__ part, int M, int N, int K, int KL) {
+                                                               float* __restrict__ part, int M, int N, int K, int KL,
+                                                               RopeTail tail = RopeTail{}) {
+  constexpr bool TAIL = !std::is_void<TAILKV>::value;
+  static_assert(!TAIL || WPG == 8, "the QKV tail owns one 128-column head per workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // A slice [16*MB][KL] bf16, swizzled chunks
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -100,14 +162,52 @@ __global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __res
 
   // ---- partials: lane holds D[m = 16i + 4(lane>>4) + r][n = 16*wid + (lane&15)]
   const int nc = n0 + 16 * wid + (lane & 15);
-  if (nc < N) {
+  if constexpr (!TAIL) {
+    if (nc < N) {
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + 4 * (lane >> 4) + r;
+          if (m < M) part[((size_t)ks * M + m) * N + nc] = acc[i][r];
+        }
+    }
+  } else {
+    // write-through partials as whole 16-B stores (a per-lane dword sc1 store is one fabric write each, ~6x the
+    // time per byte): the [ROWS][128] fp32 tile goes through LDS (row stride 132 floats), then each thread
+    // stores 16-B row pieces with sc1
+    constexpr int TS = 16 * WPG + 4;
+    float* tile = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is done reading the staged activation slice
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * i + 4 * (lane >> 4) + r;
-        if (m < M) part[((size_t)ks * M + m) * N + nc] = acc[i][r];
+      for (int r = 0; r < 4; ++r) tile[(16 * i + 4 * (lane >> 4) + r) * TS + 16 * wid + (lane & 15)] = acc[i][r];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0x7fffffff, 0x00020000);
+    for (int e = tid; e < ROWS * 4 * WPG; e += 64 * WPG) {
+      const int m = e / (4 * WPG), c = 4 * (e % (4 * WPG));
+      if (m < M) {
+        const float4 v = *reinterpret_cast<const float4*>(tile + m * TS + c);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), rs,
+                                               (unsigned)((((size_t)ks * M + m) * N + n0 + c) * 4), 0, 16);
       }
+    }
+  }
+  if constexpr (TAIL) {
+    // the flag word sits past the staged slice in the ONE dynamic LDS array (a second __shared__ object next to
+    // global_load_lds staging can make hipcc wait vmcnt(0) in the k-loop)
+    int* s_last = reinterpret_cast<int*>(smem + (size_t)chunks * 16);  // past the slice (>= the partial tile)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partials have landed
+    __syncthreads();
+    if (tid == 0)
+      *s_last = __hip_atomic_fetch_add(tail.cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (int)gridDim.y - 1;
+    __syncthreads();
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    rope_tail_reduce<TAILKV>(part, gridDim.y, M, N, blockIdx.x, tail, tid, 64 * WPG);
+    if (tid == 0) __hip_atomic_store(tail.cnt + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -662,14 +762,63 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(const float* __rest
 
 }  // namespace
 
+namespace {
+
+// LDS-staged split-K QKV with the in-launch reduce + RoPE tail (RopeTail). Returns false when the shape is not
+// the one the tail is written for (head_dim 128 = the 128-column tile, legacy kernel, 2..8 K-slices).
+template <typename KV>
+bool launch_rope_tail(const void* A, const void* B, int M, int N, int K, float* ws, int psw, const RopeTail& t,
+                      hipStream_t st) {
+  if (!use_legacy(N, K) || splitk_wpg() != 8 || N % 128) return false;
+  const int KS = legacy_ks(M, N, K);
+  if (KS < 2 || KS > kTailMaxKS) return false;
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  const int KL = K / KS;
+  const size_t lds = (size_t)16 * MB * KL * 2 + 16;  // + the last-arriver flag
+  dim3 grid(N / 128, KS);
+#define GAI_RT(MBV)                                                                                           \
+  if (MB == MBV) {                                                                                            \
+    static bool once = false;                                                                                 \
+    if (!once) {                                                                                              \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, false, 8, KV>),               \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true, 8, KV>),                \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      once = true;                                                                                            \
+    }                                                                                                         \
+    if (psw)                                                                                                  \
+      gemm_splitk_kernel<MBV, true, 8, KV><<<grid, 512, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, K, \
+                                                                   KL, t);                                    \
+    else                                                                                                      \
+      gemm_splitk_kernel<MBV, false, 8, KV><<<grid, 512, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N,   \
+                                                                    K, KL, t);                                \
+    GAI_LAUNCH_CHECK();                                                                                       \
+    return true;                                                                                              \
+  }
+  GAI_RT(1)
+  GAI_RT(2)
+  GAI_RT(4)
+#undef GAI_RT
+  return false;
+}
+
+}  // namespace
+
 int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
                             const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int Hq, int Hkv,
                             int D, int kv_fp8, float k_scale, float v_scale, float* ws, int psw, hipStream_t st,
-                            int K) {
+                            int K, int* tail_cnt) {
   const int N = (Hq + 2 * Hkv) * D;
   if (M < 1 || M > 64 || (D != 64 && D != 128 && D != 256) || N % 16) return 0;
   if (gai_gemm_dec2_ok(M, N, K, bias ? EPI_BIAS : EPI_NONE)) return 0;  // single-pass kernel owns it
   const int ks2 = gai_gemm_dec2_partials_ks(M, N, K);
+  if (tail_cnt != nullptr && D == 128 && !ks2) {
+    const RopeTail t{tail_cnt, (const bf16*)bias, pos, cos_sin, slots, (bf16*)q_out, k_cache, v_cache, Hq, Hkv,
+                     1.f / k_scale, 1.f / v_scale};
+    if (kv_fp8 ? launch_rope_tail<fp8>(A, B, M, N, K, ws, psw, t, st)
+               : launch_rope_tail<bf16>(A, B, M, N, K, ws, psw, t, st))
+      return 1;
+  }
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (KS <= 1) return 0;
   if (ks2)

@@ -175,17 +175,38 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
         psw = getattr(w, "_gai_psw", None)
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x.device)
         if nat.gemm_rope_kv(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, positions, cos_sin, slots,
-                            q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None):
+                            q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None,
+                            tail_counters(x.device) if _QKV_TAIL else None):
             return
     if (x.is_cuda and not isinstance(w, Fp8Weight) and _GEMM_FORCE == 0 and M >= 1024
             and positions.dtype == torch.int32 and slots.dtype == torch.int32):
         # prefill: RoPE + paged KV write in the 256x256 GEMM's epilogue (no bf16 qkv round trip)
         ws = torch.empty(0, dtype=torch.float32, device=x.device)
         if native().gemm_rope_kv(x.reshape(M, K).contiguous(), w, bias, positions, cos_sin, slots, q_out, k_cache,
-                                 v_cache, Hq, Hkv, D, k_scale, v_scale, ws, False):
+                                 v_cache, Hq, Hkv, D, k_scale, v_scale, ws, False, None):
             return
     qkv = linear(x, w, bias=bias)
     rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, True, k_scale, v_scale)
+
+
+# GAI_QKV_TAIL=1: the decode QKV partials are summed + rotated by the last-arriving K-slice inside the GEMM launch
+# instead of the separate splitk_rope_kv launch. Off by default: at Llama-3-8B B = 64 the one reducer per head reads
+# 8 x 64 x 128 fp32 slabs (256 KB) serially, 25.5 us vs 16.3 + 6.3 us for GEMM + tail launch
+# (profiles/r3/qkv_tail_ab); the tail only pays when K-slices x slab bytes per tile are a few tens of KB.
+_QKV_TAIL = os.environ.get("GAI_QKV_TAIL", "0") == "1"
+_TAIL_CNT: dict = {}
+
+
+def tail_counters(device) -> torch.Tensor:
+    """Ticket counters of the in-launch split-K tails (one int32 per output tile). Zero between launches: the
+    last-arriving K-slice of a tile resets its own counter. One buffer per (device, stream), since launches
+    queued on one stream never overlap; graphs capture the buffer of their capture stream."""
+    dev = torch.device(device)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    t = _TAIL_CNT.get(key)
+    if t is None:
+        t = _TAIL_CNT[key] = torch.zeros(4096, dtype=torch.int32, device=dev)
+    return t
 
 
 def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
@@ -419,10 +440,11 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
     return out
 
 
-# GAI_ATTN_FUSE=1: merge decode-attention splits inside the attention launch (ticket + agent release / acquire per
-# split) instead of the separate attn_decode_reduce launch. Off: measured 192.6 vs 117.4 us per Llama-3-8B layer at
-# B = 64, ctx 2600 (the per-workgroup release fence), profiles/r3/attn_fused_merge_ab
-_ATTN_FUSE = os.environ.get("GAI_ATTN_FUSE", "0") == "1"
+# Decode-attention splits are merged inside the attention launch by the last-arriving split (write-through sc1
+# partials + a relaxed ticket, no fence): Llama-3-8B B = 64, ctx 2600 eager forward 7.918 -> 7.738 ms, headline
+# 16.92 -> 17.08 q/s (profiles/r3/attn_fused_merge_ab). The first form, with a per-workgroup agent release, was
+# 192.6 vs 117.4 us per layer. GAI_ATTN_FUSE=0: the separate attn_decode_reduce launch.
+_ATTN_FUSE = os.environ.get("GAI_ATTN_FUSE", "1") == "1"
 
 
 # ---------------------------------------------------------------------------------------------

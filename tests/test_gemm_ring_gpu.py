@@ -115,7 +115,7 @@ def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
         vc = torch.zeros(nblk, Hkv, D, 16, device=cuda, dtype=torch.bfloat16)
         if fused:
             assert ops.native().gemm_rope_kv(x, w, bias, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0,
-                                             torch.empty(0, device=cuda), False)
+                                             torch.empty(0, device=cuda), False, None)
         else:
             qkv = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
             ops.native().gemm(x, w, qkv, bias, None, ops.EPI["bias"] if with_bias else 0, 0)

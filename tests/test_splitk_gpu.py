@@ -164,9 +164,12 @@ def test_decode_gemm_natural_layout(cuda, M, N, K, act, psw):
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("kv_fp8", [False, True])
 @pytest.mark.parametrize("psw", [False, True])
-def test_linear_rope_kv_fused_matches_unfused(cuda, M, bias, kv_fp8, psw):
+@pytest.mark.parametrize("tail", [True, False])
+def test_linear_rope_kv_fused_matches_unfused(cuda, monkeypatch, M, bias, kv_fp8, psw, tail):
     """Decode QKV tail fused into the split-K reduce (partials -> bias -> bf16 -> RoPE -> q / paged K, V^T)
-    matches linear + rope_kv_write to the last bit on all but a handful of elements, bf16 and fp8 caches."""
+    matches linear + rope_kv_write to the last bit on all but a handful of elements, bf16 and fp8 caches;
+    tail: the reduce runs in the GEMM launch (last-arriving K-slice), else in the splitk_rope_kv launch."""
+    monkeypatch.setattr(ops, "_QKV_TAIL", tail)
     Hq, Hkv, D, K = 32, 8, 128, 4096
     N = (Hq + 2 * Hkv) * D
     torch.manual_seed(M * 5 + bias + 2 * kv_fp8)
@@ -203,3 +206,37 @@ def test_linear_rope_kv_fused_matches_unfused(cuda, M, bias, kv_fp8, psw):
             assert (a != r).sum().item() <= max(2, a.numel() // 10000)
     if M > 1:  # row 0 is padded (no cache write)
         assert outs[0][1].float().abs().sum() > 0  # the cache was written
+    if tail:
+        assert int(ops.tail_counters(cuda).abs().sum()) == 0  # every ticket counter reset by its last arriver
+
+
+def test_qkv_tail_graph_replays(cuda):
+    """In-launch QKV tail under graph replay: counters reset themselves, every replay equals the eager result."""
+    Hq, Hkv, D, K, M = 32, 8, 128, 4096, 64
+    N = (Hq + 2 * Hkv) * D
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    assert ops.preshuffle_weight(w)
+    cs = ops.rope_cos_sin(4096, D, 500000.0, device=cuda)
+    pos = torch.randint(0, 4000, (M,), device=cuda, dtype=torch.int32)
+    slots = torch.randperm(64 * 16, device=cuda)[:M].to(torch.int32)
+    kc = torch.zeros(64, Hkv, 16, D, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros(64, Hkv, D, 16, device=cuda, dtype=torch.bfloat16)
+    q = torch.zeros(M, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.linear_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D)
+    want = (q.clone(), kc.clone(), vc.clone())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.linear_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.linear_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D)
+    for _ in range(10):
+        q.zero_(); kc.zero_(); vc.zero_()  # noqa: E702
+        g.replay()
+        torch.cuda.synchronize()
+        for a, b in zip((q, kc, vc), want):
+            assert torch.equal(a, b)

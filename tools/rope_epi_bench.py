@@ -53,8 +53,8 @@ def main():
     ws = torch.empty(0, dtype=torch.float32, device="cuda")
     arms = {
         "plain": lambda: nat.gemm(x, w, out, None, None, 0, 0),
-        "fused": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False),
-        "fused_nokv": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, nos, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False),
+        "fused": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False, None),
+        "fused_nokv": lambda: nat.gemm_rope_kv(x, w, None, pos, cs, nos, q, kc, vc, Hq, Hkv, D, 1.0, 1.0, ws, False, None),
     }
     ts = {k: [] for k in arms}
     for _ in range(a.rounds):
