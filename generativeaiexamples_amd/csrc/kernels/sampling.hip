@@ -98,6 +98,30 @@ __device__ __forceinline__ void row_for_each(const float* x, int V, F&& f) {
   }
 }
 
+// Histogram add for the radix passes. Near the top of the distribution the keys share their high bytes, so in
+// the first passes most lanes of a wave hit one or two bins and plain LDS atomics serialise lane by lane (the
+// split resolve spent ~100 us per decode step in them at the headline's ~3K candidates per row). Up to 4 bins per
+// wave instruction are summed across the wave first (one atomic each); the rest add lane by lane. Every lane of
+// the wave must call it (uniform trip counts), valid or not.
+__device__ __forceinline__ void hist_add(float* hist, int bin, float w, bool valid) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long act = __ballot(valid);
+#pragma unroll 1
+  for (int it = 0; it < 4 && act; ++it) {
+    const int lead = __ffsll((long long)act) - 1;
+    const int lb = __shfl(bin, lead, 64);
+    const bool mine = valid && bin == lb;
+    if (__popcll(__ballot(mine)) < 8) break;  // spread bins (later passes): lane-by-lane atomics are cheaper
+    float v = mine ? w : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == lead) atomicAdd(&hist[lb], v);
+    act &= ~__ballot(mine);
+    valid = valid && !mine;
+  }
+  if (valid) atomicAdd(&hist[bin], w);
+}
+
 // Finds the largest key threshold K* with weight(key >= K*) >= target, where the weight of
 // element i is 1 (counting) or exp((x_i - mx) * invT) (mass), over elements with key >= floor_key.
 template <bool MASS>
@@ -111,6 +135,7 @@ __device__ uint32_t radix_select(const float* x, int V, float mx, float invT, ui
     for (int b = threadIdx.x; b < 256; b += kThreads) hist[b] = 0.f;
     __syncthreads();
     const uint32_t hi_mask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    // whole rows spread over many exponent bins already: plain lane atomics (hist_add measured slower here)
     for (int i = threadIdx.x; i < V; i += kThreads) {
       const float xv = x[i];
       const uint32_t k = fkey(xv);
@@ -178,7 +203,10 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
 // element outside the list has a smaller key. Gumbel-max then runs over the candidates only. Returns
 // false (the caller takes the full radix path) when more than kCap elements qualify or the candidates
 // hold less than p of the mass (flat distributions).
-constexpr int kCap = 4096;
+// LDS candidate capacity: the headline's random-init Llama-3 logits (~N(0, 1), T = 0.2) put 3-7K of 128K tokens within
+// kCut temperatures of the row max, which overflowed 4096 on most rows and sent them to the whole-row radix passes
+// (the split resolve at 131 us per decode step instead of ~25)
+constexpr int kCap = 16384;
 constexpr float kCut = 12.f;  // candidates: logits within 12 temperatures of the max (weight >= e^-12)
 
 __device__ bool nucleus_fast(const float* x, int V, float mx, float invT, float p, uint64_t seed, int64_t step,
@@ -362,8 +390,12 @@ __global__ __launch_bounds__(kThreads) void sample_kernel(const float* __restric
 // Same token as sample_kernel for a fixed (seed, step) up to float summation order at exact-cut ties.
 constexpr int kChunk = 8192;   // logits per split workgroup (32 per thread, 8 float4 registers)
 constexpr int kSplitT = 256;
-constexpr int kSlot = 1024;    // candidate slots per chunk (chunk-max relative: flat rows reach a few hundred)
+// candidate slots per chunk (compacted relative to the CHUNK max: the headline's random-init logits, ~N(0, 1) at
+// T = 0.2, put up to ~2.2K of a chunk's 8192 within kCut of it; 1024 slots overflowed and sent the row to the
+// whole-row fallback)
+constexpr int kSlot = 4096;
 constexpr int kSplitMinV = 16384;
+constexpr int kMaxSplits = 128;  // chunks per row the resolve kernel takes (V <= 1M); wider rows: whole-row kernel
 constexpr int kPartW = 8;      // words per (row, split) partial: max, sum, argmax, gval, gidx, count
 
 __device__ __forceinline__ int nsplit(int V) { return (V + kChunk - 1) / kChunk; }
@@ -503,11 +535,12 @@ __device__ uint32_t radix_select_cands(const uint64_t* cand, int n, float mx, fl
     for (int b = threadIdx.x; b < 256; b += kThreads) hist[b] = 0.f;
     __syncthreads();
     const uint32_t hi_mask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-    for (int j = threadIdx.x; j < n; j += kThreads) {
-      const uint32_t kk = (uint32_t)(cand[j] >> 32);
-      if (kk < floor_key || (kk & hi_mask) != prefix) continue;
-      const float w = MASS ? __expf((key_to_float(kk) - mx) * invT) : 1.f;
-      atomicAdd(&hist[(kk >> shift) & 255], w);
+    for (int j0 = 0; j0 < n; j0 += kThreads) {
+      const int j = j0 + threadIdx.x;
+      const uint32_t kk = j < n ? (uint32_t)(cand[j] >> 32) : 0u;
+      const bool ok = j < n && kk >= floor_key && (kk & hi_mask) == prefix;
+      const float w = MASS && ok ? __expf((key_to_float(kk) - mx) * invT) : 1.f;
+      hist_add(hist, (kk >> shift) & 255, w, ok);
     }
     __syncthreads();
     if (threadIdx.x < 64) {
@@ -565,12 +598,16 @@ __global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __
   __shared__ SampleSmem sm;
   __shared__ int cnt_sh;
   __shared__ int flag;
+  __shared__ float pr[kMaxSplits * kPartW];
   const int row = blockIdx.x, tid = threadIdx.x;
   const float T = temperature[row];
   const int k = top_k[row];
   const float p = top_p[row];
   const uint64_t seed = (uint64_t)seeds[row];
-  const float* pr = part + (size_t)row * S * kPartW;
+  // the row's partials land in LDS in one round of loads (runtime-trip loops over global memory below would each
+  // wait out a full load latency per chunk)
+  for (int e = tid; e < S * kPartW; e += kThreads) pr[e] = part[(size_t)row * S * kPartW + e];
+  __syncthreads();
   // row max / argmax from the partials (first index among equal maxima, as the whole-row kernel)
   ArgMax am{-INFINITY, 0x7fffffff};
   for (int j = 0; j < S; ++j) am = argmax_merge(am, ArgMax{pr[j * kPartW], __float_as_int(pr[j * kPartW + 2])});
@@ -587,31 +624,39 @@ __global__ __launch_bounds__(kThreads) void sample_split_resolve(const float* __
   }
   // candidate list: the chunks whose max lies within kCut of the row max contribute their candidates that do
   // too (nucleus_fast's set); such a chunk that overflowed its slots may have dropped one -> whole-row path
-  if (tid == 0) cnt_sh = 0, flag = S > 128;
+  if (tid == 0) cnt_sh = 0, flag = 0;
   __syncthreads();
-  for (int j = 0; j < S && !flag; ++j) {
-    const float mj = pr[j * kPartW];
-    if (!(mj > -INFINITY) || (M - mj) * invT >= kCut) continue;
-    const int c = __float_as_int(pr[j * kPartW + 5]);
-    if (c > kSlot) {
-      if (tid == 0) flag = 1;
-      break;
-    }
-    const uint64_t* src = cands + ((size_t)row * S + j) * kSlot;
-    for (int q0 = 0; q0 < c; q0 += kThreads) {
-      const int q = q0 + tid;
-      uint64_t e = 0;
-      bool keep = false;
-      if (q < c) {
-        e = src[q];
-        keep = (M - key_to_float((uint32_t)(e >> 32))) * invT < kCut;
+  if (tid < S) {  // a contributing chunk that overflowed its slots may have dropped a candidate
+    const float mj = pr[tid * kPartW];
+    if (mj > -INFINITY && (M - mj) * invT < kCut && __float_as_int(pr[tid * kPartW + 5]) > kSlot) flag = 1;
+  }
+  __syncthreads();
+  // every slot of every contributing chunk at once: kGather independent loads per thread in flight
+  constexpr int kGather = 4;
+  const uint64_t* src = cands + (size_t)row * S * kSlot;
+  for (int e0 = 0; e0 < S * kSlot && !flag; e0 += kGather * kThreads) {
+    uint64_t ev[kGather];
+    bool live[kGather];
+#pragma unroll
+    for (int u = 0; u < kGather; ++u) {
+      const int e = e0 + u * kThreads + tid;
+      const int j = e / kSlot, q = e % kSlot;
+      live[u] = false;
+      if (e < S * kSlot) {
+        const float mj = pr[j * kPartW];
+        live[u] = mj > -INFINITY && (M - mj) * invT < kCut && q < __float_as_int(pr[j * kPartW + 5]);
       }
+      ev[u] = live[u] ? src[e] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kGather; ++u) {
+      const bool keep = live[u] && (M - key_to_float((uint32_t)(ev[u] >> 32))) * invT < kCut;
       const unsigned long long msk = __ballot(keep);
       int base = 0;
       if ((tid & 63) == 0 && msk) base = atomicAdd(&cnt_sh, __popcll(msk));
       base = __shfl(base, 0, 64);
       const int pos = base + __popcll(msk & ((1ull << (tid & 63)) - 1ull));
-      if (keep && pos < kCap) sm.cand[pos] = e;
+      if (keep && pos < kCap) sm.cand[pos] = ev[u];
     }
   }
   __syncthreads();

@@ -16,7 +16,9 @@ def main():
     dev = "cuda"
     B, V = 64, 128256
     torch.manual_seed(0)
-    cases = [("greedy", 1.28, 0.0, 1.0), ("T0.2_p0.7", 1.28, 0.2, 0.7), ("T1_p0.9", 3.0, 1.0, 0.9),
+    # scale 1.0 / T 0.2 / p 0.7 = the headline bench (random-init lm_head std 1/sqrt(d): unit-variance logits)
+    cases = [("greedy", 1.28, 0.0, 1.0), ("T0.2_p0.7", 1.28, 0.2, 0.7), ("bench_T0.2_p0.7", 1.0, 0.2, 0.7),
+             ("T1_p0.9", 3.0, 1.0, 0.9),
              ("flat_T1_p0.9", 0.01, 1.0, 0.9), ("T0.7_p1", 1.28, 0.7, 1.0)]
     for name, scale, T, p in cases:
         logits = torch.randn(B, V, device=dev) * scale
