@@ -91,16 +91,27 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
-    float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale) {
+    float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale, int xcd) {
   using Cfg = PrefillCfg<D>;
   constexpr int RPW = 4 / HPW;  // row groups per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int seq = tiles[2 * blockIdx.x], qs = tiles[2 * blockIdx.x + 1];
+  // xcd: head group = linear workgroup id mod gridDim.y. Workgroups go to the 8 XCDs round-robin by linear id, so
+  // with 8 (or a multiple of 8) head groups every XCD serves one kv head (or two): the q tiles running together
+  // on it re-read that head's K/V prefixes from the XCD's own L2 instead of all heads' prefixes streaming through
+  // every XCD. MI355X (profiles/r3/attn_prefill_xcd): B 4 x S 2048 GQA 32/8 D 128 604 -> 660 TF/s, the headline
+  // chunk (7 x 2406) 703 -> 728, Gemma D 256 315 -> 473; 64 x 512 MHA D 64 413 -> 394. GAI_ATTN_XCD=0: off.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    bx = L / gridDim.y;
+    by = L % gridDim.y;
+  }
+  const int seq = tiles[2 * bx], qs = tiles[2 * bx + 1];
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int ctx = ctx_lens[seq];
-  const int head = blockIdx.y * HPW + (wid % HPW);
-  const int g = (blockIdx.y * HPW) / (Hq / Hkv);
+  const int head = by * HPW + (wid % HPW);
+  const int g = (by * HPW) / (Hq / Hkv);
   const int r0 = qs + 32 * (wid / HPW);  // first q row (within the sequence) of this wave
   const int qrow = r0 + (lane & 31);
   const int qpos = ctx - qlen + qrow;  // absolute position of this lane's query
@@ -612,6 +623,7 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   if (ntiles == 0) return;
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
+  static const int xcd = getenv("GAI_ATTN_XCD") ? atoi(getenv("GAI_ATTN_XCD")) : 1;  // A/B switch
 #define GAI_PF(DD, HP)                                                                                         \
   if (D == DD && hpw == HP) {                                                                                  \
     const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
@@ -620,13 +632,13 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
       set_max_lds(kern, lds);                                                                                  \
       kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,  \
                                                     block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale);            \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd);       \
     } else {                                                                                                   \
       auto kern = attn_prefill_kernel<DD, HP, bf16>;                                                           \
       set_max_lds(kern, lds);                                                                                  \
       kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, \
                                                     block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale);            \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd);       \
     }                                                                                                          \
     GAI_LAUNCH_CHECK();                                                                                        \
     return;                                                                                                    \

@@ -347,7 +347,8 @@ def prefill_tile_list(q_lens: Sequence[int], rows: int, ctx_lens: Sequence[int] 
     """Varlen tile list [(seq, q_start), ...] for attention_prefill, longest first: a causal tile's work
     grows with its last query position (ctx - qlen + q_start + rows keys), and workgroups are dispatched
     roughly in tile order, so issuing the long tiles first keeps them off the tail of the grid
-    (longest-processing-time-first scheduling)."""
+    (longest-processing-time-first scheduling). Grouping the tiles by sequence instead (for L2 reuse of a K/V
+    prefix on the kernel's per-XCD kv heads) measured 1-7 % slower (profiles/r3/attn_prefill_xcd)."""
     t = [(b, s) for b, n in enumerate(q_lens) for s in range(0, n, rows)]
     if ctx_lens is None:
         ctx_lens = q_lens

@@ -265,6 +265,7 @@ def main():
                          (1601 * 8, 4096, 1024, "clip-L mlp up b8"), (64, 28672, 4096, "gate_up decode b64")])
     if "prefill" in only:
         bench_prefill(rows, 4, 2048, 32, 8, 128)
+        bench_prefill(rows, 7, 2406, 32, 8, 128)  # one headline 16K prefill chunk: 7 RAG prompts of 2406 tokens
         bench_prefill(rows, 64, 512, 16, 16, 64)
         bench_prefill(rows, 4, 2048, 16, 16, 256)  # Gemma-7B attention shape
     if "decode_sweep" in only:
