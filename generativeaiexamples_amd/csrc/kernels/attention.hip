@@ -417,12 +417,23 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     Raw v8[H][V16 ? D / 16 : 1];
   };
   const int last_page = (kend - 1) / kBS;
-  auto load_chunk = [&](int kb, Chunk& c) {
+  // physical blocks of a chunk's pages (scalar loads). The non-pipelined loop looks the NEXT chunk's blocks up
+  // before issuing this chunk's K/V loads, so a K/V load never waits on a block-table round trip of its own.
+  struct Blk {
+    int b[H][2];
+  };
+  auto lookup = [&](int kb, Blk& o) {
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const int p0 = min(kb / kBS + 2 * h, last_page);
-      const int blk0 = bt[p0];
-      const int blk1 = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : blk0;
+      o.b[h][0] = bt[p0];
+      o.b[h][1] = (p0 + 1) * kBS < ctx ? bt[p0 + 1] : o.b[h][0];
+    }
+  };
+  auto load_chunk_blk = [&](int kb, const Blk& bl, Chunk& c) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int blk0 = bl.b[h][0], blk1 = bl.b[h][1];
       const size_t pb0 = ((size_t)blk0 * Hkv + g) * kBS * D, pb1 = ((size_t)blk1 * Hkv + g) * kBS * D;
       if (V16) {
         const int m = lane & 15;
@@ -452,6 +463,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         }
       }
     }
+  };
+  auto load_chunk = [&](int kb, Chunk& c) {
+    Blk bl;
+    lookup(kb, bl);
+    load_chunk_blk(kb, bl, c);
   };
   auto compute_chunk = [&](int kb, const Chunk& c) {
     f32x4 s[H][2];
@@ -526,10 +542,16 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         if (kb >= kend) break;
       }
     }
-  } else {
+  } else if (kb < kend) {
+    Blk nb;
+    lookup(kb, nb);
     for (; kb < kend; kb += kStep) {
       Chunk c;
-      load_chunk(kb, c);
+      load_chunk_blk(kb, nb, c);  // blocks looked up one chunk earlier
+      // the next chunk's blocks, issued after this chunk's K/V loads (SMEM returns out of order, so a wait for the
+      // blocks in use would also wait for these) and landing under this chunk's compute; pages past the split
+      // clamp to its last page (looked up, never loaded)
+      lookup(kb + kStep, nb);
       compute_chunk(kb, c);
     }
   }

@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_quant_rows_fp8_matches_reference(cuda):
+    torch.manual_seed(5)
     x = torch.randn(77, 1024, device="cuda", dtype=torch.bfloat16) * 3
     q, s = ops.quant_fp8(x)
     qr, sr = ref.quant_rows_fp8(x.cpu())
