@@ -435,7 +435,8 @@ def test_gemm_large_repeatable(cuda, M, N, K):
 def test_sample_split_path_matches_whole_row(cuda):
     """The split-row sampler (stats / candidate / resolve kernels, V >= 16K) must draw the whole-row
     kernel's token for the same (seed, step): greedy, pure temperature, top-k, top-p, top-k + top-p,
-    masked rows and flat rows (candidate overflow -> whole-row fallback inside the resolve kernel)."""
+    masked rows, rows with more candidates than the LDS list holds and flat rows (-> whole-row fallback inside
+    the resolve kernel)."""
     from generativeaiexamples_amd.ops import native
 
     torch.manual_seed(21)
@@ -444,14 +445,18 @@ def test_sample_split_path_matches_whole_row(cuda):
     logits[5:8] *= 0.01           # flat rows: > 4096 candidates
     logits[9, 1000:] = float("-inf")  # heavily masked row
     logits[10, 5] = 40.0          # one dominant token
+    logits[40:46] *= 3.0 / 1.28   # T = 1 on N(0, 3) rows: ~47K candidates, more than the LDS list holds
     temp = torch.full((B,), 0.2, device=cuda)
     temp[:4] = 0.0
     temp[20:28] = 0.9
+    temp[40:46] = 1.0
     top_p = torch.full((B,), 0.7, device=cuda)
     top_p[20:24] = 1.0            # pure temperature rows
+    top_p[40:46] = 0.9
     top_k = torch.zeros(B, dtype=torch.int32, device=cuda)
     top_k[24:28] = 50
     top_k[28:32] = 1
+    top_k[44:46] = 20000          # top-k cut beyond the candidate list, then top-p
     seeds = torch.arange(B, dtype=torch.int64, device=cuda) * 7 + 3
     nat = native()
     assert nat.sample_ws_bytes(B, V) > 0
