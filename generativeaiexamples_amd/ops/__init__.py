@@ -406,13 +406,15 @@ class DecodeWorkspace:
         return self.fixed_split or self.choose_split(self.max_ctx)
 
     @staticmethod
-    def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int = 1536) -> int:
+    def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int | None = None) -> int:
         """Split length (multiple of 128) giving ~target_wgs workgroups of (split, kv-head, sequence).
         The head_dim-128 kernel runs 3 workgroups per CU (VGPR-bound), i.e. 768 resident on 256 CUs,
         so 1536 = exactly two waves of workgroups. Measured on MI355X (B=64, 8 KV heads, ctx
         2.3-2.6k, profiles/r1/decode_attn_split_sweep_v2.jsonl): 896-key splits (1536 WGs) 5.34 TB/s vs
         768-key splits (2048 WGs = 2.67 waves, a 1/3-empty last wave) 5.04 TB/s; 256-key splits
         4.5 TB/s (per-workgroup prologue / combine not amortised)."""
+        if target_wgs is None:
+            target_wgs = _DECODE_TARGET_WGS
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128
@@ -422,6 +424,9 @@ class DecodeWorkspace:
         if self.fixed_split:
             return self.fixed_split
         return self.choose_split(max_ctx, batch, hkv)
+
+
+_DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1536"))  # sweeps only
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
