@@ -92,6 +92,12 @@ def parse():
     return ap.parse_args()
 
 
+def _sync():
+    """Device barrier of the timed region (a no-op on the CPU rehearsal path: gloo ranks, tiny models)."""
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
@@ -133,7 +139,7 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
     for i in range(args.probe_c1):
         qid = base + i
         planted = plant([qid], [synthetic_question(qid)])
-        torch.cuda.synchronize()
+        _sync()
         t0 = time.perf_counter()
         req = retrieve([qid])[0]
         while engine.has_work():
@@ -153,7 +159,7 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
         arrivals.append(t)
     qids = [base + 500 + i for i in range(n)]
     planted = plant(qids, [synthetic_question(q) for q in qids])
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     reqs, nxt = [], 0
     while nxt < n or engine.has_work():
@@ -314,10 +320,10 @@ def main():
         questions = [synthetic.question(q) for q in qids]
         planted = plant(qids, questions)
         ctx.barrier()
-        torch.cuda.synchronize()
+        _sync()
         t0 = time.perf_counter()
         emb = embedder.embed(questions, input_type="query")
-        torch.cuda.synchronize()
+        _sync()
         t_e = time.perf_counter()
         rel, rows = sharded.search_raw(emb, args.top_k)
         rows = rows.cpu().tolist()
@@ -329,7 +335,7 @@ def main():
         t_retrieved = time.perf_counter()
         while engine.has_work():
             engine.step()
-        torch.cuda.synchronize()
+        _sync()
         ctx.barrier()
         t1 = time.perf_counter()
         t_first = max(r.first_token_time for r in reqs)  # every prompt prefilled (its first token sampled)
