@@ -17,7 +17,9 @@ __device__ __forceinline__ void store_out(void* C, const bf16* bias, const bf16*
   if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
   if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
   if (EPI == EPI_BIAS_QUICKGELU) v = quick_gelu(v);
-  if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) v += (float)R[(size_t)m * ldc + n];
+  // residual with bf16 output = the unfused pair: bf16 projection output, then the add rounded again (the rounding of
+  // the decode add+RMSNorm tails and of norm_kernel's residual add, so a fused prefill residual is bitwise theirs)
+  if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) v = (OUTF32 ? v : (float)(bf16)v) + (float)R[(size_t)m * ldc + n];
   if (OUTF32)
     reinterpret_cast<float*>(C)[(size_t)m * ldc + n] = v;
   else

@@ -447,10 +447,10 @@ __device__ __forceinline__ void epilogue_rows(const f32x4 (&acc_i)[NJ], void* C,
         v[r] = x0[r];
         v[4 + r] = x1[r];
       }
-      if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) {
+      if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) {  // bf16(bf16(acc) + R): gai_epilogue.h store_out
         const bf16x8 rv = load8(R + (size_t)m * ldc + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+        for (int e = 0; e < 8; ++e) v[e] = (float)(bf16)v[e] + (float)rv[e];
       }
       bf16x8 o;
 #pragma unroll

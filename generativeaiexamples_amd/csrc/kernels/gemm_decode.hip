@@ -238,10 +238,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
         for (int q = 0; q < KQ; ++q) t += red[(q * ROWS + m) * RS + c0 + x];
         v[x] = dec_act<EPI>(t, bias, n + x);
       }
-      if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) {
+      if (EPI == EPI_RESIDUAL || EPI == EPI_BIAS_RESIDUAL) {  // bf16 output: bf16(bf16(acc) + R) (store_out)
         const bf16x8 rv = load8(R + (size_t)m * ldc + n);
 #pragma unroll
-        for (int x = 0; x < 8; ++x) v[x] += (float)rv[x];
+        for (int x = 0; x < 8; ++x) v[x] = (OUTF32 ? v[x] : (float)(bf16)v[x]) + (float)rv[x];
       }
       dec_store8<OUTF32>(C, (size_t)m * ldc + n, v);
     }

@@ -377,17 +377,18 @@ __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restr
   }
   amax = block_max(amax, red);
   const float s = fmaxf(amax, 1e-12f) / kFp8Max;
+  // x * (1 / s), one multiply per element (ops.reference.quant_rows_fp8 does the same) instead of an IEEE x / s
+  // (~10 VALU per element) on every prefill activation
+  const float inv = 1.f / s;
   if (threadIdx.x == 0) scale[row] = s;
   uint8_t* qr = q + (size_t)row * K;
-  // x / s (IEEE division, as the fp32 reference), not x * (1 / s): the reciprocal's extra rounding moved ~0.1 %
-  // of the codes across a rounding boundary; the kernel is memory-bound, the division is free
   for (int c = threadIdx.x * 8; c < K; c += 256 * 8) {
     const bf16x8 v = load8(xr + c);
     int w0 = 0, w1 = 0;
-    w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] / s, (float)v[1] / s, w0, false);
-    w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] / s, (float)v[3] / s, w0, true);
-    w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] / s, (float)v[5] / s, w1, false);
-    w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] / s, (float)v[7] / s, w1, true);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] * inv, (float)v[1] * inv, w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] * inv, (float)v[3] * inv, w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] * inv, (float)v[5] * inv, w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * inv, (float)v[7] * inv, w1, true);
     *reinterpret_cast<int2*>(qr + c) = make_int2(w0, w1);
   }
 }

@@ -345,7 +345,8 @@ def quant_rows_fp8(x: torch.Tensor):
     """Per-row dynamic e4m3fn quantisation: (q [.., K] float8_e4m3fn, scale [rows] fp32 = amax/448)."""
     xf = x.float().reshape(-1, x.shape[-1])
     s = xf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX
-    q = (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    # x * (1 / s) in fp32, as the kernel (a reciprocal multiply, not a division per element)
+    q = (xf * (1.0 / s)[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
     return q.reshape(x.shape), s
 
 

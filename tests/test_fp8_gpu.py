@@ -16,9 +16,9 @@ def test_quant_rows_fp8_matches_reference(cuda):
     q, s = ops.quant_fp8(x)
     qr, sr = ref.quant_rows_fp8(x.cpu())
     torch.testing.assert_close(s.cpu(), sr, rtol=1e-6, atol=0)
-    # same RNE rounding: allow a handful of ties to differ by one ulp
+    # same reciprocal multiply and RNE rounding: at most a handful of codes one ulp apart
     diff = (q.cpu().float() - qr.float()).abs()
-    assert (diff > 0).float().mean() < 1e-3
+    assert (diff > 0).float().mean() < 1e-4
     rel = diff / qr.float().abs().clamp_min(1e-3)
     assert rel.max() <= 0.13
 
