@@ -645,10 +645,12 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   if (ntiles == 0) return;
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
-  // XCD kv-head placement for head_dim >= 128 (decoder prefill, long prefixes); the head_dim-64 encoders (e5, CLIP
-  // ViT, short sequences) ran 413 -> 394 TF/s with it (profiles/r3/attn_prefill_xcd). GAI_ATTN_XCD=0 / 2: off / on.
+  // XCD kv-head placement for causal decoder prefill at head_dim >= 128 (long K/V prefixes re-read by many q tiles).
+  // Off for the head_dim-64 encoders (413 -> 394 TF/s with it) and for non-causal attention: config 4 (Mllama
+  // cross-attention over the vision tokens) ran 6.69 -> 6.52 q/s with it (profiles/r3/attn_prefill_xcd).
+  // GAI_ATTN_XCD=0 / 2: off / on everywhere.
   static const int xcd_env = getenv("GAI_ATTN_XCD") ? atoi(getenv("GAI_ATTN_XCD")) : 1;
-  const int xcd = xcd_env == 2 || (xcd_env == 1 && D >= 128);
+  const int xcd = xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal);
 #define GAI_PF(DD, HP)                                                                                         \
   if (D == DD && hpw == HP) {                                                                                  \
     const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
