@@ -23,6 +23,7 @@
 #include "gai_kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 using namespace gai;
 
@@ -83,11 +84,26 @@ __device__ __forceinline__ void dec_store8(void* C, size_t off, const float (&v)
 // PSW: W is the fragment-shuffled copy [N/16][K/32][64 lanes][8] (ops.shuffle_fragments): a wave's k32 step
 // is ONE contiguous KiB (8 full 128-B lines) instead of 16 half lines, loaded non-temporally (read once;
 // profiles/r2/dec_stream_microbench.jsonl: 5.8-6.5 TB/s shuffled + nt vs 5.0-5.4 on the natural layout).
+// MoE (moe_offs != nullptr): blockIdx.z = expert e of W [E, N, K]; its rows are moe_offs[e] .. moe_offs[e + 1] of the
+// expert-sorted order (<= 16 MB of them, host-checked), gathered from A through moe_rows when given, and written to
+// C rows moe_offs[e] + m: the grouped expert GEMM of a decode step as a weight stream (moe.hip routes it here).
 template <int MB, int NT, int EPI, bool OUTF32, bool PART = false, bool PSW = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                                 void* C, const bf16* __restrict__ bias, const bf16* R,
-                                                                int M, int N, int K, int ldc, float* __restrict__ part) {
+                                                                int M, int N, int K, int ldc, float* __restrict__ part,
+                                                                const int* __restrict__ moe_rows,
+                                                                const int* __restrict__ moe_offs) {
   constexpr int KQ = 8 / NT;
+  int row0 = 0;
+  if (moe_offs != nullptr) {  // wave-uniform: the whole workgroup leaves before any barrier when the expert is idle
+    const int e = blockIdx.z;
+    row0 = moe_offs[e];
+    M = moe_offs[e + 1] - row0;
+    if (M <= 0) return;
+    W += (size_t)e * N * K;
+    if constexpr (OUTF32) C = reinterpret_cast<float*>(C) + (size_t)row0 * ldc;
+    else C = reinterpret_cast<bf16*>(C) + (size_t)row0 * ldc;
+  }
   using Cf = DecCfg<MB, KQ>;
   constexpr int ROWS = Cf::ROWS, SPS = Cf::SPS, RB = Cf::RB, CPR = Cf::CPR, L = Cf::L, BKS = Cf::BKS;
   constexpr int BN = 16 * NT;
@@ -120,7 +136,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_dec2_kernel(const bf16* __re
   for (int j = 0; j < 4; ++j) {
     const int p = (wid * 4 + j) * 64 + lane;
     const int strip = p / (ROWS * CPR), rem = p % (ROWS * CPR), r = rem / CPR, c = rem % CPR;
-    asrc[j] = A + (size_t)min(r, M - 1) * K + kbase + (size_t)strip * KW + 8 * c;
+    const int rr = min(r, M - 1);
+    const int src = moe_offs == nullptr ? rr : moe_rows != nullptr ? moe_rows[row0 + rr] : row0 + rr;
+    asrc[j] = A + (size_t)src * K + kbase + (size_t)strip * KW + 8 * c;
     adst[j] = strip * ROWS * RB + r * RB + 16 * (c ^ dec_swz<MB, KQ>(r));
   }
   bf16x8 ast[2][4];
@@ -253,7 +271,8 @@ constexpr int dec2_steps_multiple() { return DecCfg<MB, 8 / NT>::L; }
 
 template <int MB, int NT, int EPI, bool OUTF32, bool PART = false, bool PSW = false>
 void dec2_launch(const void* A, const void* W, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                 hipStream_t st, int KS = 1, float* part = nullptr) {
+                 hipStream_t st, int KS = 1, float* part = nullptr, const int* moe_rows = nullptr,
+                 const int* moe_offs = nullptr, int E = 1) {
   auto kern = gemm_dec2_kernel<MB, NT, EPI, OUTF32, PART, PSW>;
   constexpr int lds = 2 * kStage;
   static bool once = false;
@@ -262,8 +281,8 @@ void dec2_launch(const void* A, const void* W, void* C, const void* bias, const 
     once = true;
   }
   const int blocks = (N + 16 * NT - 1) / (16 * NT);
-  kern<<<dim3(blocks, KS), kThreads, lds, st>>>((const bf16*)A, (const bf16*)W, C, (const bf16*)bias, (const bf16*)R,
-                                                M, N, K, ldc, part);
+  kern<<<dim3(blocks, KS, E), kThreads, lds, st>>>((const bf16*)A, (const bf16*)W, C, (const bf16*)bias,
+                                                   (const bf16*)R, M, N, K, ldc, part, moe_rows, moe_offs);
   GAI_LAUNCH_CHECK();
 }
 
@@ -434,4 +453,44 @@ int dec2_part_dispatch(const void* A, const void* W, int M, int N, int K, float*
 int gai_gemm_dec2_partials_ks(int M, int N, int K) { return dec2_part_dispatch(nullptr, nullptr, M, N, K, nullptr, 0, false); }
 int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, int psw) {
   return dec2_part_dispatch(A, W, M, N, K, ws, st, true, psw != 0);
+}
+
+// Decode-sized grouped expert GEMM (moe.hip: rows_total <= 64, so no expert holds more than 64 rows): one weight
+// stream per (expert, column tile) on the LDS-staged decode kernel, instead of 128 x 128 tiles that stage 128 A rows
+// for a handful of live ones and keep one 32 KB stage in flight per CU. swiglu: W rows interleaved per 16
+// [gate16 | up16] (ops.interleave_gate_up), C = silu(gate) * up. Returns 0 when the shape does not fit.
+int gai_moe_gemm_dec2(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E,
+                      int rows_total, int N, int K, int swiglu, hipStream_t st) {
+  if (rows_total < 1 || rows_total > 64 || N % 32) return 0;
+  const int ldc = swiglu ? N / 2 : N;
+  const int epi = swiglu ? EPI_SWIGLU : EPI_NONE;
+#define GAI_MOE(MBV)                                                                                             \
+  {                                                                                                              \
+    const int NT = dec2_pick_nt<MBV>(N, K, swiglu != 0);                                                          \
+    if (NT == 0 || (swiglu && NT < 2)) return 0;                                                                  \
+    auto go = [&](auto ntc) {                                                                                     \
+      constexpr int NTV = decltype(ntc)::value;                                                                   \
+      if (epi == EPI_SWIGLU) {                                                                                    \
+        if constexpr (NTV >= 2)                                                                                   \
+          dec2_launch<MBV, NTV, EPI_SWIGLU, false>(A, W, C, nullptr, nullptr, rows_total, N, K, ldc, st, 1,       \
+                                                   nullptr, a_rows, offs, E);                                     \
+      } else {                                                                                                    \
+        dec2_launch<MBV, NTV, EPI_NONE, false>(A, W, C, nullptr, nullptr, rows_total, N, K, ldc, st, 1, nullptr,  \
+                                               a_rows, offs, E);                                                  \
+      }                                                                                                           \
+    };                                                                                                            \
+    switch (NT) {                                                                                                 \
+      case 8: go(std::integral_constant<int, 8>{}); return 1;                                                     \
+      case 4: go(std::integral_constant<int, 4>{}); return 1;                                                     \
+      case 2: go(std::integral_constant<int, 2>{}); return 1;                                                     \
+      case 1: if (!swiglu) { go(std::integral_constant<int, 1>{}); return 1; } return 0;                          \
+      default: return 0;                                                                                          \
+    }                                                                                                             \
+  }
+  static const bool off = getenv("GAI_MOE_DEC2") && atoi(getenv("GAI_MOE_DEC2")) == 0;
+  if (off) return 0;
+  if (rows_total <= 16) GAI_MOE(1)
+  if (rows_total <= 32) GAI_MOE(2)
+  GAI_MOE(4)
+#undef GAI_MOE
 }

@@ -207,9 +207,15 @@ void gai_moe_route(const float* logits, int T, int E, int k, int renorm, int* id
   GAI_LAUNCH_CHECK();
 }
 
+// gemm_decode.hip: decode-sized grouped GEMM on the weight-streaming decode kernel (0 = shape not handled)
+int gai_moe_gemm_dec2(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E,
+                      int rows_total, int N, int K, int swiglu, hipStream_t st);
+
 void gai_moe_gemm(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E, int rows_total,
                   int N, int K, int swiglu, hipStream_t st) {
   if (rows_total == 0) return;
+  // decode steps (<= 64 expert rows in all): every expert's weights streamed once by the decode kernel
+  if (gai_moe_gemm_dec2(A, a_rows, W, C, offs, E, rows_total, N, K, swiglu, st)) return;
   if (K % MBK) gai_launch_error(__FILE__, __LINE__, "moe_gemm: K must be a multiple of 64");
   const dim3 grid((rows_total + MBM - 1) / MBM + E, (N + MBN - 1) / MBN);
   const int lds = 4 * kMTile;

@@ -25,7 +25,10 @@ def test_moe_route(cuda):
     _close(w, w_r, 1e-5, 1e-5, "route weights")
 
 
-@pytest.mark.parametrize("T,E,k,D,I", [(1, 8, 2, 256, 512), (37, 8, 2, 512, 256), (700, 4, 2, 1024, 1024)])
+# (2, 8, 2, 4096, 1024) / (32, 8, 2, 4096, 4096): decode-sized steps (<= 64 expert rows) on the weight-streaming
+# decode kernel, idle experts included; the others on the 128 x 128 grouped kernel
+@pytest.mark.parametrize("T,E,k,D,I", [(1, 8, 2, 256, 512), (37, 8, 2, 512, 256), (700, 4, 2, 1024, 1024),
+                                       (2, 8, 2, 4096, 1024), (32, 8, 2, 4096, 4096)])
 def test_moe_gemm_and_combine(cuda, T, E, k, D, I):
     torch.manual_seed(T)
     x = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
