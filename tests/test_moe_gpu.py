@@ -112,3 +112,36 @@ def test_ep_padded_step_graph_capture(cuda, monkeypatch):
     dense = ops.moe_combine(ops.moe_gemm(ops.moe_gemm(x, a_rows, w13, offs, T * k, True), None, w2, offs, T * k,
                                          False), pos, wts)
     _close(out, dense, 2e-2, 2e-2, "padded EP vs local MoE")
+
+
+def test_mixtral_dense_prefill_matches_grouped(cuda, monkeypatch):
+    """Prefill-sized MoE steps run every expert on the dense GEMMs (host-read expert row ranges); the same layer
+    on the grouped kernel and the fp32 reference agree within bf16 tolerance."""
+    from generativeaiexamples_amd.models import mixtral as mx
+
+    cfg = mx.MixtralConfig.tiny_moe(hidden_size=1024, intermediate_size=2048, num_experts=8)
+    m = mx.MixtralModel(cfg, device=cuda).random_init(3)
+    torch.manual_seed(4)
+    x = torch.randn(1500, cfg.hidden_size, device=cuda, dtype=torch.bfloat16)
+    res = torch.randn_like(x)
+    outs = {}
+    for rows in (1, 1 << 30):  # dense prefill path / grouped kernel
+        monkeypatch.setattr(mx, "_DENSE_PREFILL_MIN_ROWS", rows)
+        outs[rows] = m.moe_mlp(x, 0, res.clone())
+    _close(outs[1], outs[1 << 30], 2e-2, 2e-2, "dense vs grouped MoE")
+    w, p = m.w, "l0."
+    ids, wts = ops.moe_route(ops.linear(x, w[p + "router"], out_dtype=torch.float32), cfg.top_k)  # the layer's routing
+    ids, wts = ids.cpu(), wts.cpu()
+    want = res.float().cpu().clone()
+    xf = x.float().cpu()
+    w13 = w[p + "w13"].float().cpu().view(cfg.num_experts, -1, 2, 16, cfg.hidden_size)
+    w2 = w[p + "w2"].float().cpu()
+    for j in range(cfg.top_k):
+        for e in range(cfg.num_experts):
+            sel = ids[:, j] == e
+            if sel.any():
+                gu = w13[e].reshape(-1, 2, 16, cfg.hidden_size)
+                g = xf[sel] @ gu[:, 0].reshape(-1, cfg.hidden_size).t()
+                u = xf[sel] @ gu[:, 1].reshape(-1, cfg.hidden_size).t()
+                want[sel] += wts[sel, j:j + 1] * ((torch.nn.functional.silu(g) * u) @ w2[e].t())
+    _close(outs[1], want, 3e-2, 3e-2, "dense MoE vs fp32")
