@@ -218,14 +218,19 @@ def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
     return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
 
 
+def psw_qualifies(w) -> bool:
+    """A bf16 [N, K] CUDA weight the fragment-shuffled decode layout takes (N % 16 == 0, K % 512 == 0, N >= 64)."""
+    if not (isinstance(w, torch.Tensor) and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return False
+    N, K = w.shape
+    return not (N % 16 or K % 512 or N < 64)
+
+
 def preshuffle_weight(w: torch.Tensor) -> bool:
     """Attach a fragment-shuffled copy of a bf16 weight for the decode GEMM (M <= 64). Costs one extra
     copy of the weight in HBM (16 GB for Llama-3-8B: 288 GB per MI355X buys decode bandwidth).
-    Returns False when the shape does not qualify (N % 16, K % 512)."""
-    if not (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2):
-        return False
-    N, K = w.shape
-    if N % 16 or K % 512 or N < 64:
+    Returns False when the shape does not qualify (psw_qualifies)."""
+    if not psw_qualifies(w):
         return False
     w._gai_psw = shuffle_fragments(w)
     return True

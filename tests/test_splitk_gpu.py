@@ -106,6 +106,24 @@ def test_engine_preshuffles_projections(cuda):
     assert getattr(m.w["l0.attn_norm"], "_gai_psw", None) is None
 
 
+def test_preshuffle_budget_takes_whole_kinds_by_priority(cuda):
+    """A budget that holds gate_up + down but nothing else copies exactly those kinds (every layer)."""
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+
+    m = LlamaModel(LlamaConfig.tiny(hidden_size=512, intermediate_size=1024, num_heads=8), device=cuda).random_init(0)
+    size = lambda kind: sum(v.numel() * v.element_size() for k, v in m.w.items()  # noqa: E731
+                            if k.rsplit(".", 1)[-1] == kind)
+    for kind in ("gate_up", "down", "o"):
+        assert all(ops.psw_qualifies(v) for k, v in m.w.items() if k.rsplit(".", 1)[-1] == kind), kind
+    budget = size("gate_up") + size("down") + 1  # nothing after them fits
+    assert m.preshuffle_decode_weights(budget_bytes=budget) == size("gate_up") + size("down")
+    for i in range(m.cfg.num_layers):
+        assert getattr(m.w[f"l{i}.gate_up"], "_gai_psw", None) is not None
+        assert getattr(m.w[f"l{i}.down"], "_gai_psw", None) is not None
+        assert getattr(m.w[f"l{i}.qkv"], "_gai_psw", None) is None and getattr(m.w[f"l{i}.o"], "_gai_psw", None) is None
+    assert getattr(m.w["lm_head"], "_gai_psw", None) is None
+
+
 @pytest.mark.parametrize("M", [1, 17, 64])
 @pytest.mark.parametrize("K", [4096, 14336])
 @pytest.mark.parametrize("bias", [False, True])
