@@ -252,12 +252,13 @@ class LlamaModel:
         kinds: dict = {}
         for k, v in self.w.items():
             kind = k.rsplit(".", 1)[-1]
-            if kind in self.DECODE_PROJECTIONS and isinstance(v, torch.Tensor) and getattr(v, "_gai_psw", None) is None:
+            done = v.dec is not None if isinstance(v, ops.Fp8Weight) else getattr(v, "_gai_psw", None) is not None
+            if kind in self.DECODE_PROJECTIONS and isinstance(v, (torch.Tensor, ops.Fp8Weight)) and not done:
                 kinds.setdefault(kind, {})[id(v)] = v  # tied weights count once
         added, left = 0, budget_bytes
         for kind in self.PSW_PRIORITY:
             ws = [v for v in kinds.get(kind, {}).values() if ops.psw_qualifies(v)]
-            need = sum(v.numel() * v.element_size() for v in ws)
+            need = sum(ops.psw_bytes(v) for v in ws)
             if not ws or (left is not None and need > left):
                 continue
             for v in ws:

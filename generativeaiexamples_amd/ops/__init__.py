@@ -219,21 +219,55 @@ def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
 
 
 def psw_qualifies(w) -> bool:
-    """A bf16 [N, K] CUDA weight the fragment-shuffled decode layout takes (N % 16 == 0, K % 512 == 0, N >= 64)."""
+    """A bf16 [N, K] CUDA weight (or an fp8 one, whose decode copy is bf16) the fragment-shuffled decode layout
+    takes (N % 16 == 0, K % 512 == 0, N >= 64)."""
+    if isinstance(w, Fp8Weight):
+        return w.q.is_cuda and w.q.dim() == 2 and not (w.q.shape[0] % 16 or w.q.shape[1] % 512 or w.q.shape[0] < 64)
     if not (isinstance(w, torch.Tensor) and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2):
         return False
     N, K = w.shape
     return not (N % 16 or K % 512 or N < 64)
 
 
-def preshuffle_weight(w: torch.Tensor) -> bool:
+def psw_bytes(w) -> int:
+    """HBM the decode copy of w takes (bf16 for fp8 weights too)."""
+    return w.numel() * 2
+
+
+def preshuffle_weight(w) -> bool:
     """Attach a fragment-shuffled copy of a bf16 weight for the decode GEMM (M <= 64). Costs one extra
-    copy of the weight in HBM (16 GB for Llama-3-8B: 288 GB per MI355X buys decode bandwidth).
-    Returns False when the shape does not qualify (psw_qualifies)."""
+    copy of the weight in HBM (16 GB for Llama-3-8B: 288 GB per MI355X buys decode bandwidth). An Fp8Weight gets
+    its dequantised values in that layout (Fp8Weight.dec). Returns False when the shape does not qualify
+    (psw_qualifies)."""
     if not psw_qualifies(w):
         return False
+    if isinstance(w, Fp8Weight):
+        w.dec = shuffle_fragments(w.dequantize(torch.bfloat16))
+        return True
     w._gai_psw = shuffle_fragments(w)
     return True
+
+
+def _decode_psw_linear(x, psw, bias, residual, act, out_dtype, out):
+    """Decode GEMM (M <= 64) from a fragment-ordered bf16 weight copy, with linear()'s epilogues."""
+    K = x.shape[-1]
+    M, N = x.numel() // K, psw.shape[0]
+    if act == "swiglu":
+        epi, ncol = EPI["swiglu"], N // 2
+    elif act in ("gelu", "relu", "quick_gelu"):
+        epi, ncol = EPI[act], N
+    elif residual is not None:
+        epi, ncol = (EPI["bias_residual"] if bias is not None else EPI["residual"]), N
+    else:
+        epi, ncol = (EPI["bias"] if bias is not None else 0), N
+    if out is None:
+        out = torch.empty(*x.shape[:-1], ncol, dtype=out_dtype or x.dtype, device=x.device)
+    if M == 0:
+        return out
+    nat = native()
+    ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x.device)
+    nat.gemm_splitk(x.reshape(M, K).contiguous(), psw, out, bias, residual, epi, ws, True)
+    return out
 
 
 def _native_gemm(x2, w, out, bias, residual, epi):
@@ -252,12 +286,14 @@ _FP8_FORCE = int(os.environ.get("GAI_FP8_FORCE", "0"))  # 0 auto, 2 tiled, 3 lar
 
 
 class Fp8Weight:
-    """Per-output-channel OCP e4m3fn weight, quantised once at load time, plus its fp32 scales [N]."""
+    """Per-output-channel OCP e4m3fn weight, quantised once at load time, plus its fp32 scales [N]. ``dec``:
+    optional decode copy (the dequantised bf16 values in MFMA fragment order, preshuffle_weight) that decode-sized
+    GEMMs stream instead of running the 128x128 fp8 tile kernel on a few rows."""
 
-    __slots__ = ("q", "scale")
+    __slots__ = ("q", "scale", "dec")
 
     def __init__(self, q: torch.Tensor, scale: torch.Tensor):
-        self.q, self.scale = q, scale
+        self.q, self.scale, self.dec = q, scale, None
 
     @classmethod
     def quantize(cls, w: torch.Tensor) -> "Fp8Weight":
@@ -303,6 +339,10 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, bias=None, residual=None, act=None
     out_dtype = out_dtype or x.dtype
     K = x.shape[-1]
     M = x.numel() // K
+    if w.dec is not None and x.is_cuda and M <= 64 and act in (None, "swiglu", "gelu", "relu", "quick_gelu"):
+        # decode: stream the fragment-ordered bf16 copy of the fp8 values (the 128x128 fp8 tile kernel ran the
+        # Llama-3.2-11B decode projections at ~0.4 TB/s on <= 32 rows); bf16 activations, fp32 accumulation
+        return _decode_psw_linear(x, w.dec, bias, residual, act, out_dtype, out)
     xq, sx = quant_fp8(x)
     if not x.is_cuda:
         return _into(out, ref.linear_fp8(xq, sx, w.q, w.scale, bias, residual, act, out_dtype))

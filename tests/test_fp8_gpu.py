@@ -90,3 +90,23 @@ def test_gemm_fp8_large_exact_integers(cuda):
     ops.native().gemm_fp8(a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn), torch.ones(M, device="cuda"),
                           torch.ones(N, device="cuda"), out, None, None, 0, 3)
     torch.testing.assert_close(out, a @ b.t(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M", [1, 32, 64])
+@pytest.mark.parametrize("act", [None, "swiglu"])
+def test_fp8_weight_decode_copy(cuda, M, act):
+    """Decode-sized GEMMs of an fp8 weight stream its dequantised bf16 copy in fragment order (Fp8Weight.dec):
+    equal to the fp32 GEMM on the dequantised weight; wider rows keep the fp8 MFMA path."""
+    torch.manual_seed(M)
+    N, K = 4096, 4096
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    W = ops.Fp8Weight.quantize(w)
+    assert ops.preshuffle_weight(W) and W.dec is not None and W.dec.dtype == torch.bfloat16
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    got = ops.linear(x, W, act=act).float()
+    want = ref.linear(x.float().cpu(), W.dequantize(torch.float32).cpu(), act=act).float()
+    torch.testing.assert_close(got.cpu(), want, rtol=2e-2, atol=2e-2)
+    xl = torch.randn(200, K, device=cuda, dtype=torch.bfloat16)  # prefill-sized: fp8 operands as before
+    got_l = ops.linear(xl, W, act=act).float().cpu()
+    want_l = ref.linear(xl.float().cpu(), W.dequantize(torch.float32).cpu(), act=act).float()
+    assert (got_l - want_l).abs().max() <= 0.1 * want_l.abs().max() + 0.05
