@@ -155,14 +155,20 @@ def parse_tool_calls(text: str, tools: List[Dict[str, Any]]) -> Optional[List[Di
     m = _JSON_OBJ.search(cand)
     if not m:
         return None
-    calls = []
-    blobs = [m.group(0)]
-    if ";" in cand:  # several calls separated by ';'
-        blobs = [b for b in cand.split(";") if b.strip()]
-    for b in blobs:
+    # one JSON object, or several separated by ';' (Llama 3.1 style): decoded one after another, so a ';' inside
+    # an argument string is data, not a separator
+    objs, dec, i = [], json.JSONDecoder(), m.start()
+    while i < len(cand) and cand[i] == "{":  # text after the last call is ignored
         try:
-            o = json.loads(b.strip())
+            o, i = dec.raw_decode(cand, i)
         except json.JSONDecodeError:
+            return None
+        objs.append(o)
+        while i < len(cand) and (cand[i].isspace() or cand[i] == ";"):
+            i += 1
+    calls = []
+    for o in objs:
+        if not isinstance(o, dict):
             return None
         name = o.get("name")
         args = o.get("parameters", o.get("arguments", {}))

@@ -169,3 +169,15 @@ def test_structured_output_budget_too_small_is_rejected(client):
         "max_tokens": 3, "messages": [{"role": "user", "content": "q"}],
         "response_format": {"type": "json_schema", "json_schema": {"name": "Answer", "schema": SCHEMA}}})
     assert r.status_code == 400 and "max_tokens" in r.text
+
+
+def test_parse_tool_calls_semicolons_inside_arguments():
+    """';' separates Llama-3.1-style calls only between objects: inside an argument string it is data."""
+    from generativeaiexamples_amd.serving.openai_api import parse_tool_calls
+
+    tools = [{"type": "function", "function": {"name": "search"}}, {"type": "function", "function": {"name": "calc"}}]
+    one = parse_tool_calls('{"name": "search", "parameters": {"query": "a;b; c"}}', tools)
+    assert len(one) == 1 and json.loads(one[0]["function"]["arguments"]) == {"query": "a;b; c"}
+    two = parse_tool_calls('{"name": "search", "parameters": {"query": "x;y"}}; {"name": "calc", "parameters": {}}', tools)
+    assert [c["function"]["name"] for c in two] == ["search", "calc"]
+    assert parse_tool_calls('{"name": "nope", "parameters": {}}', tools) is None
