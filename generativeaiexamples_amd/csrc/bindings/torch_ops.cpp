@@ -133,6 +133,17 @@ bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias
                                  (float)v_scale, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream(), K, cnt) != 0;
 }
 
+// The epilogue reads bias / residual through raw pointers: an epilogue code whose operand is missing
+// would read address 0 on the device, so refuse it on the host.
+static void check_epi_operands(int64_t epi, const optional<Tensor>& bias, const optional<Tensor>& R,
+                               const char* what) {
+  TORCH_CHECK(epi >= 0 && epi <= 7, what, ": unknown epilogue ", epi);
+  const bool needs_bias = epi == 1 || epi == 2 || epi == 5 || epi == 6 || epi == 7;
+  const bool needs_res = epi == 3 || epi == 5;
+  TORCH_CHECK(!needs_bias || bias.has_value(), what, ": epilogue ", epi, " needs a bias");
+  TORCH_CHECK(!needs_res || R.has_value(), what, ": epilogue ", epi, " needs a residual");
+}
+
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
           int64_t epi, int64_t force) {
   check_bf16(A, "A");
@@ -146,6 +157,7 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
   TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm: C must be bf16 or fp32");
   const int ldc = epi == 4 ? N / 2 : N;
   TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm: C has wrong size");
+  check_epi_operands(epi, bias, R, "gemm");
   if (bias) check_bf16(*bias, "bias");
   if (R) {
     check_bf16(*R, "residual");
@@ -358,6 +370,7 @@ void gemm_splitk(const Tensor& A, const Tensor& B, Tensor& C, const optional<Ten
   TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm_splitk: C has wrong size");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_cuda() &&
                   (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K), "gemm_splitk: workspace too small");
+  check_epi_operands(epi, bias, R, "gemm_splitk");
   if (bias) check_bf16(*bias, "bias");
   if (R) {
     check_bf16(*R, "residual");
@@ -397,6 +410,7 @@ void gemm_fp8(const Tensor& A, const Tensor& B, const Tensor& sa, const Tensor& 
   TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm_fp8: C must be bf16 or fp32");
   const int ldc = epi == 4 ? N / 2 : N;
   TORCH_CHECK(C.numel() == (int64_t)M * ldc, "gemm_fp8: C has wrong size");
+  check_epi_operands(epi, bias, R, "gemm_fp8");
   if (bias) check_bf16(*bias, "bias");
   if (R) {
     check_bf16(*R, "residual");

@@ -92,6 +92,43 @@ def test_gemm_fp8_large_exact_integers(cuda):
     torch.testing.assert_close(out, a @ b.t(), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("epi,what", [(1, "bias"), (3, "residual"), (5, "bias"), (9, "unknown")])
+def test_gemm_epilogue_missing_operand_refused(cuda, epi, what):
+    """An epilogue whose bias / residual operand is absent is refused on the host (the kernel would read
+    address 0), for the bf16, split-K and fp8 GEMM entry points alike."""
+    M, N, K = 256, 256, 256
+    nat = ops.native()
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match=what):
+        nat.gemm(x, w, out, None, None, epi, 0)
+    W = ops.Fp8Weight.quantize(w)
+    xq, sx = ops.quant_fp8(x)
+    with pytest.raises(RuntimeError, match=what):
+        nat.gemm_fp8(xq, W.q, sx, W.scale, out, None, None, epi, 0)
+    ws = torch.empty(1 << 20, device="cuda", dtype=torch.float32)
+    with pytest.raises(RuntimeError, match=what):
+        nat.gemm_splitk(x[:8], w, out[:8], None, None, epi, ws, False)
+    torch.cuda.synchronize()
+
+
+def test_gemm_fp8_large_rule_deep_grid(cuda):
+    """K = 1280 (the vision encoder's width): both fp8 kernels agree. The auto rule sends such a GEMM to the
+    256x256 pipelined kernel once its grid is >= 8 waves of 256 tiles (e.g. the 204928 x 5120 fc1)."""
+    M, N, K = 4096, 1280, 1280
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    W = ops.Fp8Weight.quantize((torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16))
+    xq, sx = ops.quant_fp8(x)
+    outs = []
+    for force in (2, 3):
+        out = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        ops.native().gemm_fp8(xq, W.q, sx, W.scale, out, None, None, 0, force)
+        outs.append(out)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("M", [1, 32, 64])
 @pytest.mark.parametrize("act", [None, "swiglu"])
 def test_fp8_weight_decode_copy(cuda, M, act):
