@@ -27,6 +27,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
                                                       int T, int Hq, int Hkv, int rope, float inv_ks, float inv_vs) {
   constexpr int LPH = D / 8;  // lanes per head: each lane owns 4 rotation pairs
   constexpr int HPB = 256 / LPH;
+  if (threadIdx.x >= HPB * LPH) return;  // D = 96: 12 lanes per head, 21 heads per block, 4 idle lanes
   const int H = Hq + 2 * Hkv;
   const long item = (long)blockIdx.x * HPB + threadIdx.x / LPH;  // (token, head)
   if (item >= (long)T * H) return;
@@ -60,8 +61,9 @@ void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, co
     return;                                                                                                 \
   }
   GAI_ROPE_CASE(64)
+  GAI_ROPE_CASE(96)
   GAI_ROPE_CASE(128)
   GAI_ROPE_CASE(256)
 #undef GAI_ROPE_CASE
-  gai_launch_error(__FILE__, __LINE__, "rope_kv: head_dim must be 64, 128 or 256");
+  gai_launch_error(__FILE__, __LINE__, "rope_kv: head_dim must be 64, 96, 128 or 256");
 }

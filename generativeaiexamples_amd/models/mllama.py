@@ -7,7 +7,7 @@ Vision encoder (ViT-H/14 class, 560-px tiles, up to 4 tiles per image):
   gated position + tile embedding -> LN -> 32 encoder layers (intermediate outputs of 5 of them kept)
   -> LN -> post-tile embedding -> 8 gated "global" layers -> concat(final, 5 intermediates) [*, 7680]
   -> multimodal projector GEMM -> cross-attention states [tiles * 1601, 4096].
-  Head dim 80 is zero-padded to 128 inside the QKV / O weights so attention runs on the D=128 MFMA
+  Head dim 80 is zero-padded to 96 inside the QKV / O weights so attention runs on the D=96 MFMA
   flash-attention kernel (padded q/k dims add 0 to the scores, padded v dims produce 0 columns that
   the zero O-proj columns ignore); the softmax scale stays 1/sqrt(80). The tanh gates of the gated
   layers are folded into the O / FC2 weights at load time, so every layer is the plain fused path.
@@ -67,7 +67,7 @@ class MllamaVisionConfig:
 
     @property
     def head_dim_padded(self) -> int:
-        return 64 if self.head_dim <= 64 else 128
+        return 64 if self.head_dim <= 64 else 96 if self.head_dim <= 96 else 128
 
     @property
     def num_patches(self) -> int:

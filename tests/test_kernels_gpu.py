@@ -81,7 +81,7 @@ def _make_cache(nb, Hkv, D, device):
     return k, v
 
 
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 96, 128])
 def test_rope_kv_write(cuda, D):
     torch.manual_seed(4)
     Hq, Hkv, T = 8, 2, 45
@@ -117,7 +117,8 @@ def _paged_setup(seq_lens, Hkv, D, device, seed=0):
     return kc.to(device), vc.to(device), bt.to(device)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (128, 32, 8), (64, 4, 4), (128, 8, 1), (64, 16, 8)])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (128, 32, 8), (64, 4, 4), (128, 8, 1), (64, 16, 8), (96, 16, 16),
+                                      (96, 8, 2)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_attention_prefill(cuda, D, Hq, Hkv, causal):
     torch.manual_seed(5)
@@ -222,7 +223,7 @@ def test_attention_decode_fused_merge_reuse(cuda):
 F8 = torch.float8_e4m3fn
 
 
-@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("D", [64, 96, 128, 256])
 def test_rope_kv_write_fp8(cuda, D):
     torch.manual_seed(14)
     Hq, Hkv, T = 8, 2, 45
@@ -264,7 +265,7 @@ def test_attention_decode_fp8(cuda, D, Hq, Hkv):
         _close(o, o_ref, 2e-2, 2e-2, f"fp8 decode split={ws.split_keys}")
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 16, 8), (256, 8, 4)])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 16, 8), (256, 8, 4), (96, 16, 16)])
 def test_attention_prefill_fp8(cuda, D, Hq, Hkv):
     torch.manual_seed(16)
     ctx, qlen = [77, 300, 1030], [77, 33, 1030]
