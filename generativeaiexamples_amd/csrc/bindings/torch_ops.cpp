@@ -11,6 +11,9 @@
 
 #include "gai_kernels.h"
 
+// moe.hip (declared here: a gai_kernels.h edit rebuilds every kernel)
+void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st);
+
 void gai_launch_error(const char* file, int line, const char* msg) {
   throw std::runtime_error(std::string("gai kernel error at ") + file + ":" + std::to_string(line) + ": " + msg);
 }
@@ -432,6 +435,22 @@ void moe_gemm(const Tensor& A, const optional<Tensor>& a_rows, const Tensor& W, 
                offs.data_ptr<int>(), W.size(0), rows_total, W.size(1), W.size(2), swiglu ? 1 : 0, cur_stream());
 }
 
+void moe_dispatch(const Tensor& ids, int64_t E, Tensor& a_rows, Tensor& offs, Tensor& pos) {
+  check_i32(ids, "expert ids");
+  check_i32(a_rows, "a_rows");
+  check_i32(offs, "offs");
+  check_i32(pos, "pos");
+  TORCH_CHECK(ids.is_contiguous() && a_rows.is_contiguous() && offs.is_contiguous() && pos.is_contiguous(),
+              "moe_dispatch: tensors must be contiguous");
+  TORCH_CHECK(ids.dim() == 2, "moe_dispatch: ids must be [T, k]");
+  const int64_t n = ids.numel();
+  TORCH_CHECK(E >= 1 && E <= 2048, "moe_dispatch: 1 <= experts <= 2048");
+  TORCH_CHECK(a_rows.numel() == n && pos.numel() == n && offs.numel() == E + 1, "moe_dispatch: output sizes");
+  if (n == 0) return;
+  gai_moe_dispatch(ids.data_ptr<int>(), (int)n, (int)ids.size(1), (int)E, a_rows.data_ptr<int>(),
+                   offs.data_ptr<int>(), pos.data_ptr<int>(), cur_stream());
+}
+
 void moe_combine(const Tensor& Y, const Tensor& pos, const Tensor& w, const optional<Tensor>& residual, Tensor& out) {
   check_bf16(Y, "Y");
   check_i32(pos, "pos");
@@ -664,6 +683,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_route", &moe_route);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
+  m.def("moe_dispatch", &moe_dispatch);
   m.def("embedding", &embedding);
   m.def("decode_advance", &decode_advance);
   m.def("pool", &pool);

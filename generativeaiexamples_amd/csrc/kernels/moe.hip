@@ -198,7 +198,68 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict
   store8(out + (size_t)t * D + u * 8, o);
 }
 
+
+// Expert-sorted dispatch plan for small steps (decode: T*k rows) in ONE workgroup, replacing a stable
+// argsort + scatter_add + cumsum + index_put (~10 launches and a radix sort per MoE layer). Counting sort:
+// per-expert counts in LDS -> exclusive offsets -> chunks of 256 rows placed in flat order, each row's rank
+// = expert cursor + rows of the same expert in earlier waves of the chunk + earlier lanes of its own wave
+// (wave ballot per distinct expert), so rows of one expert keep their (token, slot) order like the stable
+// argsort. Out-of-range ids are clamped so every output stays defined (moe_route never produces them).
+__global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict__ ids, int n, int k, int E,
+                                                           int* __restrict__ a_rows, int* __restrict__ offs,
+                                                           int* __restrict__ pos) {
+  extern __shared__ int dsm[];  // cursor[E] | wave counts [4][E]
+  int* cursor = dsm;
+  int* wcnt = dsm + E;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < E; e += 256) cursor[e] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) atomicAdd(&cursor[min(max(ids[i], 0), E - 1)], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int e = 0; e < E; ++e) {
+      const int c = cursor[e];
+      cursor[e] = run;
+      offs[e] = run;
+      run += c;
+    }
+    offs[E] = run;
+  }
+  for (int base = 0; base < n; base += 256) {
+    for (int x = tid; x < 4 * E; x += 256) wcnt[x] = 0;
+    __syncthreads();  // cursors final (first chunk) / advanced; wave counts cleared
+    const int i = base + tid;
+    const int e = i < n ? min(max(ids[i], 0), E - 1) : -1;
+    unsigned long long rest = __ballot(e >= 0);
+    int rank = 0;
+    while (rest) {  // wave-uniform: one pass per distinct expert in the wave
+      const int leader = __builtin_ctzll(rest);
+      const int le = __shfl(e, leader, 64);
+      const unsigned long long m = __ballot(e == le);
+      if (e == le) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == leader) wcnt[wid * E + le] = __popcll(m);
+      rest &= ~m;
+    }
+    __syncthreads();
+    if (e >= 0) {
+      int r = cursor[e] + rank;
+      for (int w = 0; w < wid; ++w) r += wcnt[w * E + e];
+      a_rows[r] = i / k;
+      pos[i] = r;
+    }
+    __syncthreads();
+    for (int x = tid; x < E; x += 256) cursor[x] += wcnt[x] + wcnt[E + x] + wcnt[2 * E + x] + wcnt[3 * E + x];
+  }
+}
+
 }  // namespace
+
+void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st) {
+  if (E < 1 || E > 2048) gai_launch_error(__FILE__, __LINE__, "moe_dispatch: 1 <= experts <= 2048");
+  moe_dispatch_kernel<<<1, 256, 5 * E * sizeof(int), st>>>(ids, n, k, E, a_rows, offs, pos);
+  GAI_LAUNCH_CHECK();
+}
 
 void gai_moe_route(const float* logits, int T, int E, int k, int renorm, int* ids, float* w, hipStream_t st) {
   if (T == 0) return;

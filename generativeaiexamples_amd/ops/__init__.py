@@ -637,9 +637,21 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):
     return ids, w
 
 
+_MOE_DISPATCH_MAX = int(os.environ.get("GAI_MOE_DISPATCH_MAX", "4096"))
+
+
 def moe_dispatch(ids: torch.Tensor, num_experts: int):
-    """Expert-sorted dispatch plan without host sync: (a_rows [T*k], offsets [E+1], pos [T,k])."""
+    """Expert-sorted dispatch plan without host sync: (a_rows [T*k], offsets [E+1], pos [T,k]).
+    Up to _MOE_DISPATCH_MAX rows (decode steps) one single-workgroup counting-sort kernel builds it; larger
+    steps keep the stable argsort (the one workgroup walks rows 256 at a time)."""
     T, k = ids.shape
+    if ids.is_cuda and 0 < T * k <= _MOE_DISPATCH_MAX:
+        dev = ids.device
+        a_rows = torch.empty(T * k, dtype=torch.int32, device=dev)
+        offs = torch.empty(num_experts + 1, dtype=torch.int32, device=dev)
+        pos = torch.empty(T, k, dtype=torch.int32, device=dev)
+        native().moe_dispatch(ids.to(torch.int32).contiguous(), num_experts, a_rows, offs, pos)
+        return a_rows, offs, pos
     flat = ids.reshape(-1).long()
     order = torch.argsort(flat, stable=True)
     a_rows = (order // k).to(torch.int32)

@@ -145,3 +145,29 @@ def test_mixtral_dense_prefill_matches_grouped(cuda, monkeypatch):
                 u = xf[sel] @ gu[:, 1].reshape(-1, cfg.hidden_size).t()
                 want[sel] += wts[sel, j:j + 1] * ((torch.nn.functional.silu(g) * u) @ w2[e].t())
     _close(outs[1], want, 3e-2, 3e-2, "dense MoE vs fp32")
+
+
+@pytest.mark.parametrize("T,k,E", [(1, 2, 8), (64, 2, 8), (300, 2, 9), (2048, 2, 8), (37, 4, 65), (5, 2, 1024)])
+def test_moe_dispatch_kernel_matches_stable_argsort(cuda, T, k, E):
+    """The single-workgroup counting-sort dispatch equals the stable argsort plan row for row (rows of one
+    expert in (token, slot) order), skewed expert loads and unused experts included."""
+    g = torch.Generator().manual_seed(T * 131 + E)
+    ids = torch.randint(0, E, (T, k), generator=g, dtype=torch.int32)
+    if T > 8:
+        ids[: T // 2, 0] = E // 2  # a hot expert spanning many chunks and waves
+    a_rows = torch.empty(T * k, dtype=torch.int32, device=cuda)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=cuda)
+    pos = torch.empty(T, k, dtype=torch.int32, device=cuda)
+    ops.native().moe_dispatch(ids.to(cuda), E, a_rows, offs, pos)
+    flat = ids.reshape(-1).long()
+    order = torch.argsort(flat, stable=True)
+    want_pos = torch.empty(T * k, dtype=torch.int64)
+    want_pos[order] = torch.arange(T * k)
+    want_offs = torch.zeros(E + 1, dtype=torch.int64)
+    want_offs[1:] = torch.bincount(flat, minlength=E).cumsum(0)
+    assert torch.equal(offs.cpu().long(), want_offs)
+    assert torch.equal(a_rows.cpu().long(), order // k)
+    assert torch.equal(pos.cpu().long().reshape(-1), want_pos)
+    # and through ops.moe_dispatch (native up to _MOE_DISPATCH_MAX rows)
+    r, o, p = ops.moe_dispatch(ids.to(cuda), E)
+    assert torch.equal(r.cpu().long(), order // k) and torch.equal(o.cpu().long(), want_offs)
