@@ -637,13 +637,14 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True):
     return ids, w
 
 
-_MOE_DISPATCH_MAX = int(os.environ.get("GAI_MOE_DISPATCH_MAX", "4096"))
+_MOE_DISPATCH_MAX = int(os.environ.get("GAI_MOE_DISPATCH_MAX", "8192"))
 
 
 def moe_dispatch(ids: torch.Tensor, num_experts: int):
     """Expert-sorted dispatch plan without host sync: (a_rows [T*k], offsets [E+1], pos [T,k]).
     Up to _MOE_DISPATCH_MAX rows (decode steps) one single-workgroup counting-sort kernel builds it; larger
-    steps keep the stable argsort (the one workgroup walks rows 256 at a time)."""
+    steps keep the stable argsort (the one workgroup walks rows 256 at a time: level at ~16K rows,
+    profiles/r3/moe_dispatch/dispatch_microbench.txt)."""
     T, k = ids.shape
     if ids.is_cuda and 0 < T * k <= _MOE_DISPATCH_MAX:
         dev = ids.device
