@@ -11,9 +11,6 @@
 
 #include "gai_kernels.h"
 
-// moe.hip (declared here: a gai_kernels.h edit rebuilds every kernel)
-void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st);
-
 void gai_launch_error(const char* file, int line, const char* msg) {
   throw std::runtime_error(std::string("gai kernel error at ") + file + ":" + std::to_string(line) + ": " + msg);
 }

@@ -92,6 +92,10 @@ void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N
                   int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st);
 
 // moe.hip
+void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st);
+// gemm_decode.hip: decode-sized grouped GEMM on the weight-streaming decode kernel (0 = shape not handled)
+int gai_moe_gemm_dec2(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E,
+                      int rows_total, int N, int K, int swiglu, hipStream_t st);
 void gai_moe_route(const float* logits, int T, int E, int k, int renorm, int* ids, float* w, hipStream_t st);
 void gai_moe_gemm(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E, int rows_total,
                   int N, int K, int swiglu, hipStream_t st);

@@ -250,6 +250,7 @@ __global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict
     }
     __syncthreads();
     for (int x = tid; x < E; x += 256) cursor[x] += wcnt[x] + wcnt[E + x] + wcnt[2 * E + x] + wcnt[3 * E + x];
+    __syncthreads();  // every cursor update has read its wave counts before the next chunk clears them
   }
 }
 
@@ -267,10 +268,6 @@ void gai_moe_route(const float* logits, int T, int E, int k, int renorm, int* id
   moe_route_kernel<<<(T + 255) / 256, 256, 0, st>>>(logits, T, E, k, renorm, ids, w);
   GAI_LAUNCH_CHECK();
 }
-
-// gemm_decode.hip: decode-sized grouped GEMM on the weight-streaming decode kernel (0 = shape not handled)
-int gai_moe_gemm_dec2(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E,
-                      int rows_total, int N, int K, int swiglu, hipStream_t st);
 
 void gai_moe_gemm(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E, int rows_total,
                   int N, int K, int swiglu, hipStream_t st) {

@@ -38,6 +38,17 @@ class StreamItem:
 log = logging.getLogger(__name__)
 
 
+def _settle(fut: concurrent.futures.Future, res=None, exc: Optional[BaseException] = None) -> None:
+    """Complete ``fut`` unless it is already done (cancelled by its awaiting task): never raises."""
+    try:
+        if exc is not None:
+            fut.set_exception(exc)
+        else:
+            fut.set_result(res)
+    except concurrent.futures.InvalidStateError:
+        pass
+
+
 class AsyncLLMEngine:
     """``watchdog_s`` (env GAI_WATCHDOG_S, default 300): a step running longer than this (hung kernel or
     collective) marks the engine unhealthy - /v1/health/ready turns 503 so a router drains it - dumps
@@ -53,6 +64,7 @@ class AsyncLLMEngine:
         self.watchdog_s = watchdog_s if watchdog_s is not None else float(os.environ.get("GAI_WATCHDOG_S", "300"))
         self.admission_wait_s = float(os.environ.get("GAI_ADMISSION_WAIT_MS", "25")) / 1000.0
         self._step_started: Optional[float] = None
+        self._hung = False  # the watchdog fired on the running step: nothing reaches the engine thread now
         # (request id, generated tokens, finish reason) of recently finished requests (benchmarks, tests)
         self.completed: collections.deque = collections.deque(maxlen=4096)
         # per finished streamed request, perf_counter timestamps (CLOCK_MONOTONIC: comparable across processes):
@@ -66,10 +78,15 @@ class AsyncLLMEngine:
         self.watchdog = threading.Thread(target=self._watch, daemon=True, name="llm-watchdog")
         self.watchdog.start()
 
-    def _fail_all(self, e: BaseException):
+    def _fail_all(self, e: BaseException, inbox: bool = False):
         for rid, (loop, q) in list(self.queues.items()):
             loop.call_soon_threadsafe(q.put_nowait, e)
         self.queues.clear()
+        if inbox:  # a hung step never drains the inbox: fail the admissions waiting in it too
+            with self.cv:
+                pending, self.inbox = list(self.inbox), collections.deque()
+            for _, _, _, fut in pending:
+                _settle(fut, exc=e)
 
     def _watch(self):
         period = max(0.05, min(1.0, self.watchdog_s / 4))
@@ -77,10 +94,10 @@ class AsyncLLMEngine:
             t = self._step_started
             if t is not None and self.healthy and time.perf_counter() - t > self.watchdog_s:
                 err = TimeoutError(f"engine step exceeded the {self.watchdog_s:.1f}s watchdog")
-                self.error, self.healthy = err, False
+                self.error, self.healthy, self._hung = err, False, True
                 log.error("%s; dumping thread stacks", err)
                 faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
-                self._fail_all(err)
+                self._fail_all(err, inbox=True)
 
     @property
     def tokenizer(self):
@@ -91,6 +108,9 @@ class AsyncLLMEngine:
         engine holds its lock for a whole step (a prefill chunk waits ~0.2 s on the GPU), and an event-loop
         thread blocked on that lock stalls every open SSE stream (served first-frame delay 0.5 s p50)."""
         fut: concurrent.futures.Future = concurrent.futures.Future()
+        if self._hung:  # the engine thread is stuck in a step: fail now instead of waiting forever
+            _settle(fut, exc=self.error or RuntimeError("engine step hung"))
+            return fut
         with self.cv:
             self.inbox.append((fn, args, kw, fut))
             self.cv.notify()
@@ -102,10 +122,15 @@ class AsyncLLMEngine:
                 if not self.inbox:
                     return
                 fn, args, kw, fut = self.inbox.popleft()
+            # a caller that went away (asyncio cancellation of the wrapped future) is skipped, never half-applied
+            if not fut.set_running_or_notify_cancel():
+                continue
             try:
-                fut.set_result(fn(*args, **kw))
+                res = fn(*args, **kw)
             except BaseException as e:  # noqa: BLE001 - delivered to the caller
-                fut.set_exception(e)
+                _settle(fut, exc=e)
+            else:
+                _settle(fut, res=res)
 
     def _loop(self):
         eng = self.engine
@@ -115,15 +140,16 @@ class AsyncLLMEngine:
                     self.cv.wait(0.05)
             if not self.running:
                 break
-            self._drain()
+            self._safe_drain()
             if not eng.has_work():
                 continue
             self._admission_wait(eng)
-            self._drain()  # requests that arrived during the wait join this step
+            self._safe_drain()  # requests that arrived during the wait join this step
             try:
                 t0 = self._step_started = time.perf_counter()
                 outs = eng.step()
                 self._step_started = None
+                self._hung = False
                 METRICS.observe_step(time.perf_counter() - t0, len(outs), eng)
             except BaseException as e:  # engine failure: fail every pending request, keep serving health
                 self._step_started = None
@@ -138,6 +164,12 @@ class AsyncLLMEngine:
                 loop.call_soon_threadsafe(q.put_nowait, o)
                 if o.finished:
                     self.queues.pop(o.request_id, None)
+
+    def _safe_drain(self):
+        try:
+            self._drain()
+        except BaseException:  # noqa: BLE001 - one bad inbox item must not end the engine thread
+            log.exception("engine inbox item failed")
 
     def _admission_wait(self, eng) -> None:
         """Before a step that would only start prefill for newly queued prompts (nothing running, nothing in
@@ -254,7 +286,7 @@ class AsyncLLMEngine:
             pending, self.inbox = list(self.inbox), collections.deque()
             self.cv.notify_all()
         for _, _, _, fut in pending:
-            fut.set_exception(RuntimeError("engine shut down"))
+            _settle(fut, exc=RuntimeError("engine shut down"))
         self._stop.set()
         with self.cv:
             self.cv.notify_all()

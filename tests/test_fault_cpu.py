@@ -82,3 +82,83 @@ def test_watchdog_fails_hung_step():
     assert time.perf_counter() - t0 < 2.5  # failed by the watchdog, not after the 3 s step
     assert not eng.healthy
     eng.shutdown()
+
+
+class _SlowEngine:
+    """Fake engine: every step takes 0.3 s and emits one finishing token for each admitted request."""
+    tok = None
+
+    def __init__(self, step_s=0.3):
+        self.step_s, self.live, self.admitted = step_s, [], []
+        self.stats = dict(prefill_tokens=0, decode_tokens=0)
+
+    def add_request(self, ids, params, rid, images=None, lora=None):
+        self.admitted.append(rid)
+        self.live.append(rid)
+
+        class Req:
+            finished = False
+            output_ids = [1]
+            first_token_time = None
+        return Req()
+
+    def has_work(self):
+        return bool(self.live)
+
+    def step(self):
+        from generativeaiexamples_amd.engine.llm_engine import RequestOutput
+        time.sleep(self.step_s)
+        outs = [RequestOutput(r, 7, "a", True, "stop") for r in self.live]
+        self.live = []
+        return outs
+
+    def abort(self, rid):
+        return True
+
+
+def test_cancel_during_admission_keeps_engine_alive():
+    """a client that disconnects while its admission waits in the inbox must be skipped, and the
+    engine thread must keep serving later requests."""
+    from generativeaiexamples_amd.serving.async_engine import AsyncLLMEngine
+    fake = _SlowEngine()
+    eng = AsyncLLMEngine(fake, watchdog_s=30)
+
+    async def consume(rid):
+        return [it async for it in eng.generate([1, 2], None, rid)]
+
+    async def go():
+        busy = asyncio.create_task(consume("busy"))  # keeps the engine thread inside a 0.3 s step
+        await asyncio.sleep(0.1)
+        victim = asyncio.create_task(consume("victim"))  # its admission now waits in the inbox
+        await asyncio.sleep(0.05)
+        victim.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await victim
+        assert len(await busy) == 1
+        after = await asyncio.wait_for(consume("after"), timeout=5)
+        assert len(after) == 1 and after[0].finished
+
+    asyncio.run(go())
+    assert eng.thread.is_alive() and eng.healthy
+    assert "victim" not in fake.admitted  # cancelled before it ran: never half-applied
+    eng.shutdown()
+
+
+def test_watchdog_fails_new_admissions_fast():
+    """while a step is hung, new requests fail with the engine error instead of waiting."""
+    from generativeaiexamples_amd.serving.async_engine import AsyncLLMEngine
+    eng = AsyncLLMEngine(_SlowEngine(step_s=3.0), watchdog_s=0.4)
+
+    async def go():
+        first = asyncio.create_task(eng.complete([1], None, "r0"))
+        await asyncio.sleep(1.0)  # the watchdog has fired on the hung step
+        t0 = time.perf_counter()
+        with pytest.raises(TimeoutError):
+            await eng.complete([1], None, "r1")
+        assert time.perf_counter() - t0 < 0.5
+        with pytest.raises(RuntimeError):
+            await first
+
+    asyncio.run(go())
+    assert not eng.healthy
+    eng.shutdown()

@@ -147,7 +147,8 @@ def test_mixtral_dense_prefill_matches_grouped(cuda, monkeypatch):
     _close(outs[1], want, 3e-2, 3e-2, "dense MoE vs fp32")
 
 
-@pytest.mark.parametrize("T,k,E", [(1, 2, 8), (64, 2, 8), (300, 2, 9), (2048, 2, 8), (37, 4, 65), (5, 2, 1024)])
+@pytest.mark.parametrize("T,k,E", [(1, 2, 8), (64, 2, 8), (300, 2, 9), (2048, 2, 8), (37, 4, 65), (5, 2, 1024),
+                                   (300, 2, 64), (2048, 2, 128), (700, 2, 1024)])  # E >= 17 over many chunks
 def test_moe_dispatch_kernel_matches_stable_argsort(cuda, T, k, E):
     """The single-workgroup counting-sort dispatch equals the stable argsort plan row for row (rows of one
     expert in (token, slot) order), skewed expert loads and unused experts included."""

@@ -50,7 +50,9 @@ for spec in "$@"; do
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
              python3 "$PWD/bench.py" "${rest[@]}" --json-out "$O/$n.json" || exit $?
            python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
-             > /dev/null || exit $? ;;
+             > /dev/null || exit $?
+           python tools/trace_gaps.py "/tmp/prof_$n/**/*kernel_trace.csv" --from-frac 0.6 --top 40 \
+             -o "$O/${n}_gaps.json" > /dev/null || exit $? ;;
     py)    step 600 "$O/$n.log" python "${rest[@]}" || exit $? ;;
     pyprof) rm -rf "/tmp/prof_$n"
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
