@@ -90,7 +90,8 @@ def run(args, ctx) -> dict:
         reqs = []
         for q, st in zip(qs, states):
             ids = apply_chat_template([{"role": "system", "content": system},
-                                       {"role": "user", "content": q}], tok)
+                                       {"role": "user", "content": [{"type": "image"}, {"type": "text", "text": q}]}],
+                                      tok, image_token_id=llm.mcfg.image_token_id)
             reqs.append(engine.add_request(ids, params, images=[st]))
         while engine.has_work():
             engine.step()

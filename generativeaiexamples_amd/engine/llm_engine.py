@@ -278,7 +278,7 @@ class LLMEngine:
             if images:
                 if not hasattr(self.model, "register_request"):
                     raise ValueError(f"{self.model.cfg.name} does not accept image inputs")
-                self.model.register_request(sid, images)
+                self.model.register_request(sid, images, prompt_ids=req.prompt_ids)
             if max_new == 0:
                 self._release(sid)
                 req.finished, req.finish_reason = True, "length"

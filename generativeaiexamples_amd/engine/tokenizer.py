@@ -151,21 +151,48 @@ def load_tokenizer(path: Optional[str], family: str = "llama3", vocab_size: Opti
 
 
 # ----------------------------------------------------------------------------------- chat templates
-def apply_chat_template(messages: List[dict], tok: Tokenizer, add_generation_prompt: bool = True) -> List[int]:
-    """Llama-3 chat format when its header tokens exist, else a plain role-prefixed format."""
+def image_token_of(model) -> Optional[int]:
+    """The image placeholder token id of a multimodal generator (Mllama's <|image|>), None for text models."""
+    return getattr(getattr(model, "mcfg", None), "image_token_id", None)
+
+
+def apply_chat_template(messages: List[dict], tok: Tokenizer, add_generation_prompt: bool = True,
+                        image_token_id: Optional[int] = None) -> List[int]:
+    """Llama-3 chat format when its header tokens exist, else a plain role-prefixed format. A list content holds
+    OpenAI-style parts: text parts are encoded in order; image parts (``image_url`` / ``image``) become
+    ``image_token_id`` where they stand (Llama-3.2-Vision's <|image|>) when one is given, else they are dropped."""
     sh, eh, eot = tok.token_id("<|start_header_id|>"), tok.token_id("<|end_header_id|>"), tok.token_id("<|eot_id|>")
     ids: List[int] = []
     if tok.bos_id is not None:
         ids.append(tok.bos_id)
+
+    def body(content) -> List[int]:
+        if not isinstance(content, list):
+            return tok.encode("\n\n" + (content or "").strip())
+        out, first_text = tok.encode("\n\n"), True
+        for p in content:
+            if not isinstance(p, dict):
+                continue
+            if p.get("type") in ("image_url", "image"):
+                if image_token_id is not None:
+                    out.append(image_token_id)
+            elif p.get("type") in ("text", None):
+                t = p.get("text", "")
+                out += tok.encode(t.lstrip() if first_text else t)
+                first_text = False
+        return out
+
     if sh is not None and eh is not None and eot is not None:
         for m in messages:
-            content = m.get("content") or ""
-            if isinstance(content, list):  # multimodal parts: keep the text
-                content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
-            ids += [sh] + tok.encode(m.get("role", "user")) + [eh] + tok.encode("\n\n" + content.strip()) + [eot]
+            ids += [sh] + tok.encode(m.get("role", "user")) + [eh] + body(m.get("content")) + [eot]
         if add_generation_prompt:
             ids += [sh] + tok.encode("assistant") + [eh] + tok.encode("\n\n")
         return ids
+    if image_token_id is not None and any(isinstance(m.get("content"), list) and any(
+            isinstance(p, dict) and p.get("type") in ("image_url", "image") for p in m["content"]) for m in messages):
+        ids.append(image_token_id)
+    messages = [dict(m, content="".join(p.get("text", "") for p in m["content"] if isinstance(p, dict))
+                     if isinstance(m.get("content"), list) else m.get("content")) for m in messages]
     text = "".join(f"{m.get('role', 'user')}: {m.get('content') or ''}\n" for m in messages)
     if add_generation_prompt:
         text += "assistant: "

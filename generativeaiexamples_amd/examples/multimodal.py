@@ -37,13 +37,14 @@ def vlm_describer(hub):
     import base64
 
     from ..engine import SamplingParams
-    from ..engine.tokenizer import apply_chat_template
+    from ..engine.tokenizer import apply_chat_template, image_token_of
 
     def describe(path: str, context: str) -> str:
         with open(path, "rb") as f:
             uri = "data:image;base64," + base64.b64encode(f.read()).decode()
         ask = DESCRIBE_PROMPT + (f" Text around the image: {context}" if context else "")
-        ids = apply_chat_template([{"role": "user", "content": ask}], llm.tokenizer)
+        ids = apply_chat_template([{"role": "user", "content": [{"type": "image"}, {"type": "text", "text": ask}]}],
+                                  llm.tokenizer, image_token_id=image_token_of(llm.engine.model))
         out = llm.generate_sync(ids, SamplingParams(temperature=0.0, max_tokens=256), images=[uri])
         return "".join(it.delta for it in out).strip()
 

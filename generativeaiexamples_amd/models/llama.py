@@ -142,6 +142,12 @@ class LlamaConfig:
     def from_hf(path: str) -> "LlamaConfig":
         with open(os.path.join(path, "config.json")) as f:
             c = json.load(f)
+        return LlamaConfig(**LlamaConfig.hf_fields(c, os.path.basename(path.rstrip("/"))))
+
+    @staticmethod
+    def hf_fields(c: dict, name: str) -> dict:
+        """LlamaConfig keyword arguments of a HF decoder config.json (llama / mistral / mixtral / gemma /
+        starcoder2 / qwen2 / qwen3; transformers 4 and 5 rope layouts)."""
         eos = c.get("eos_token_id", 2)
         mt = c.get("model_type", "llama")
         flags = {}
@@ -156,17 +162,34 @@ class LlamaConfig:
             flags = dict(arch="qwen2", qkv_bias=True)
         elif mt == "qwen3":
             flags = dict(arch="qwen3", qk_norm=True, qkv_bias=bool(c.get("attention_bias", False)))
-        elif mt == "mistral":
+        elif mt in ("mistral", "mixtral"):
             flags = dict(arch="mistral")
-        return LlamaConfig(**flags,
+        theta, scaling = hf_rope(c)
+        return dict(**flags,
             vocab_size=c["vocab_size"], hidden_size=c["hidden_size"], intermediate_size=c["intermediate_size"],
             num_layers=c["num_hidden_layers"], num_heads=c["num_attention_heads"],
-            num_kv_heads=c.get("num_key_value_heads", c["num_attention_heads"]),
+            num_kv_heads=c.get("num_key_value_heads") or c["num_attention_heads"],
             head_dim=c.get("head_dim") or c["hidden_size"] // c["num_attention_heads"],
-            rope_theta=c.get("rope_theta", 10000.0), rope_scaling=c.get("rope_scaling"),
+            rope_theta=theta, rope_scaling=scaling,
             rms_eps=c.get("rms_norm_eps", 1e-5), max_position=c.get("max_position_embeddings", 8192),
             tie_embeddings=c.get("tie_word_embeddings", False), bos_token_id=c.get("bos_token_id", 1),
-            eos_token_ids=tuple(eos) if isinstance(eos, list) else (eos,), name=os.path.basename(path.rstrip("/")))
+            eos_token_ids=tuple(eos) if isinstance(eos, list) else (eos,), name=name)
+
+
+def hf_rope(c: dict) -> tuple:
+    """(rope_theta, llama3 scaling dict or None) of a HF config: transformers 4 keeps ``rope_theta`` and
+    ``rope_scaling`` at the top level (the published Llama-3.x checkpoints), transformers 5 writes one
+    ``rope_parameters`` dict. Only the default and ``llama3`` rope types exist in this framework."""
+    rp = c.get("rope_parameters") or {}
+    theta = float(c.get("rope_theta") or rp.get("rope_theta") or 10000.0)
+    sc = c.get("rope_scaling") or rp
+    kind = (sc or {}).get("rope_type", (sc or {}).get("type", "default"))
+    if kind in ("default", None) or not sc:
+        return theta, None
+    if kind != "llama3":
+        raise ValueError(f"rope_type {kind!r} is not supported (default and llama3 are)")
+    return theta, {k: sc[k] for k in ("factor", "low_freq_factor", "high_freq_factor",
+                                      "original_max_position_embeddings") if k in sc}
 
 
 class LlamaModel:

@@ -44,6 +44,14 @@ class MixtralConfig(LlamaConfig):
                              max_position=32768, bos_token_id=1, eos_token_ids=(2,), **kw)
 
     @staticmethod
+    def from_hf(path: str) -> "MixtralConfig":
+        import json
+        with open(os.path.join(path, "config.json")) as f:
+            c = json.load(f)
+        return MixtralConfig(**LlamaConfig.hf_fields(c, os.path.basename(path.rstrip("/"))),
+                             num_experts=c.get("num_local_experts", 8), top_k=c.get("num_experts_per_tok", 2))
+
+    @staticmethod
     def tiny_moe(**kw):
         base = dict(vocab_size=512, hidden_size=256, intermediate_size=256, num_layers=2, num_heads=4, num_kv_heads=2,
                     head_dim=64, max_position=2048, bos_token_id=1, eos_token_ids=(2,), name="tiny-moe",

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from .. import ops
 from .clip import _to_chw_float
 from .common import ForwardBatch, PackedAttention, quantize_linear_weights_fp8, randn_like_
-from .llama import LlamaConfig, LlamaModel
+from .llama import LlamaConfig, LlamaModel, hf_rope
 
 MLLAMA_MEAN = (0.48145466, 0.4578275, 0.40821073)
 MLLAMA_STD = (0.26862954, 0.26130258, 0.27577711)
@@ -124,8 +124,8 @@ class MllamaConfig:
         text = LlamaConfig(vocab_size=t["vocab_size"], hidden_size=t["hidden_size"],
                            intermediate_size=t["intermediate_size"], num_layers=t["num_hidden_layers"],
                            num_heads=t["num_attention_heads"], num_kv_heads=t["num_key_value_heads"],
-                           head_dim=t["hidden_size"] // t["num_attention_heads"], rope_theta=t["rope_theta"],
-                           rope_scaling=t.get("rope_scaling"), rms_eps=t.get("rms_norm_eps", 1e-5),
+                           head_dim=t["hidden_size"] // t["num_attention_heads"], rope_theta=hf_rope(t)[0],
+                           rope_scaling=hf_rope(t)[1], rms_eps=t.get("rms_norm_eps", 1e-5),
                            max_position=t.get("max_position_embeddings", 131072),
                            bos_token_id=t.get("bos_token_id", 128000),
                            eos_token_ids=tuple(eos) if isinstance(eos, list) else (eos,),
@@ -139,6 +139,44 @@ class MllamaConfig:
         return MllamaConfig(text=text, vision=vis, cross_layers=tuple(t["cross_attention_layers"]),
                             image_token_id=c.get("image_token_index", 128256),
                             extra_vocab=8, name=text.name)
+
+
+class _TileMaskAttention(PackedAttention):
+    """Vision self-attention under the reference's tile mask (see MllamaModel._tile_layout): per image, valid
+    queries see all L keys, masked queries the first nvalid keys; both segments read the image's one set of
+    paged K/V blocks (two varlen sequences sharing a block table)."""
+
+    def __init__(self, nvalid: Sequence[int], L: int, num_heads: int, head_dim: int, device, dtype=torch.bfloat16):
+        BS = ops.BLOCK
+        nb = (L + BS - 1) // BS
+        q_lens, rows, ctx = [], [], []
+        for b, nv in enumerate(nvalid):
+            blocks = torch.arange(b * nb, (b + 1) * nb, dtype=torch.int32)
+            for ql, kl in ((nv, L), (L - nv, nv)):
+                if ql:
+                    q_lens.append(ql)
+                    rows.append(blocks)
+                    ctx.append(kl)
+        self.H = self.Hkv = num_heads
+        self.hd, self.causal, self.dtype, self.device = head_dim, False, dtype, torch.device(device)
+        self.q_lens, self.kv_lens, self.T = q_lens, ctx, len(nvalid) * L
+        dev = self.device
+        self.positions = torch.zeros(self.T, dtype=torch.int32, device=dev)
+        self.block_tables = torch.stack(rows).to(dev, non_blocking=True)
+        self.slots = torch.cat([b * nb * BS + torch.arange(L, dtype=torch.int32)
+                                for b in range(len(nvalid))]).to(dev, non_blocking=True)
+        cu = [0]
+        for n in q_lens:
+            cu.append(cu[-1] + n)
+        self.cu_q = torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True)
+        self.ctx = torch.tensor(ctx, dtype=torch.int32).to(dev, non_blocking=True)
+        self.tiles = ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev) if dev.type == "cuda" else None
+        nblk = len(nvalid) * nb
+        self.k_cache = torch.zeros(nblk + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
+        self.v_cache = torch.zeros(nblk + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)
+        self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)
+        self.rope = False
+        self.cs = torch.zeros(1, head_dim, dtype=torch.float32, device=dev)
 
 
 @dataclass
@@ -197,6 +235,7 @@ class MllamaModel(LlamaModel):
         self.max_cross_tokens = V.max_num_tiles * V.tokens_per_tile
         self.max_images_in_flight = max_images_in_flight
         self.cross: Optional[CrossCache] = None
+        self.img_start: Dict[int, int] = {}  # sequence id -> position of its first <|image|> token
         self.vscale = 1.0 / math.sqrt(V.head_dim)
         self.mean = torch.tensor(MLLAMA_MEAN, dtype=torch.float32, device=self.device)
         self.inv_std = 1.0 / torch.tensor(MLLAMA_STD, dtype=torch.float32, device=self.device)
@@ -408,32 +447,71 @@ class MllamaModel(LlamaModel):
                 kept.append(h)
         return h, kept
 
+    def _tile_layout(self, images: Sequence[ImageInput]):
+        """Token layout of the vision encoder, the reference's (HF / Meta Mllama): every image runs ALL
+        max_num_tiles tiles (absent tiles are zero pixels), each tile's 1 + num_patches tokens zero-padded to a
+        multiple of 8 (P8). A token is *valid* when its tile is present and it is not padding. The reference's
+        mask blocks attention only between two masked tokens: a valid token attends to every token of its image
+        (padding and absent tiles included), a masked one to the valid ones. Tokens are kept valid-first per image
+        (the encoder has no positional term inside attention, so order is free): the mask becomes two query
+        segments over ONE key image, so the paged varlen kernel runs it as two sequences sharing blocks.
+        Returns (perm [B * L] natural -> valid-first index, per-image valid counts, L)."""
+        V = self.mcfg.vision
+        NT, TPT = V.max_num_tiles, V.tokens_per_tile
+        P8 = (TPT + 7) // 8 * 8
+        L = NT * P8
+        perm, nvalid = [], []
+        for b, im in enumerate(images):
+            nat = torch.arange(L).view(NT, P8)
+            valid = torch.zeros(NT, P8, dtype=torch.bool)
+            valid[: im.num_tiles, :TPT] = True
+            perm.append(torch.cat([nat[valid], nat[~valid]]) + b * L)
+            nvalid.append(im.num_tiles * TPT)
+        return torch.cat(perm), nvalid, L
+
     @torch.no_grad()
     def encode_images(self, images: Sequence[ImageInput]) -> List[torch.Tensor]:
         """-> per image cross-attention states [n_tiles * 1601, text hidden] (bf16)."""
         V, w, g = self.mcfg.vision, self.w, self.gates
         D, NT, TPT = V.hidden_size, V.max_num_tiles, V.tokens_per_tile
+        P8 = (TPT + 7) // 8 * 8
+        B = len(images)
         pix = torch.cat([im.pixels for im in images]).contiguous()
         ntiles = [im.num_tiles for im in images]
         nt = sum(ntiles)
         x = ops.patchify(pix, V.patch_size, self.mean, self.inv_std, V.patch_k)
-        pe = ops.linear(x, w["v.patch"]).view(nt, V.num_patches, D)
+        pe_live = ops.linear(x, w["v.patch"]).view(nt, V.num_patches, D)
+        # every image carries NT tiles: absent tiles are zero pixels = zero patch embeddings (no bias)
+        pe = torch.zeros(B, NT, V.num_patches, D, device=self.device, dtype=self.dtype)
+        o = 0
+        for b, n in enumerate(ntiles):
+            pe[b, :n] = pe_live[o:o + n]
+            o += n
+        ar = torch.tensor([im.aspect_ratio_id for im in images], device=self.device)
         # tanh-gated embeddings (tiny elementwise work next to the 40 layers; plain torch ops)
-        pre = torch.cat([w["v.pre_tile"][im.aspect_ratio_id].view(NT, D)[: im.num_tiles] for im in images])
-        pe = pe + (g["pre_tile"] * pre.float()).to(self.dtype)[:, None, :]
-        tile_pos = torch.cat([w["v.tile_pos"][im.aspect_ratio_id].view(NT, TPT, D)[: im.num_tiles]
-                              for im in images])
-        pos = ((1 - g["pos"]) * w["v.pos"].float()[None] + g["pos"] * tile_pos.float()).to(self.dtype)
-        cls = w["v.cls"].view(1, 1, D).expand(nt, 1, D)
-        h = (torch.cat([cls, pe], 1) + pos).reshape(nt * TPT, D)
-        h = ops.layer_norm(h, w["v.ln_pre_w"], w["v.ln_pre_b"], V.ln_eps)
-        attn = PackedAttention([n * TPT for n in ntiles], V.num_heads, V.head_dim_padded, self.device, self.dtype)
+        pre = w["v.pre_tile"][ar].view(B, NT, 1, D).float()
+        pe = (pe.float() + g["pre_tile"] * pre).to(self.dtype)
+        pos = (1 - g["pos"]) * w["v.pos"].float().view(1, 1, TPT, D) + \
+            g["pos"] * w["v.tile_pos"][ar].view(B, NT, TPT, D).float()
+        cls = w["v.cls"].view(1, 1, 1, D).expand(B, NT, 1, D)
+        h = (torch.cat([cls, pe], 2).float() + pos).to(self.dtype).reshape(B * NT * TPT, D)
+        h = ops.layer_norm(h, w["v.ln_pre_w"], w["v.ln_pre_b"], V.ln_eps).view(B, NT, TPT, D)
+        h = F.pad(h, (0, 0, 0, P8 - TPT))  # padding tokens enter the encoder as exact zeros
+        perm, nvalid, L = self._tile_layout(images)
+        perm = perm.to(self.device)
+        h = h.reshape(B * L, D).index_select(0, perm).contiguous()
+        attn = _TileMaskAttention(nvalid, L, V.num_heads, V.head_dim_padded, self.device, self.dtype)
         h, kept = self._vision_layers(h, 0, V.num_layers, attn, keep=set(V.intermediate_layers))
         h = ops.layer_norm(h, w["v.ln_post_w"], w["v.ln_post_b"], V.ln_eps)
-        post = torch.cat([w["v.post_tile"][im.aspect_ratio_id].view(NT, D)[: im.num_tiles] for im in images])
-        h = (h.view(nt, TPT, D).float() + g["post_tile"] * post.float()[:, None, :]).to(self.dtype).view(nt * TPT, D)
+        post = w["v.post_tile"][ar].view(B, NT, 1, D).expand(B, NT, P8, D).reshape(B * L, D).index_select(0, perm)
+        h = (h.float() + g["post_tile"] * post.float()).to(self.dtype)
         h, _ = self._vision_layers(h, V.num_layers, V.num_layers + V.num_global_layers, attn)
-        feats = torch.cat([h] + kept, dim=-1)  # [nt * TPT, 7680]
+        # valid tokens only (valid-first layout: the first n * TPT of each image, tile-major like the reference)
+        sel = torch.cat([torch.arange(nv) + b * L for b, nv in enumerate(nvalid)]).to(self.device)
+        # intermediate features interleaved per channel (the reference stacks them on a new last dim):
+        # column D + d * n_kept + j = channel d of kept layer j
+        inter = torch.stack([k.index_select(0, sel) for k in kept], dim=-1).flatten(-2)
+        feats = torch.cat([h.index_select(0, sel), inter], dim=-1)
         states = ops.linear(feats, w["proj"], bias=w["proj_b"])
         out, o = [], 0
         for n in ntiles:
@@ -450,13 +528,25 @@ class MllamaModel(LlamaModel):
         return self.cross
 
     @torch.no_grad()
-    def register_request(self, sid: int, images: Sequence) -> int:
+    def image_start(self, prompt_ids: Optional[Sequence[int]]) -> int:
+        """Position of the first <|image|> token: text before it attends to no image (HF Mllama's
+        ``full_text_row_masked_out_mask``: those rows get neither the cross-attention nor the cross layer's MLP
+        output). A prompt without the token attends from position 0."""
+        if prompt_ids is None:
+            return 0
+        for i, t in enumerate(prompt_ids):
+            if t == self.mcfg.image_token_id:
+                return i
+        return 0
+
+    def register_request(self, sid: int, images: Sequence, prompt_ids: Optional[Sequence[int]] = None) -> int:
         """Encode the request's image(s) and write the cross K/V of every cross layer. Returns #tokens.
         ``images`` holds raw images / :class:`ImageInput` or already-encoded cross states [n, hidden]
         (``encode_images`` batches many requests' images through one vision forward)."""
         if not images:
             return 0
         cc, c, w = self._ensure_cross(), self.cfg, self.w
+        self.img_start[sid] = self.image_start(prompt_ids)
         if all(isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[1] == c.hidden_size for x in images):
             states = torch.cat(list(images))  # cross states already encoded (batched by the caller)
         else:
@@ -479,6 +569,7 @@ class MllamaModel(LlamaModel):
         return n
 
     def release_request(self, sid: int):
+        self.img_start.pop(sid, None)
         if self.cross is not None:
             self.cross.release(sid)
 
@@ -502,14 +593,16 @@ class MllamaModel(LlamaModel):
             fb.extra = None  # text-only step: cross layers are skipped
             return
         bt, lens, has = self._cross_rows(fb.seq_ids)
-        rows = []
+        # per token: -1 = no image (masked), else the position its image starts at (masked before it)
+        starts = []
         for i, n in enumerate(fb.prefill_qlen):
-            rows += [bool(has[i])] * n
-        rows += [bool(x) for x in has[len(fb.prefill_qlen):]]
+            starts += [self.img_start.get(fb.seq_ids[i], 0) if has[i] else -1] * n
+        starts += [0 if x else -1 for x in has[len(fb.prefill_qlen):]]  # decode rows are past their prompt
         d = self.device
+        st = torch.tensor(starts, dtype=torch.int32).to(d, non_blocking=True)
+        row_mask = ((st >= 0) & (fb.positions >= st)).to(self.dtype).view(-1, 1)
         fb.extra = dict(cross_bt=bt.to(d, non_blocking=True), cross_len=lens.to(d, non_blocking=True),
-                        row_mask=torch.tensor(rows, dtype=self.dtype).view(-1, 1).to(d, non_blocking=True),
-                        max_cross=int(lens.max()), num_prefill_seqs=len(fb.prefill_qlen))
+                        row_mask=row_mask, max_cross=int(lens.max()), num_prefill_seqs=len(fb.prefill_qlen))
 
     def graph_static_inputs(self, bs: int) -> dict:
         self._ensure_cross()
@@ -607,18 +700,25 @@ class MllamaModel(LlamaModel):
         def rms(v, g):
             return v * torch.rsqrt(v.pow(2).mean(-1, keepdim=True) + c.rms_eps) * g
 
+        live = (torch.arange(T) >= self.image_start(ids.tolist())).float()[:, None]
         for i in range(c.num_layers):
             p = f"l{i}."
             if i in self.cross_set:
                 if states is None:
                     continue
+                x_in = x
                 hn = rms(x, wf[p + "attn_norm"])
                 q = rms((hn @ wf[p + "q"].t()).view(T, H, hd), wf[p + "q_norm"])
                 k = rms((states @ wf[p + "k"].t()).view(-1, Hkv, hd), wf[p + "k_norm"])
                 v = (states @ wf[p + "v"].t()).view(-1, Hkv, hd)
                 k, v = k.repeat_interleave(H // Hkv, 1), v.repeat_interleave(H // Hkv, 1)
                 a = F.scaled_dot_product_attention(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1))
-                x = x + a.transpose(0, 1).reshape(T, -1) @ wf[p + "o"].t()
+                x = x + live * (a.transpose(0, 1).reshape(T, -1) @ wf[p + "o"].t())
+                hn = rms(x, wf[p + "mlp_norm"])
+                y = ops.reference.linear(hn, wf[p + "gate_up"], act="swiglu", out_dtype=torch.float32)
+                x = x + live * (y @ wf[p + "down"].t())
+                assert torch.equal(x[live[:, 0] == 0], x_in[live[:, 0] == 0])
+                continue
             else:
                 hn = rms(x, wf[p + "attn_norm"])
                 qkv = hn @ wf[p + "qkv"].t()
@@ -636,17 +736,25 @@ class MllamaModel(LlamaModel):
         return x @ wf["lm_head"].t()
 
     def _reference_vision(self, im: ImageInput, wf) -> torch.Tensor:
+        """fp32 oracle in the reference's own layout: NT tiles x P8 tokens, mask(i, j) = valid_i or valid_j."""
         V, g = self.mcfg.vision, self.gates
         D, NT, TPT, P = V.hidden_size, V.max_num_tiles, V.tokens_per_tile, V.patch_size
-        n = im.num_tiles
+        P8 = (TPT + 7) // 8 * 8
+        n, ar = im.num_tiles, im.aspect_ratio_id
         px = im.pixels.float().cpu()
         x = (px - torch.tensor(MLLAMA_MEAN).view(1, 3, 1, 1)) / torch.tensor(MLLAMA_STD).view(1, 3, 1, 1)
         conv = wf["v.patch"][:, : 3 * P * P].reshape(D, 3, P, P)
-        pe = F.conv2d(x, conv, stride=P).flatten(2).transpose(1, 2)
-        pe = pe + g["pre_tile"] * wf["v.pre_tile"][im.aspect_ratio_id].view(NT, D)[:n, None]
-        h = torch.cat([wf["v.cls"].view(1, 1, D).expand(n, 1, D), pe], 1)
-        h = h + (1 - g["pos"]) * wf["v.pos"][None] + g["pos"] * wf["v.tile_pos"][im.aspect_ratio_id].view(NT, TPT, D)[:n]
-        h = F.layer_norm(h.reshape(1, n * TPT, D), (D,), wf["v.ln_pre_w"], wf["v.ln_pre_b"], V.ln_eps)
+        pe = torch.zeros(NT, V.num_patches, D)
+        pe[:n] = F.conv2d(x, conv, stride=P).flatten(2).transpose(1, 2)
+        pe = pe + g["pre_tile"] * wf["v.pre_tile"][ar].view(NT, 1, D)
+        h = torch.cat([wf["v.cls"].view(1, 1, D).expand(NT, 1, D), pe], 1)
+        h = h + (1 - g["pos"]) * wf["v.pos"][None] + g["pos"] * wf["v.tile_pos"][ar].view(NT, TPT, D)
+        h = F.layer_norm(h, (D,), wf["v.ln_pre_w"], wf["v.ln_pre_b"], V.ln_eps)
+        h = F.pad(h, (0, 0, 0, P8 - TPT)).reshape(1, NT * P8, D)
+        valid = torch.zeros(NT, P8, dtype=torch.bool)
+        valid[:n, :TPT] = True
+        valid = valid.reshape(-1)
+        allowed = valid[:, None] | valid[None, :]
         H, hp, hd = V.num_heads, V.head_dim_padded, V.head_dim
 
         def layers(h, lo, hi, keep=()):
@@ -656,7 +764,7 @@ class MllamaModel(LlamaModel):
                 xx = F.layer_norm(h, (D,), wf[p + "ln1_w"], wf[p + "ln1_b"], V.ln_eps)
                 qkv = (xx @ wf[p + "qkv"].t()).view(1, -1, 3, H, hp)[..., :hd]
                 q, k, v = qkv.permute(2, 0, 3, 1, 4)
-                a = F.scaled_dot_product_attention(q, k, v)  # [1, H, N, hd]
+                a = F.scaled_dot_product_attention(q, k, v, attn_mask=allowed)  # [1, H, N, hd]
                 a = F.pad(a, (0, hp - hd)).transpose(1, 2).reshape(1, -1, H * hp)
                 h = h + a @ wf[p + "o"].t()
                 xx = F.layer_norm(h, (D,), wf[p + "ln2_w"], wf[p + "ln2_b"], V.ln_eps)
@@ -667,7 +775,7 @@ class MllamaModel(LlamaModel):
 
         h, kept = layers(h, 0, V.num_layers, set(V.intermediate_layers))
         h = F.layer_norm(h, (D,), wf["v.ln_post_w"], wf["v.ln_post_b"], V.ln_eps)
-        h = h.view(n, TPT, D) + g["post_tile"] * wf["v.post_tile"][im.aspect_ratio_id].view(NT, D)[:n, None]
-        h, _ = layers(h.reshape(1, n * TPT, D), V.num_layers, V.num_layers + V.num_global_layers)
-        feats = torch.cat([h] + kept, -1)[0]
+        h = h.view(NT, P8, D) + g["post_tile"] * wf["v.post_tile"][ar].view(NT, 1, D)
+        h, _ = layers(h.reshape(1, NT * P8, D), V.num_layers, V.num_layers + V.num_global_layers)
+        feats = torch.cat([h, torch.stack(kept, -1).flatten(-2)], -1)[0][valid]
         return feats @ wf["proj"].t() + wf["proj_b"]

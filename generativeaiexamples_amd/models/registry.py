@@ -74,6 +74,10 @@ def build_llm(preset: str = "llama3-8b", weights: Optional[str] = None, device=N
         arch = json.load(open(os.path.join(weights, "config.json"))).get("model_type", "llama")
         if arch == "opt":
             m = OPTModel(OPTConfig.from_hf(weights), device=device)
+        elif arch == "mixtral":
+            m = MixtralModel(MixtralConfig.from_hf(weights), device=device)
+        elif arch == "mllama":
+            m = MllamaModel(MllamaConfig.from_hf(weights), device=device)
         elif arch == "qwen3_next":
             m = Qwen3NextModel(Qwen3NextConfig.from_hf(weights), device=device)
         elif dtype is not None:
@@ -139,6 +143,11 @@ def _load_st(m, path):
 def build_encoder(preset: str = "e5-large-v2", weights: Optional[str] = None, device=None, seed: int = 0,
                   reranker: bool = False) -> Tuple[BertModel, Tokenizer, str]:
     if _is_hf_dir(weights):
+        import json
+        if json.load(open(os.path.join(weights, "config.json"))).get("model_type") == "clip":
+            m = ClipModel(ClipConfig.from_hf(weights), device=device)
+            _load_st(m, weights)
+            return m, load_tokenizer(weights, "clip", m.cfg.vocab_size), os.path.basename(weights.rstrip("/"))
         cfg = BertConfig.from_hf(weights)
         m = BertModel(cfg, device=device)
         _load_st(m, weights)
@@ -170,7 +179,8 @@ def build_reranker_service(preset: str = "nv-rerankqa-mistral-4b", weights: Opti
         import json
         arch = json.load(open(os.path.join(weights, "config.json"))).get("model_type", "bert")
         if arch in ("mistral", "llama"):
-            cfg = DecoderRerankerConfig.nv_rerankqa_mistral_4b()
+            cfg = DecoderRerankerConfig(**LlamaConfig.hf_fields(
+                json.load(open(os.path.join(weights, "config.json"))), os.path.basename(weights.rstrip("/"))))
             m = DecoderRerankerModel(cfg, device=device)
             _load_st(m, weights)
             return DecoderReranker(m, load_tokenizer(weights, "llama3", cfg.vocab_size)), os.path.basename(weights.rstrip("/"))

@@ -30,7 +30,7 @@ from pydantic import BaseModel, Field
 from starlette.concurrency import run_in_threadpool
 
 from ..engine.sampling import SamplingParams
-from ..engine.tokenizer import apply_chat_template
+from ..engine.tokenizer import apply_chat_template, image_token_of
 from ..utils.metrics import METRICS
 from .hub import ServiceHub
 
@@ -227,8 +227,10 @@ def _messages_for_template(req: ChatRequest) -> List[dict]:
     msgs = []
     for m in req.messages:
         content = m.content
-        if isinstance(content, list):
-            content = "".join(p.get("text", "") for p in content if p.get("type") in ("text", None))
+        if isinstance(content, list):  # text parts joined; image parts kept as markers for the image token
+            imgs = [{"type": "image"} for p in content if p.get("type") in ("image_url", "image")]
+            text = "".join(p.get("text", "") for p in content if p.get("type") in ("text", None))
+            content = imgs + [{"type": "text", "text": text}] if imgs else text
         if m.role == "tool":
             msgs.append({"role": "ipython", "content": content or ""})
         elif m.tool_calls:
@@ -307,7 +309,7 @@ def create_openai_app(hub: ServiceHub) -> FastAPI:
         if req.n != 1:
             return _err(400, "only n=1 is supported")
         tok = llm.tokenizer
-        ids = apply_chat_template(_messages_for_template(req), tok)
+        ids = apply_chat_template(_messages_for_template(req), tok, image_token_id=image_token_of(llm.engine.model))
         params = _params(req, hub.default_max_tokens)
         try:
             params.guided = guide_for(req, tok)

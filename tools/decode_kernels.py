@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--ctx", type=int, default=2600)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-psw", action="store_true", help="plain-layout decode weights (no fragment copies)")
     a = ap.parse_args()
     m, tok, name = build_llm(a.model, device="cuda")
@@ -45,8 +45,23 @@ def main():
         for _ in range(a.iters):
             m.forward(fb, kv, ws)
         torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.iters
-    print(f"{name} decode B={B} ctx={a.ctx}: {1000 * dt:.3f} ms/forward (eager, includes launch overhead)")
+        dt = (time.perf_counter() - t0) / a.iters
+        print(f"{name} decode B={B} ctx={a.ctx}: {1000 * dt:.3f} ms/forward (eager, includes launch overhead)")
+        # the engine's path: the forward captured once, replayed (kernel boundaries only, no host launches)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            m.forward(fb, kv, ws)
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            g.replay()
+        torch.cuda.synchronize()
+        dg = (time.perf_counter() - t0) / a.iters
+        print(f"{name} decode B={B} ctx={a.ctx}: {1000 * dg:.3f} ms/forward (graph replay)")
 
 
 if __name__ == "__main__":
