@@ -104,12 +104,22 @@ class VectorStore:
                 for hs, (_, k, thr) in zip(hits, items)]
 
     @tracing.traced("retriever")
-    def similarity_search_with_relevance_scores(self, query: str, k: int = 4,
-                                                score_threshold: Optional[float] = None) -> List[Tuple[Document, float]]:
+    def similarity_search_with_relevance_scores(self, query: str, k: int = 4, score_threshold: Optional[float] = None,
+                                                filter: Optional[dict] = None) -> List[Tuple[Document, float]]:  # noqa: A002
+        """Top-k (document, relevance) for a query. ``filter`` (LangChain's metadata-equality dict) searches only
+        the matching rows inside the index - a partition scan for partition keys such as ``conversation`` - so a
+        filtered top-k is exact however large the rest of the collection is."""
         import time
 
         t0 = time.perf_counter()
-        hits = self.batcher.submit((query, k, score_threshold)).result()
+        if filter:
+            from ..utils.streams import on_retrieval_stream
+            with on_retrieval_stream(self.index.device):
+                q = self.emb.embed_tensor([query], "query")
+                hits = self.index.search(q.to(self.index.device), k, score_threshold, filter=filter)[0]
+            hits = [(h.document, h.score) for h in hits]
+        else:
+            hits = self.batcher.submit((query, k, score_threshold)).result()
         METRICS.search.observe(time.perf_counter() - t0)
         return hits
 

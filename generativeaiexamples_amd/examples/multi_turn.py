@@ -48,10 +48,14 @@ class MultiTurnRAG(BasicRAG):
         return self._ranker
 
     def _fetch(self, store, query, conv_id=None):
+        """k = 40 candidates when a ranker exists (else top_k), kept above ``retriever.score_threshold`` like the
+        reference's ``similarity_score_threshold`` retrievers (chains.py:147-167); memory is searched inside the
+        conversation's own partition of the index (exact top-k of that conversation, never crowded out)."""
         r = self.cfg.retriever
         k = CANDIDATES_WITH_RANKER if self.ranker else r.top_k
-        hits = store.similarity_search_with_relevance_scores(query, k * (4 if conv_id else 1), None)
-        docs = [d for d, s in hits if conv_id is None or d.metadata.get("conversation") == conv_id][:k]
+        hits = store.similarity_search_with_relevance_scores(
+            query, k, r.score_threshold, filter={"conversation": conv_id} if conv_id else None)
+        docs = [d for d, _ in hits][:k]
         if self.ranker and docs:
             docs = self.ranker.compress_documents(docs, query)
         else:

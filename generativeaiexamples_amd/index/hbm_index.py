@@ -29,6 +29,10 @@ import torch
 from .. import ops
 
 
+def _hashable(v):
+    return v if isinstance(v, (str, int, float, bool, type(None))) else json.dumps(v, sort_keys=True, default=str)
+
+
 @dataclass
 class Document:
     page_content: str
@@ -40,6 +44,9 @@ class SearchHit:
     row: int
     score: float          # relevance score (higher is better)
     document: Document
+
+
+PARTITION_KEYS = ("conversation",)
 
 
 class HBMIndex:
@@ -57,6 +64,11 @@ class HBMIndex:
         self.dead = 0
         self.lock = threading.RLock()
         self.wal = None
+        # metadata keys whose values partition the rows (a conversation's memory, a tenant): a filtered search on
+        # one of them scans only that partition's rows, so a small partition is never crowded out of a global
+        # top-k by the rest of the collection
+        self.partition_keys = set(PARTITION_KEYS)
+        self.parts: Dict[tuple, List[int]] = {}
 
     # ------------------------------------------------------------------ sizing
     def __len__(self) -> int:
@@ -102,11 +114,23 @@ class HBMIndex:
                 self.bias[self.n:self.n + k] = 0.0
             self.docs.extend(documents)
             self.n += k
+            self._index_parts(rows, documents)
             if self.wal:
                 for r, d in zip(rows, documents):
                     self.wal.write(json.dumps({"op": "add", "row": r, "doc": _doc_json(d)}) + "\n")
                 self.wal.flush()
         return rows
+
+    def _index_parts(self, rows: Sequence[int], documents: Sequence[Optional[Document]]):
+        for r, d in zip(rows, documents):
+            if d is None:
+                continue
+            for key in self.partition_keys & d.metadata.keys():
+                self.parts.setdefault((key, _hashable(d.metadata[key])), []).append(r)
+
+    def _rebuild_parts(self):
+        self.parts = {}
+        self._index_parts(range(self.n), self.docs[: self.n])
 
     def add_random(self, n: int, seed: int = 0, doc_fn=None, chunk: int = 1 << 20):
         """Bulk-insert n random unit vectors (synthetic corpora for benchmarks); docs lazily from doc_fn(row)."""
@@ -152,6 +176,8 @@ class HBMIndex:
                     self.wal.flush()
                 if self.dead * 4 > self.n and self.n > 1024:
                     self.compact()
+                else:
+                    self._rebuild_parts()
             return len(rows)
 
     def delete_filename(self, filename: str) -> int:
@@ -174,6 +200,7 @@ class HBMIndex:
             self.bias[self.n:] = float("-inf")
             self.docs = docs
             self.dead = 0
+            self._rebuild_parts()
 
     # ------------------------------------------------------------------ query
     def _relevance(self, raw: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
@@ -200,9 +227,39 @@ class HBMIndex:
         rel = self._relevance(raw, q)
         return rel, rows
 
-    def search(self, queries: torch.Tensor, k: int = 4, score_threshold: Optional[float] = None
-               ) -> List[List[SearchHit]]:
-        rel, rows = self.search_raw(queries, k)
+    def rows_where(self, filt: Dict[str, Any]) -> List[int]:
+        """Live rows whose document metadata equals every (key, value) of ``filt``: a partition lookup when one
+        key is a partition key, else a scan of the stored documents."""
+        with self.lock:
+            cand = None
+            for key, val in filt.items():
+                if key in self.partition_keys:
+                    cand = list(self.parts.get((key, _hashable(val)), []))
+                    break
+            if cand is None:
+                cand = range(self.n)
+            return [r for r in cand if r < len(self.docs) and self.docs[r] is not None
+                    and all(self.docs[r].metadata.get(k2) == v2 for k2, v2 in filt.items())]
+
+    def _search_rows(self, q: torch.Tensor, k: int, rows: List[int]):
+        """Exact top-k over a row subset (gathered to a contiguous slab, same scan kernel and bias)."""
+        if not rows:
+            z = torch.empty(q.shape[0], 0, device=self.device)
+            return z, z.long()
+        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        with self.lock:
+            sub, bias = self.vectors.index_select(0, idx).contiguous(), self.bias.index_select(0, idx).contiguous()
+        raw, loc = ops.sim_topk(q.to(self.dtype), sub, bias, len(rows), min(k, 64, len(rows)))
+        out = torch.where(loc >= 0, idx[loc.clamp_min(0)], torch.full_like(loc, -1))
+        return self._relevance(raw, q), out
+
+    def search(self, queries: torch.Tensor, k: int = 4, score_threshold: Optional[float] = None,
+               filter: Optional[Dict[str, Any]] = None) -> List[List[SearchHit]]:  # noqa: A002 - LangChain's name
+        if filter:
+            q = self._prep(queries if queries.ndim == 2 else queries[None])
+            rel, rows = self._search_rows(q, k, self.rows_where(filter))
+        else:
+            rel, rows = self.search_raw(queries, k)
         rel, rows = rel.cpu().tolist(), rows.cpu().tolist()
         out = []
         for rs, ids in zip(rel, rows):
@@ -263,6 +320,7 @@ class HBMIndex:
             idx.docs = [_doc_from_json(json.loads(line)) for line in f]
         idx.n, idx.dead = n, meta.get("dead", 0)
         idx._replay_wal(path)
+        idx._rebuild_parts()
         return idx
 
     def _replay_wal(self, path: str):
