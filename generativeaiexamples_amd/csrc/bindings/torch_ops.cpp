@@ -531,6 +531,83 @@ void geglu_interleaved(const Tensor& x, Tensor& y) {
   gai_geglu_interleaved(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
 }
 
+void custom_all_to_all(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
+                       const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
+                       int64_t slot_bytes) {
+  check_dev(inp, "inp");
+  check_dev(out, "out");
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous(), "custom_all_to_all: contiguous tensors");
+  TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.numel() == out.numel(), "custom_all_to_all: in/out mismatch");
+  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= GAI_AR_MAX_BLOCKS, "custom_all_to_all: counters");
+  check_i32(err, "err");
+  const int world = (int)data_ptrs.size();
+  TORCH_CHECK(world >= 2 && world <= GAI_AR_MAX_WORLD && (int)sig_ptrs.size() == world, "custom_all_to_all: world");
+  TORCH_CHECK(rank >= 0 && rank < world, "custom_all_to_all: rank");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(bytes % world == 0, "custom_all_to_all: the input must split into equal segments");
+  void* d[GAI_AR_MAX_WORLD];
+  uint32_t* s[GAI_AR_MAX_WORLD];
+  for (int q = 0; q < world; ++q) {
+    d[q] = reinterpret_cast<void*>(data_ptrs[q]);
+    s[q] = reinterpret_cast<uint32_t*>(sig_ptrs[q]);
+  }
+  gai_custom_all_to_all(inp.data_ptr(), out.data_ptr(), bytes / world, d, s,
+                        reinterpret_cast<uint32_t*>(counters.data_ptr()), (int)rank, world, slot_bytes,
+                        err.data_ptr<int>(), cur_stream());
+}
+
+void ep_pack(const Tensor& x, const Tensor& ids, const Tensor& offs, const Tensor& a_pairs, int64_t W, int64_t C,
+             int64_t e_local, Tensor& send, const optional<Tensor>& send_eid) {
+  check_bf16(x, "x");
+  check_i32(ids, "ids");
+  check_i32(offs, "offs");
+  check_i32(a_pairs, "a_pairs");
+  check_bf16(send, "send");
+  TORCH_CHECK(ids.dim() == 2 && x.dim() == 2 && ids.size(0) == x.size(0), "ep_pack: ids [T, k] for x [T, D]");
+  TORCH_CHECK(offs.numel() == W + 1 && a_pairs.numel() == ids.numel(), "ep_pack: plan sizes");
+  TORCH_CHECK(send.dim() == 2 && send.is_contiguous() && send.size(0) == W * C && send.size(1) >= x.size(1),
+              "ep_pack: send slabs [W*C, ld >= D]");
+  int* eid = nullptr;
+  if (send_eid) {
+    check_i32(*send_eid, "send_eid");
+    TORCH_CHECK(send_eid->numel() == W * C, "ep_pack: send_eid [W*C]");
+    eid = send_eid->data_ptr<int>();
+  }
+  gai_ep_pack(x.data_ptr(), ids.data_ptr<int>(), offs.data_ptr<int>(), a_pairs.data_ptr<int>(), (int)W, (int)C,
+              (int)ids.size(1), (int)x.size(1), (int)send.size(1), (int)e_local, send.data_ptr(), eid, cur_stream());
+}
+
+void ep_combine(const Tensor& back, const Tensor& ids, const Tensor& pos, const Tensor& offs, const Tensor& w,
+                const optional<Tensor>& residual, int64_t e_local, int64_t C, Tensor& out) {
+  check_bf16(back, "back");
+  check_i32(ids, "ids");
+  check_i32(pos, "pos");
+  check_i32(offs, "offs");
+  check_f32(w, "w");
+  check_bf16(out, "out");
+  TORCH_CHECK(ids.dim() == 2 && pos.numel() == ids.numel() && w.numel() == ids.numel(), "ep_combine: plan sizes");
+  TORCH_CHECK(out.size(0) == ids.size(0) && out.size(1) == back.size(1), "ep_combine: out [T, D]");
+  gai_ep_combine(back.data_ptr(), ids.data_ptr<int>(), pos.data_ptr<int>(), offs.data_ptr<int>(), w.data_ptr<float>(),
+                 opt_ptr(residual), out.data_ptr(), (int)ids.size(0), (int)ids.size(1), (int)out.size(1),
+                 (int)e_local, (int)C, cur_stream());
+}
+
+void moe_dispatch_by(const Tensor& ids, int64_t E, int64_t div, Tensor& a_rows, Tensor& offs, Tensor& pos,
+                     Tensor& a_pairs) {
+  check_i32(ids, "expert ids");
+  check_i32(a_pairs, "a_pairs");
+  TORCH_CHECK(ids.is_contiguous() && a_rows.is_contiguous() && offs.is_contiguous() && pos.is_contiguous() &&
+              a_pairs.is_contiguous(), "moe_dispatch_by: tensors must be contiguous");
+  TORCH_CHECK(ids.dim() == 2 && div >= 1, "moe_dispatch_by: ids [T, k], divisor >= 1");
+  const int64_t n = ids.numel();
+  TORCH_CHECK(E >= 1 && E <= 2048, "moe_dispatch_by: 1 <= buckets <= 2048");
+  TORCH_CHECK(a_rows.numel() == n && pos.numel() == n && a_pairs.numel() == n && offs.numel() == E + 1,
+              "moe_dispatch_by: output sizes");
+  if (n == 0) return;
+  gai_moe_dispatch(ids.data_ptr<int>(), (int)n, (int)ids.size(1), (int)E, a_rows.data_ptr<int>(),
+                   offs.data_ptr<int>(), pos.data_ptr<int>(), cur_stream(), (int)div, a_pairs.data_ptr<int>());
+}
+
 void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
                       const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
                       int64_t slot_bytes) {
@@ -681,6 +758,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("moe_dispatch", &moe_dispatch);
+  m.def("moe_dispatch_by", &moe_dispatch_by);
+  m.def("ep_pack", &ep_pack);
+  m.def("ep_combine", &ep_combine);
+  m.def("custom_all_to_all", &custom_all_to_all);
   m.def("embedding", &embedding);
   m.def("decode_advance", &decode_advance);
   m.def("pool", &pool);

@@ -307,7 +307,90 @@ __global__ __launch_bounds__(kArThreads) void ar_twoshot_kernel(const uint4* in,
   if (tid == 0) counters[b] = e;
 }
 
+
+// One-shot all-to-all on the same buffers (expert-parallel token exchange, parallel/ep.py): the input is W
+// equal segments, segment q bound for rank q. Block b owns chunk b of every segment: it pushes chunk b of
+// segment q into slot `rank` of peer q's data area (direct xGMI writes, all peers at once), signals every
+// peer with the block's epoch, waits for all of them, then copies chunk b of every local slot q into output
+// segment q. Epochs, parities and the bounded wait are the one-shot all-reduce's (shared counters and
+// signals: every rank issues the same sequence of collectives), so it replays from a HIP graph too.
+template <int W>
+__global__ __launch_bounds__(kArThreads) void a2a_oneshot_kernel(const uint4* in, uint4* out, ArPtrs p,
+                                                                 uint32_t* __restrict__ counters, int rank,
+                                                                 int64_t seg16, int64_t slot_bytes, int* err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t e_sh;
+  if (tid == 0) e_sh = counters[b] + 1u;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int par = (int)(e & 1u);
+  constexpr int64_t kVec = GAI_AR_CHUNK / 16;
+  const int64_t v0 = (int64_t)b * kVec, v1 = min(v0 + kVec, seg16);
+  const int64_t my_off = ((int64_t)par * W + rank) * slot_bytes;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    uint4* dst = reinterpret_cast<uint4*>(p.data[q] + my_off);
+    const uint4* src = in + (int64_t)q * seg16;
+    for (int64_t v = v0 + tid; v < v1; v += kArThreads) dst[v] = src[v];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (tid < W) __hip_atomic_store(p.sig[tid] + b * GAI_AR_MAX_WORLD + rank, e, __ATOMIC_RELEASE,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) {
+    uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > p.spin_limit) {
+        atomicOr(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const char* base = p.data[rank] + (int64_t)par * W * slot_bytes;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const uint4* src = reinterpret_cast<const uint4*>(base + q * slot_bytes);
+    uint4* dst = out + (int64_t)q * seg16;
+    for (int64_t v = v0 + tid; v < v1; v += kArThreads) dst[v] = src[v];
+  }
+  if (tid == 0) counters[b] = e;
+}
+
 }  // namespace
+
+void gai_custom_all_to_all(const void* in, void* out, int64_t seg_bytes, void* const* peer_data,
+                           uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
+                           int* err, hipStream_t st) {
+  if (seg_bytes == 0) return;
+  if (seg_bytes % 16 || seg_bytes > slot_bytes) gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: segment size");
+  const int64_t nblk = (seg_bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
+  if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: segment too large");
+  ArPtrs p{};
+  p.spin_limit = ar_spin_limit();
+  for (int q = 0; q < world; ++q) {
+    p.data[q] = static_cast<char*>(peer_data[q]);
+    p.sig[q] = peer_sig[q];
+  }
+#define GAI_A2A(WW)                                                                                             \
+  if (world == WW) {                                                                                            \
+    a2a_oneshot_kernel<WW><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p, counters, rank,  \
+                                                             seg_bytes / 16, slot_bytes, err);                  \
+    GAI_LAUNCH_CHECK();                                                                                         \
+    return;                                                                                                     \
+  }
+  GAI_A2A(2)
+  GAI_A2A(4)
+  GAI_A2A(8)
+  GAI_A2A(3)
+  GAI_A2A(5)
+  GAI_A2A(6)
+  GAI_A2A(7)
+#undef GAI_A2A
+  gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: world size must be 2..8");
+}
 
 void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
                           uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,

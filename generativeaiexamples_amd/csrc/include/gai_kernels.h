@@ -92,7 +92,13 @@ void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N
                   int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st);
 
 // moe.hip
-void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st);
+void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st,
+                      int div = 1, int* a_pairs = nullptr);
+// expert parallelism (moe.hip): fixed-capacity send slabs and the weighted combine of the returned slabs
+void gai_ep_pack(const void* x, const int* ids, const int* offs, const int* a_pairs, int W, int C, int k, int D,
+                 int ld, int e_local, void* send, int* send_eid, hipStream_t st);
+void gai_ep_combine(const void* back, const int* ids, const int* pos, const int* offs, const float* w,
+                    const void* residual, void* out, int T, int k, int D, int e_local, int C, hipStream_t st);
 // gemm_decode.hip: decode-sized grouped GEMM on the weight-streaming decode kernel (0 = shape not handled)
 int gai_moe_gemm_dec2(const void* A, const int* a_rows, const void* W, void* C, const int* offs, int E,
                       int rows_total, int N, int K, int swiglu, hipStream_t st);
@@ -127,6 +133,10 @@ void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, voi
                           uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
                           int* err, hipStream_t st);
 // two-shot (reduce-scatter + all-gather) over its own buffers: region_bytes per (parity, src, region)
+// one-shot all-to-all of W equal segments over the one-shot all-reduce's buffers / signals
+void gai_custom_all_to_all(const void* in, void* out, int64_t seg_bytes, void* const* peer_data,
+                           uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
+                           int* err, hipStream_t st);
 void gai_custom_allreduce_twoshot(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
                                   uint32_t* const* peer_sig, uint32_t* counters, int rank, int world,
                                   int64_t region_bytes, int* err, hipStream_t st);

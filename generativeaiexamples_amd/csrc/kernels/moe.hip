@@ -205,16 +205,18 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict
 // = expert cursor + rows of the same expert in earlier waves of the chunk + earlier lanes of its own wave
 // (wave ballot per distinct expert), so rows of one expert keep their (token, slot) order like the stable
 // argsort. Out-of-range ids are clamped so every output stays defined (moe_route never produces them).
+// div > 1 buckets id / div instead of id (expert parallelism: the destination rank of a global expert id);
+// a_pairs (optional) receives the flat pair index i of every sorted row next to its token i / k.
 __global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict__ ids, int n, int k, int E,
                                                            int* __restrict__ a_rows, int* __restrict__ offs,
-                                                           int* __restrict__ pos) {
+                                                           int* __restrict__ pos, int div, int* __restrict__ a_pairs) {
   extern __shared__ int dsm[];  // cursor[E] | wave counts [4][E]
   int* cursor = dsm;
   int* wcnt = dsm + E;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int e = tid; e < E; e += 256) cursor[e] = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += 256) atomicAdd(&cursor[min(max(ids[i], 0), E - 1)], 1);
+  for (int i = tid; i < n; i += 256) atomicAdd(&cursor[min(max(ids[i] / div, 0), E - 1)], 1);
   __syncthreads();
   if (tid == 0) {
     int run = 0;
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict
     for (int x = tid; x < 4 * E; x += 256) wcnt[x] = 0;
     __syncthreads();  // cursors final (first chunk) / advanced; wave counts cleared
     const int i = base + tid;
-    const int e = i < n ? min(max(ids[i], 0), E - 1) : -1;
+    const int e = i < n ? min(max(ids[i] / div, 0), E - 1) : -1;
     unsigned long long rest = __ballot(e >= 0);
     int rank = 0;
     while (rest) {  // wave-uniform: one pass per distinct expert in the wave
@@ -246,6 +248,7 @@ __global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict
       int r = cursor[e] + rank;
       for (int w = 0; w < wid; ++w) r += wcnt[w * E + e];
       a_rows[r] = i / k;
+      if (a_pairs != nullptr) a_pairs[r] = i;
       pos[i] = r;
     }
     __syncthreads();
@@ -254,11 +257,94 @@ __global__ __launch_bounds__(256) void moe_dispatch_kernel(const int* __restrict
   }
 }
 
+// Expert-parallel send slab (decode, graph-capturable; parallel/ep.py dispatch_padded): W destination slabs
+// of C rows. Slab row s = dest * C + r holds the r-th pair bound for rank dest in (token, choice) order (the
+// moe_dispatch plan of the pairs bucketed by dest: offs / a_pairs), or padding past that rank's count: its
+// local expert id is then the sentinel e_local, which the receiver's grouped GEMM skips (its row is not read).
+// One wave per slab row, 16 B per lane. Rows are ld elements apart; with ld > D the local expert id is also
+// stored as an int32 in the row's tail (element D), so rows and ids cross the wire in ONE exchange.
+__global__ __launch_bounds__(256) void ep_pack_kernel(const bf16* __restrict__ x, const int* __restrict__ ids,
+                                                      const int* __restrict__ offs, const int* __restrict__ a_pairs,
+                                                      int rows, int C, int k, int D, int ld, int e_local,
+                                                      bf16* __restrict__ send, int* __restrict__ send_eid) {
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (s >= rows) return;
+  const int dest = s / C, j = offs[dest] + s % C;
+  const bool live = j < offs[dest + 1];
+  const int pair = live ? a_pairs[j] : 0;
+  const int eid = live ? ids[pair] - dest * e_local : e_local;
+  if (lane == 0) {
+    if (send_eid != nullptr) send_eid[s] = eid;
+    if (ld > D) *reinterpret_cast<int*>(send + (size_t)s * ld + D) = eid;
+  }
+  if (!live) return;
+  const bf16* src = x + (size_t)(pair / k) * D;
+  bf16* dst = send + (size_t)s * ld;
+  for (int c = lane * 8; c < D; c += 512) store8(dst + c, load8(src + c));
+}
+
+// Expert-parallel combine: out[t] = sum_j w[t, j] * back[slab row of pair (t, j)] (+ residual), the slab row
+// recomputed from the same plan (dest = id / e_local, r = pos - offs[dest]; pairs past the capacity C were
+// dropped and contribute nothing). fp32 accumulation in choice order, like moe_combine.
+__global__ __launch_bounds__(256) void ep_combine_kernel(const bf16* __restrict__ back, const int* __restrict__ ids,
+                                                         const int* __restrict__ pos, const int* __restrict__ offs,
+                                                         const float* __restrict__ w, const bf16* residual,
+                                                         bf16* __restrict__ out, int T, int k, int D, int e_local,
+                                                         int C) {
+  const int units = D / 8;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)T * units) return;
+  const int t = (int)(e / units), u = (int)(e % units);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const int i = t * k + j, dest = ids[i] / e_local, r = pos[i] - offs[dest];
+    if (r >= C) continue;
+    const float wj = w[i];
+    const bf16x8 y = load8(back + (size_t)(dest * C + r) * D + u * 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += wj * (float)y[q];
+  }
+  if (residual) {
+    const bf16x8 r = load8(residual + (size_t)t * D + u * 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += (float)r[q];
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (bf16)acc[q];
+  store8(out + (size_t)t * D + u * 8, o);
+}
+
 }  // namespace
 
-void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st) {
+void gai_ep_pack(const void* x, const int* ids, const int* offs, const int* a_pairs, int W, int C, int k, int D,
+                 int ld, int e_local, void* send, int* send_eid, hipStream_t st) {
+  if (D % 8 || ld % 8 || ld < D || (ld > D && ld < D + 2))
+    gai_launch_error(__FILE__, __LINE__, "ep_pack: D and the row stride must be multiples of 8 (stride D or >= D + 8)");
+  if (send_eid == nullptr && ld == D) gai_launch_error(__FILE__, __LINE__, "ep_pack: nowhere to store expert ids");
+  const int rows = W * C;
+  if (rows == 0) return;
+  ep_pack_kernel<<<(rows + 3) / 4, 256, 0, st>>>((const bf16*)x, ids, offs, a_pairs, rows, C, k, D, ld, e_local,
+                                                 (bf16*)send, send_eid);
+  GAI_LAUNCH_CHECK();
+}
+
+void gai_ep_combine(const void* back, const int* ids, const int* pos, const int* offs, const float* w,
+                    const void* residual, void* out, int T, int k, int D, int e_local, int C, hipStream_t st) {
+  if (T == 0) return;
+  if (D % 8) gai_launch_error(__FILE__, __LINE__, "ep_combine: hidden size must be a multiple of 8");
+  const long n = (long)T * (D / 8);
+  ep_combine_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const bf16*)back, ids, pos, offs, w,
+                                                                 (const bf16*)residual, (bf16*)out, T, k, D, e_local,
+                                                                 C);
+  GAI_LAUNCH_CHECK();
+}
+
+void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st,
+                      int div, int* a_pairs) {
   if (E < 1 || E > 2048) gai_launch_error(__FILE__, __LINE__, "moe_dispatch: 1 <= experts <= 2048");
-  moe_dispatch_kernel<<<1, 256, 5 * E * sizeof(int), st>>>(ids, n, k, E, a_rows, offs, pos);
+  if (div < 1) gai_launch_error(__FILE__, __LINE__, "moe_dispatch: bucket divisor >= 1");
+  moe_dispatch_kernel<<<1, 256, 5 * E * sizeof(int), st>>>(ids, n, k, E, a_rows, offs, pos, div, a_pairs);
   GAI_LAUNCH_CHECK();
 }
 

@@ -219,8 +219,14 @@ class LLMEngine:
         # small all-reduce per step agrees on the largest token count (the padded exchange's capacity) and
         # on whether anyone prefills; a rank with nothing scheduled runs a one-token dummy forward
         self.ep_group = getattr(model, "ep_group", None)
+        self._ep_bucket: Optional[int] = None  # EP lockstep: the graph bucket every rank replays this step
         if self.ep_group is not None:
-            cfg.use_graphs = False
+            import torch.distributed as dist
+            # single-step decode graphs when the step's exchanges are capturable: RCCL, or the peer-memory
+            # all-to-all (model.ep_xchg) over any control plane; every rank replays the bucket of the largest
+            # per-rank batch, so all ranks exchange slabs of one capacity
+            cfg.use_graphs = cfg.use_graphs and self.device.type == "cuda" and (
+                dist.get_backend(self.ep_group) == "nccl" or getattr(model, "ep_xchg", None) is not None)
             self.multi_graphs_ok = False
             cfg.decode_steps = 1
 
@@ -328,6 +334,16 @@ class LLMEngine:
         t = torch.tensor(vals, dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ep_group)
         return [int(v) for v in t.tolist()]
+
+    def _ep_idle_graph(self, t_max: int) -> None:
+        """A rank with nothing scheduled replays the step's bucket graph with every row padding (scratch page,
+        ctx 1): it joins the same captured all-to-alls as its busy peers."""
+        z = np.zeros(0, np.int32)
+        plan = dict(op="graph", n=0, arr=[z, z, z, z, np.zeros((0, 1), np.int32)], seq_ids=[])
+        self._bank()
+        self._run_graph(plan)
+        self.stager.fence()
+        self._step_done()
 
     def _ep_dummy_forward(self) -> None:
         """One decode row on the scratch page: keeps this rank in the step's all-to-alls."""
@@ -441,6 +457,8 @@ class LLMEngine:
             fb.extra = self.model.graph_static_inputs(bs)
         if getattr(self.model, "lora_names", None):
             fb.lora_slots = torch.zeros(bs, dtype=torch.int32, device=d)
+        if self.ep_group is not None:  # the bucket's exchange capacity is baked into its graph
+            self.model.ep_capacity_tokens, self.model.ep_exact = bs, False
         s = torch.cuda.Stream(device=d)
         s.wait_stream(torch.cuda.current_stream(d))
         with torch.cuda.stream(s):
@@ -683,7 +701,8 @@ class LLMEngine:
         """(plan, seq_order) of a one-token step: a captured decode graph when the batch is pure decode and
         fits a bucket, otherwise an eager (prefill / mixed) forward. Sampling parameters ride along."""
         P, nd = b.num_prefill_tokens, len(b.decode_seq_ids)
-        if P == 0 and self.device.type == "cuda" and self.cfg.use_graphs and self._graph_bucket(nd) is not None:
+        if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
+                and self._graph_bucket(max(nd, self._ep_bucket or 0)) is not None):
             seq_order = [int(x) for x in b.decode_seq_ids]
             plan = dict(op="graph", n=nd, arr=[b.token_ids, b.positions, b.slots, b.decode_ctx,
                                                 b.decode_block_tables], seq_ids=seq_order)
@@ -737,7 +756,7 @@ class LLMEngine:
 
     def _run_graph(self, plan: dict):
         n = plan["n"]
-        bs = self._graph_bucket(n)
+        bs = self._graph_bucket(max(n, self._ep_bucket or 0))
         if bs not in self.graphs:
             self._capture(bs)
         g, fb, logits = self.graphs[bs]
@@ -785,8 +804,14 @@ class LLMEngine:
             if t_max == 0:
                 return None
             self.model.ep_capacity_tokens, self.model.ep_exact = t_max, bool(any_prefill)
+            graphed = (not any_prefill and self.cfg.use_graphs and self.device.type == "cuda"
+                       and self._graph_bucket(t_max) is not None)
+            self._ep_bucket = t_max if graphed else None
             if n_tok == 0:
-                self._ep_dummy_forward()
+                if graphed:
+                    self._ep_idle_graph(t_max)
+                else:
+                    self._ep_dummy_forward()
                 return None
         if n_tok == 0:
             return None

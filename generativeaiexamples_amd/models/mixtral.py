@@ -77,6 +77,13 @@ class MixtralModel(LlamaModel):
         self.ep_capacity_tokens = 0   # EP lockstep: the step's largest per-rank token count (set by the engine)
         self.ep_exact = False         # EP lockstep: some rank prefills this step -> exact-count exchange
         super().__init__(cfg, device, dtype, dist_ctx)
+        # decode-time token exchange: the one-shot peer-memory all-to-all (direct xGMI writes, graph-capturable even
+        # over a gloo control plane); GAI_EP_A2A=rccl keeps RCCL's all_to_all_single
+        self.ep_xchg = None
+        if (ep_group is not None and self.ep_size > 1 and self.device.type == "cuda"
+                and os.environ.get("GAI_EP_A2A", "peer") != "rccl"):
+            from ..parallel.custom_ar import CustomAllReduce
+            self.ep_xchg = CustomAllReduce(group=ep_group, device=self.device)
 
     def _alloc(self):
         c = self.cfg
@@ -176,9 +183,10 @@ class MixtralModel(LlamaModel):
             out = ep.combine(y, wts, plan, group=self.ep_group)
         else:  # decode: fixed capacity agreed for this step, no host sync (graph-capturable)
             cap = max(self.ep_capacity_tokens, x.shape[0]) * c.top_k
-            rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group)
+            rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group,
+                                                 xchg=self.ep_xchg)
             y = ep.local_experts_padded(rows, eid, w13, w2)
-            out = ep.combine_padded(y, wts, plan, group=self.ep_group)
+            return ep.combine_padded(y, wts, plan, group=self.ep_group, xchg=self.ep_xchg, residual=residual)
         if residual is not None:
             out = out + residual
         return out

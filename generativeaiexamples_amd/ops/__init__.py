@@ -664,6 +664,51 @@ def moe_dispatch(ids: torch.Tensor, num_experts: int):
     return a_rows, offs, pos.view(T, k)
 
 
+def ep_dispatch_plan(ids: torch.Tensor, world: int, e_local: int):
+    """Expert-parallel send plan of the (token, choice) pairs: (offs [W+1], pos [T, k], a_pairs [T*k]) = the pairs
+    counting-sorted by destination rank id // e_local (moe_dispatch's kernel with a bucket divisor), sync-free."""
+    T, k = ids.shape
+    if ids.is_cuda and 0 < T * k <= _MOE_DISPATCH_MAX:
+        dev = ids.device
+        a_rows = torch.empty(T * k, dtype=torch.int32, device=dev)
+        a_pairs = torch.empty(T * k, dtype=torch.int32, device=dev)
+        offs = torch.empty(world + 1, dtype=torch.int32, device=dev)
+        pos = torch.empty(T, k, dtype=torch.int32, device=dev)
+        native().moe_dispatch_by(ids.to(torch.int32).contiguous(), world, e_local, a_rows, offs, pos, a_pairs)
+        return offs, pos, a_pairs
+    return ref.ep_dispatch_plan(ids, world, e_local)
+
+
+def ep_pack(x: torch.Tensor, ids: torch.Tensor, offs, a_pairs, world: int, capacity: int, e_local: int,
+            ids_in_rows: bool = False):
+    """-> (send slabs [W*C, D], local expert ids [W*C] int32; padding rows carry the sentinel e_local).
+    ids_in_rows: slabs are [W*C, D + 8] with each row's expert id stored as an int32 in its tail (one exchange
+    moves rows and ids); the second result is then None."""
+    if not x.is_cuda:
+        send, eid = ref.ep_pack(x, ids, offs, a_pairs, world, capacity, e_local)
+        if ids_in_rows:
+            tail = torch.zeros(send.shape[0], 8, dtype=send.dtype)
+            tail[:, :2] = eid.view(torch.bfloat16).view(-1, 2)
+            return torch.cat([send, tail], 1), None
+        return send, eid
+    D = x.shape[1]
+    send = torch.empty(world * capacity, D + 8 if ids_in_rows else D, dtype=x.dtype, device=x.device)
+    eid = None if ids_in_rows else torch.empty(world * capacity, dtype=torch.int32, device=x.device)
+    native().ep_pack(x.contiguous(), ids.to(torch.int32).contiguous(), offs, a_pairs, world, capacity, e_local, send,
+                     eid)
+    return send, eid
+
+
+def ep_combine(back, ids, pos, offs, w, residual, e_local: int, capacity: int):
+    """out[t] = sum_j w[t, j] * back[slab row of (t, j)] (+ residual): the returned expert outputs, weighted."""
+    if not back.is_cuda:
+        return ref.ep_combine(back, ids, pos, offs, w, residual, e_local, capacity)
+    out = torch.empty(ids.shape[0], back.shape[1], dtype=back.dtype, device=back.device)
+    native().ep_combine(back.contiguous(), ids.to(torch.int32).contiguous(), pos.contiguous(), offs,
+                        w.to(torch.float32).contiguous(), residual, e_local, capacity, out)
+    return out
+
+
 def moe_gemm(A, a_rows, W, offs, rows_total: int, swiglu: bool):
     """Grouped expert GEMM over expert-sorted rows (A rows gathered through a_rows when given)."""
     if not A.is_cuda:

@@ -281,6 +281,47 @@ def moe_combine(Y, pos, w, residual=None):
     return y.to(Y.dtype)
 
 
+def ep_dispatch_plan(ids, world, e_local):
+    """(offs [W+1], pos [T, k], a_pairs [T*k]): the pairs stably sorted by destination rank id // e_local."""
+    T, k = ids.shape
+    dest = (ids.reshape(-1).long() // e_local).clamp(0, world - 1)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world)
+    offs = torch.zeros(world + 1, dtype=torch.int32, device=ids.device)
+    offs[1:] = counts.cumsum(0).to(torch.int32)
+    pos = torch.empty(T * k, dtype=torch.int32, device=ids.device)
+    pos[order] = torch.arange(T * k, dtype=torch.int32, device=ids.device)
+    return offs, pos.view(T, k), order.to(torch.int32)
+
+
+def ep_pack(x, ids, offs, a_pairs, world, C, e_local):
+    """Send slabs [W*C, D] + local expert ids [W*C] (padding rows: sentinel e_local, zero rows)."""
+    k, D = ids.shape[1], x.shape[1]
+    send = torch.zeros(world * C, D, dtype=x.dtype, device=x.device)
+    eid = torch.full((world * C,), e_local, dtype=torch.int32, device=x.device)
+    o, flat = offs.tolist(), ids.reshape(-1).long()
+    for d in range(world):
+        n = min(o[d + 1] - o[d], C)
+        if n > 0:
+            pairs = a_pairs[o[d]:o[d] + n].long()
+            send[d * C:d * C + n] = x[pairs // k]
+            eid[d * C:d * C + n] = (flat[pairs] - d * e_local).to(torch.int32)
+    return send, eid
+
+
+def ep_combine(back, ids, pos, offs, w, residual, e_local, C):
+    T, k = ids.shape
+    flat = ids.reshape(-1).long()
+    dest = flat // e_local
+    r = pos.reshape(-1).long() - offs.long()[dest]
+    keep = r < C
+    rows = back[(dest * C + r.clamp(max=C - 1))].float() * (w.reshape(-1).float() * keep.float())[:, None]
+    y = rows.view(T, k, -1).sum(1)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(back.dtype)
+
+
 def embedding(ids, table, vstart=0, vend=None):
     vend = table.shape[0] + vstart if vend is None else vend
     ids = ids.long()

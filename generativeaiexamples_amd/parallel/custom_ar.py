@@ -127,6 +127,20 @@ class CustomAllReduce:
                                        self.max_bytes)
         return out
 
+    def eligible_a2a(self, t: torch.Tensor) -> bool:
+        """Equal-split all-to-all of ``t`` (dim 0 split into world segments) fits the one-shot buffers."""
+        nbytes = t.numel() * t.element_size()
+        return (not self._closed and t.is_cuda and t.is_contiguous() and nbytes % (16 * self.world) == 0
+                and 0 < nbytes // self.world <= self.max_bytes)
+
+    def all_to_all(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Segment q of ``t`` (dim 0 in world equal parts) goes to rank q; segment q of the result came from rank
+        q. Direct peer writes, one hop, graph-capturable (csrc/comm/custom_ar.hip a2a_oneshot_kernel)."""
+        out = torch.empty_like(t) if out is None else out
+        _native().custom_all_to_all(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
+                                    self.max_bytes)
+        return out
+
     def eligible_rmsnorm(self, t: torch.Tensor) -> bool:
         D = t.shape[-1]
         return (self.eligible(t) and t.dtype == torch.bfloat16 and D % 2048 == 0 and 16384 % (2 * D) == 0)

@@ -106,15 +106,12 @@ def local_experts(rows: torch.Tensor, eid: torch.Tensor, w13: torch.Tensor, w2: 
     return y
 
 
-@dataclass
-class EPPaddedPlan:
-    slot: torch.Tensor  # [T*k] slab row of every (token, choice) pair on the send side
-    capacity: int
-    num_tokens: int
-    top_k: int
-
-
-def _a2a_equal(x: torch.Tensor, group) -> torch.Tensor:
+def _a2a_equal(x: torch.Tensor, group, xchg=None) -> torch.Tensor:
+    """Equal-split all-to-all: the peer-memory one-shot kernel when the group has one (``xchg``, a
+    CustomAllReduce of the EP group: direct xGMI writes, one hop, capturable even over a gloo control plane),
+    else RCCL's ``all_to_all_single`` (gloo on CPU)."""
+    if xchg is not None and xchg.eligible_a2a(x):
+        return xchg.all_to_all(x.contiguous())
     if _host_plane(x, group):
         return _a2a_equal(x.cpu(), group).to(x.device)
     out = torch.empty_like(x)
@@ -126,27 +123,39 @@ def _a2a_equal(x: torch.Tensor, group) -> torch.Tensor:
     return o32.to(x.dtype)
 
 
-def dispatch_padded(x: torch.Tensor, ids: torch.Tensor, num_experts: int, capacity: int | None = None, group=None):
+@dataclass
+class EPPaddedPlan:
+    ids: torch.Tensor   # [T, k] global expert ids of the pairs
+    pos: torch.Tensor   # [T, k] rank of each pair in its destination's (token, choice)-ordered run
+    offs: torch.Tensor  # [W + 1] start of every destination's run
+    capacity: int
+    e_local: int
+
+
+def dispatch_padded(x: torch.Tensor, ids: torch.Tensor, num_experts: int, capacity: int | None = None, group=None,
+                    xchg=None):
     """-> (rows [W*C, D], local expert ids [W*C] int32 (e_local = padding), plan). Sync-free, capturable.
-    Pairs beyond ``capacity`` for one destination are dropped (capacity = T*k never drops)."""
+    Pairs beyond ``capacity`` for one destination are dropped (capacity = T*k never drops). The plan is one
+    counting-sort kernel over the destinations (ops.ep_dispatch_plan) and the slabs one gather kernel
+    (ops.ep_pack); the rows and their expert ids travel in ONE exchange (ids packed as two bf16 lanes)."""
+    from .. import ops
+
     world = dist.get_world_size(group)
     e_local = num_experts // world
     T, k = ids.shape
-    P = T * k
-    C = P if capacity is None else capacity
-    flat = ids.reshape(-1).long()
-    dest = flat // e_local
-    onehot = torch.zeros(P, world, dtype=torch.int32, device=x.device).scatter_(1, dest[:, None], 1)
-    pos = (onehot.cumsum(0) * onehot).sum(1) - 1            # rank of the pair inside its destination slab
-    keep = pos < C
-    slot = torch.where(keep, dest * C + pos, torch.full_like(pos, world * C))  # dropped -> scratch row
-    send = torch.zeros(world * C + 1, x.shape[1], dtype=x.dtype, device=x.device)
-    send[slot] = x[torch.arange(P, device=x.device) // k]
-    send_eid = torch.full((world * C + 1,), e_local, dtype=torch.int32, device=x.device)
-    send_eid[slot] = (flat % e_local).to(torch.int32)
-    rows = _a2a_equal(send[:-1], group)
-    eid = _a2a_equal(send_eid[:-1], group)
-    return rows, eid, EPPaddedPlan(slot, C, T, k)
+    C = T * k if capacity is None else capacity
+    offs, pos, a_pairs = ops.ep_dispatch_plan(ids, world, e_local)
+    if xchg is not None:  # one exchange: the expert id rides in each slab row's 16-B tail
+        D = x.shape[1]
+        slab, _ = ops.ep_pack(x, ids, offs, a_pairs, world, C, e_local, ids_in_rows=True)
+        got = _a2a_equal(slab, group, xchg)
+        rows = got[:, :D].contiguous()
+        eid = got[:, D:D + 2].contiguous().view(torch.int32).view(-1)
+    else:
+        send, send_eid = ops.ep_pack(x, ids, offs, a_pairs, world, C, e_local)
+        rows = _a2a_equal(send, group)
+        eid = _a2a_equal(send_eid, group)
+    return rows, eid, EPPaddedPlan(ids, pos, offs, C, e_local)
 
 
 def local_experts_padded(rows: torch.Tensor, eid: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
@@ -162,10 +171,11 @@ def local_experts_padded(rows: torch.Tensor, eid: torch.Tensor, w13: torch.Tenso
     return y_sorted[pos.view(-1).long()]
 
 
-def combine_padded(y: torch.Tensor, weights: torch.Tensor, plan: EPPaddedPlan, group=None) -> torch.Tensor:
-    back = _a2a_equal(y, group)
-    back = torch.cat([back, back.new_zeros(1, back.shape[1])])  # scratch row of dropped pairs
-    pair = back[plan.slot].float()
-    w = weights.reshape(-1, 1).to(torch.float32) * (plan.slot < back.shape[0] - 1).float()[:, None]
-    out = (pair * w).view(plan.num_tokens, plan.top_k, -1).sum(1)
-    return out.to(y.dtype)
+def combine_padded(y: torch.Tensor, weights: torch.Tensor, plan: EPPaddedPlan, group=None, xchg=None,
+                   residual: torch.Tensor | None = None) -> torch.Tensor:
+    """Return the expert outputs to their ranks and reduce them with the routing weights (+ residual) in one
+    kernel (ops.ep_combine); dropped pairs contribute nothing."""
+    from .. import ops
+
+    back = _a2a_equal(y.contiguous(), group, xchg)
+    return ops.ep_combine(back, plan.ids, plan.pos, plan.offs, weights, residual, plan.e_local, plan.capacity)

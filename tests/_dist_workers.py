@@ -371,6 +371,24 @@ def custom_ar_worker(rank, world, port, out_dir):
             e = (y.float().cpu() - want).abs().max().item()
             if not e < 3e-2 * want.abs().max().item():
                 errs.append(f"ar_rmsnorm D={D} T={T} err {e}")
+    # one-shot all-to-all (expert-parallel token exchange) on the same buffers, interleaved with all-reduces:
+    # segment q of rank r carries (r, q) tags; the result's segment q must be rank q's segment `rank`
+    for seg in (8, 4104, 128 * 4104, (4 << 20) // 2):  # bf16 elements per peer (4104 = Mixtral row + id tail)
+        if seg * 2 > car.max_bytes:
+            continue
+        x = torch.empty(world, seg, dtype=torch.bfloat16)
+        for q in range(world):
+            x[q] = float(rank * 16 + q) + torch.arange(seg, dtype=torch.float32) % 64 / 64
+        torch.cuda.synchronize()
+        dist.barrier()
+        y = car.all_to_all(x.to(dev))
+        car.all_reduce(torch.ones(1024, dtype=torch.float32, device=dev))
+        torch.cuda.synchronize()
+        y = y.cpu()
+        for q in range(world):
+            want = (float(q * 16 + rank) + torch.arange(seg, dtype=torch.float32) % 64 / 64).to(torch.bfloat16)
+            if not torch.equal(y[q], want):
+                errs.append(f"all_to_all seg={seg}: segment {q} wrong")
     # graph capture: three chained all-reduces on static buffers, replayed with new inputs
     n = 64 * 4096
     static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
@@ -661,7 +679,7 @@ def tp_linear_overlap_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def tp_graph_rehearsal_worker(rank, world, port, out_dir):
+def tp_graph_rehearsal_worker(rank, world, port, out_dir, shape="tiny"):
     """One-GPU rehearsal of a TP=world decode (every rank on cuda:0, gloo control plane): the multi-step
     decode graph holds only peer-memory collectives (custom all-reduce for the embedding / block-boundary
     reductions and ops.sample_tp's candidate exchange), is captured on every rank and replayed in lockstep
@@ -669,6 +687,13 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
     the same weights (bf16 TP partial sums may flip a near-tie, after which the sequences legitimately
     diverge, so token-by-token equality with a TP=1 engine is not the criterion)."""
     import json
+    import time as _time
+
+    t_start = _time.monotonic()
+
+    def progress(msg):  # per-rank timestamped progress (read by the test when a rank is late or hangs)
+        with open(os.path.join(out_dir, f"tpg_progress_{rank}.txt"), "a") as f:
+            f.write(f"{_time.monotonic() - t_start:8.3f}s {msg}\n")
 
     os.environ.update(GAI_SINGLE_DEVICE="1", GAI_CUSTOM_AR="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
@@ -681,30 +706,45 @@ def tp_graph_rehearsal_worker(rank, world, port, out_dir):
     from generativeaiexamples_amd.parallel import dist as gdist
 
     ctx = gdist.init_distributed(tp_size=world, backend="gloo")
+    progress(f"init pid {os.getpid()}")
     from generativeaiexamples_amd import ops
     from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
-    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.engine.tokenizer import llama3_byte_tokenizer, small_byte_tokenizer
     from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
     from generativeaiexamples_amd.parallel.dist import DistContext
 
     err = None
     try:
         assert ctx.custom_ar is not None, "custom all-reduce not created"
-        cfg = LlamaConfig.tiny(num_heads=8, num_kv_heads=8, head_dim=64, hidden_size=512, intermediate_size=1024,
-                               vocab_size=4096)
+        if shape == "70b":  # Llama-3-70B layer widths (2 layers): real all-reduce message sizes, V / 8 sampler shards
+            import dataclasses
+            cfg = dataclasses.replace(LlamaConfig.llama3_70b(), num_layers=2, max_position=1024)
+        else:
+            cfg = LlamaConfig.tiny(num_heads=8, num_kv_heads=8, head_dim=64, hidden_size=512, intermediate_size=1024,
+                                   vocab_size=4096)
         ref = LlamaModel(cfg, device="cuda", dist_ctx=DistContext()).random_init(17)
         m = LlamaModel(cfg, device="cuda", dist_ctx=ctx).load_hf_state(ref.export_hf_state())
-        tok = small_byte_tokenizer(4096)
+        if rank != 0:
+            del ref  # only the leader checks tokens against the fp32 reference
+            torch.cuda.empty_cache()
+        tok = small_byte_tokenizer(cfg.vocab_size) if cfg.vocab_size <= 4096 else llama3_byte_tokenizer(cfg.vocab_size)
         ecfg = dict(num_blocks=128, max_model_len=256, use_graphs=True, decode_steps=4, max_num_seqs=8,
                     graph_batch_sizes=(4, 8), prefix_cache=False, kv_memory_fraction=0.02)
+        progress("model loaded")
         eng = LLMEngine(m, tok, EngineConfig(**ecfg))
         eng.capture_graphs(max_bs=8)
+        progress(f"graphs captured {sorted(eng.multi_graphs)}")
         if not eng.leader:
             assert eng.follow() == "stop"
+            progress("follower stopped")
         else:
             prompts = [list(range(11 + 3 * i, 11 + 3 * i + n)) for i, n in enumerate((9, 23, 40, 5, 17))]
             sp = SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
-            tp = eng.generate(prompts, sp)
+            tp = [eng.add_request(p_, sp) for p_ in prompts]
+            while eng.has_work():
+                eng.step()
+                progress(f"step {eng.stats['steps']} graph_steps {eng.stats['graph_steps']} "
+                         f"ar_err {int(ctx.custom_ar.err.item())}")
             stats = dict(eng.stats)
             eng.release_followers(stop=True)
             bad, total = [], 0
@@ -764,3 +804,86 @@ def ep_engine_worker(rank, world, port, out_dir):
         json.dump({"ep": ep, "ref": one, "e_local": m.e_local, "steps": eng.stats["steps"]}, f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def ep_gpu_rehearsal_worker(rank, world, port, out_dir):
+    """One-GPU rehearsal of Mixtral expert parallelism (VERDICT r3 "next" #4): ``world`` ranks share cuda:0 over a
+    gloo control plane; each owns 8 / world experts and serves its OWN requests (different counts and lengths:
+    idle ranks replay padding-only graphs). Prefill steps use the exact-count exchange, decode steps run as
+    captured HIP graphs whose token exchanges are the peer-memory one-shot all-to-all (native EP pack / combine
+    kernels around it). Every greedy token must be the fp32 reference argmax of its prefix up to a bf16 near-tie."""
+    import json
+    import time as _time
+
+    t_start = _time.monotonic()
+
+    def progress(msg):
+        with open(os.path.join(out_dir, f"ep_progress_{rank}.txt"), "a") as f:
+            f.write(f"{_time.monotonic() - t_start:8.3f}s {msg}\n")
+
+    os.environ.update(GAI_SINGLE_DEVICE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    os.environ["GPU_MAX_HW_QUEUES"] = "1"  # as the TP rehearsal: every rank's spin-waiting exchange resident at once
+    os.environ["GAI_AR_SPIN_LOG2"] = "29"
+    from generativeaiexamples_amd.parallel import dist as gdist
+
+    ctx = gdist.init_distributed(tp_size=1, backend="gloo")
+    progress(f"init pid {os.getpid()}")
+    import torch.distributed as dist
+
+    from generativeaiexamples_amd import ops
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.mixtral import MixtralConfig, MixtralModel
+    from generativeaiexamples_amd.parallel.dist import DistContext
+
+    err = None
+    try:
+        cfg = MixtralConfig.tiny_moe(num_experts=8, hidden_size=512, intermediate_size=512, num_heads=8,
+                                     num_kv_heads=4, head_dim=64, vocab_size=4096)
+        ref = MixtralModel(cfg, device="cuda", dist_ctx=DistContext()).random_init(3)
+        m = MixtralModel(cfg, device="cuda", dist_ctx=ctx, ep_group=dist.group.WORLD)
+        with torch.no_grad():
+            for k, t in m.w.items():
+                src = ref.w[k]
+                if k.endswith("w13") or k.endswith("w2"):
+                    src = src[m.e_start:m.e_start + m.e_local]
+                t.copy_(src)
+        assert m.ep_xchg is not None, "peer-memory all-to-all not created"
+        tok = small_byte_tokenizer(4096)
+        ecfg = dict(num_blocks=160, max_model_len=256, use_graphs=True, max_num_seqs=8, max_batched_tokens=64,
+                    prefill_chunk=32, prefix_cache=False, graph_batch_sizes=(1, 2, 4, 8), kv_memory_fraction=0.02)
+        eng = LLMEngine(m, tok, EngineConfig(**ecfg))
+        eng.capture_graphs(max_bs=8)
+        progress(f"graphs captured {sorted(eng.graphs)}")
+        n_req = 1 + 2 * rank  # ranks carry different loads: idle ranks replay padding-only graphs
+        prompts = [list(range(11 + 5 * rank + 3 * i, 11 + 5 * rank + 3 * i + 7 + 9 * ((i + rank) % 3)))
+                   for i in range(n_req)]
+        sp = SamplingParams(temperature=0.0, max_tokens=6 + 4 * rank, ignore_eos=True)
+        reqs = [eng.add_request(p_, sp) for p_ in prompts]
+        while True:
+            busy = int(eng.has_work())
+            if not eng._ep_agree([busy])[0]:  # lockstep until every rank is done
+                break
+            eng.step()
+            progress(f"step {eng.stats['steps']} graph_steps {eng.stats['graph_steps']} err {int(m.ep_xchg.err.item())}")
+        bad, total = [], 0
+        for p_, r in zip(prompts, reqs):
+            lg = ref.reference_forward(torch.tensor(p_ + r.output_ids[:-1]))[len(p_) - 1:]
+            for i, t in enumerate(r.output_ids):
+                total += 1
+                row = lg[i]
+                if float(row[t]) < float(row.max()) - 0.02 * max(1.0, float(row.abs().max())):
+                    bad.append((i, t, int(row.argmax())))
+        with open(os.path.join(out_dir, f"epg_{rank}.json"), "w") as f:
+            json.dump({"bad": bad, "total": total, "stats": dict(eng.stats), "graphs": sorted(eng.graphs),
+                       "lens": [len(r.output_ids) for r in reqs], "err": int(m.ep_xchg.err.item())}, f)
+    except Exception:  # noqa: BLE001
+        import traceback
+        err = traceback.format_exc()
+        with open(os.path.join(out_dir, f"epg_err_{rank}.txt"), "w") as f:
+            f.write(err)
+    finally:
+        gdist.shutdown()
+    if err:
+        raise SystemExit(1)

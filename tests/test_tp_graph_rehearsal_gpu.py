@@ -25,30 +25,55 @@ def _port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_tp_decode_graph_one_gpu(tmp_path, world, cuda):
+@pytest.mark.parametrize("world,shape", [(2, "tiny"), (4, "tiny"), (8, "tiny"), (8, "70b")])
+def test_tp_decode_graph_one_gpu(tmp_path, world, shape, cuda):
     """world 8 runs only with GAI_REHEARSE_TP8=1: eight processes time-slicing one GPU's hardware queues reach
     each spin-waiting all-reduce seconds apart, so the case takes minutes on a shared box (it exceeded a 170 s
     deadline in a full-suite run with nothing printed meanwhile); on a real 8-GPU node every rank has its own GPU."""
     if world == 8 and os.environ.get("GAI_REHEARSE_TP8") != "1":
         pytest.skip("8 ranks on one GPU: set GAI_REHEARSE_TP8=1 (takes minutes)")
+    import threading
+
+    from tools.queue_census import census
+
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=W.tp_graph_rehearsal_worker, args=(r, world, port, str(tmp_path)))
+    procs = [ctx.Process(target=W.tp_graph_rehearsal_worker, args=(r, world, port, str(tmp_path), shape))
              for r in range(world)]
+    peak, stop = {"procs": 0, "queues": 0}, threading.Event()
+
+    def sample():  # processes / hardware queues the GPU's scheduler must map while the ranks run
+        while not stop.wait(0.5):
+            c = census()
+            if c["queues"] > peak["queues"] or c["procs"] > peak["procs"]:
+                peak.update(procs=max(peak["procs"], c["procs"]), queues=max(peak["queues"], c["queues"]),
+                            per_pid=c["per_pid"])
+
+    mon = threading.Thread(target=sample, daemon=True)
+    mon.start()
+    t0 = time.monotonic()
     for p in procs:
         p.start()
-    deadline = time.monotonic() + (540 if world == 8 else 170)
+    deadline = time.monotonic() + (300 if world == 8 else 170)
     for p in procs:
         p.join(max(1.0, deadline - time.monotonic()))
+    stop.set()
+    late = [p.is_alive() for p in procs]
     for p in procs:
         if p.is_alive():
             p.kill()
+    print(f"TP={world}: wall {time.monotonic() - t0:.1f}s, KFD census peak {peak}")
+    for r in range(world):
+        f = tmp_path / f"tpg_progress_{r}.txt"
+        lines = f.read_text().splitlines() if f.exists() else []
+        if any(late) or r == 0:
+            print(f"rank {r} progress ({len(lines)} lines): " + " | ".join(lines[:3] + (["..."] if len(lines) > 6 else [])
+                                                                       + lines[max(3, len(lines) - 3):]))
     errs = [f.read_text() for f in tmp_path.glob("tpg_err_*.txt")]
     assert not errs, errs[0]
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = json.loads((tmp_path / "tpg.json").read_text())
-    print(f"TP={world}: {res['total'] - len(res['bad'])}/{res['total']} tokens fp32-consistent, stats {res['stats']}, "
+    print(f"TP={world} ({shape}): {res['total'] - len(res['bad'])}/{res['total']} tokens fp32-consistent, stats {res['stats']}, "
           f"flags {res['flags']}")
     assert res["multi_graphs"], "no multi-step decode graph captured"
     assert res["stats"]["graph_steps"] > 0 and res["stats"]["chained_runs"] > 0
