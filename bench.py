@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--no-probes", action="store_true", help="skip the untimed c1 / open-loop TTFT probes")
     ap.add_argument("--probe-c1", type=int, default=4,
                     help="queries of the concurrency-1 probe (each runs its full max_tokens: TTFT and TPOT)")
+    ap.add_argument("--served-steps", type=int, default=3,
+                    help="after the timed in-process steps (config 2): this many POST /generate waves through the chain "
+                         "server, reported as the 'served' sub-object (0: skip)")
     ap.add_argument("--served", action="store_true",
                     help="drive the chain server instead of the engine: every query is a concurrent POST /generate "
                          "SSE stream (basic_rag example, in-process engines), TTFT measured at the client")
@@ -197,7 +200,8 @@ def main():
         from generativeaiexamples_amd.parallel.launch import spawn_ranks
 
         sys.exit(spawn_ranks(args.gpus))
-    if args.served:  # the HTTP clients run in their own process, spawned before this one touches the GPU
+    if (args.served or args.served_steps > 0) and args.config == 2:
+        # the HTTP clients run in their own process, spawned before this one touches the GPU
         from generativeaiexamples_amd.benchmarks import served_client
 
         served_client.start()
@@ -450,6 +454,23 @@ def main():
     }
     if phase1:
         out["engine_phase_ms_per_step"] = {k: round(v / max(1, args.steps), 1) for k, v in phase1.items()}
+    if args.served_steps > 0:
+        # after the timed in-process steps (untimed for the headline): the same workload through the product path,
+        # POST /generate SSE from a separate client process, TTFT at the client (BASELINE.md protocol)
+        import copy
+
+        from generativeaiexamples_amd.benchmarks.served import run_served
+
+        sargs = copy.copy(args)
+        sargs.steps, sargs.warmup = args.served_steps, 1
+        srv = run_served(sargs, ctx, dict(lcfg=lcfg, bcfg=bcfg, embedder=embedder, index=index, engine=engine,
+                                          plant=plant, unplant=unplant, metric=METRIC, baseline_qps=BASELINE_QPS))
+        out["served"] = {k: srv[k] for k in ("value", "p50_ttft_s", "p90_ttft_s", "ms_per_step", "steps", "warmup",
+                                             "ttft_split_p50_ms", "p50_ttft_c1_s", "tpot_c1_ms", "poisson")
+                         if k in srv}
+        out["served"]["path"] = "POST /generate SSE (chain server, basic_rag), client process, TTFT at the client"
+        out["served"]["vs_in_process"] = round(srv["value"] / qps, 4)
+        log(f"served: {out['served']}")
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.json_out:

@@ -28,7 +28,7 @@ def test_bench_torchrun_two_ranks_tiny():
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(n), "--steps", str(steps), "--warmup", "0", "--model", "tiny", "--embedder", "tiny",
            "--index-size", "1500", "--batch", str(batch), "--max-tokens", "6", "--chunk-tokens", "48",
-           "--no-probes", "--no-graphs"]
+           "--no-probes", "--no-graphs", "--served-steps", "1"]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=560)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -41,3 +41,6 @@ def test_bench_torchrun_two_ranks_tiny():
     assert out["scaling"] == "weak" and out["tokens_per_query"] == 6
     # value is the whole-job rate: n * batch * steps queries over the slowest rank's timed seconds
     assert abs(out["value"] - n * batch * steps / (out["ms_per_step"] * steps / 1000)) < 1e-3 * out["value"] + 1e-3
+    # the served pass (POST /generate SSE through each rank's chain server) rides along, outside the timed steps
+    sv = out["served"]
+    assert sv["value"] > 0 and sv["steps"] == 1 and sv["p50_ttft_s"] > 0 and "vs_in_process" in sv
