@@ -531,6 +531,55 @@ void geglu_interleaved(const Tensor& x, Tensor& y) {
   gai_geglu_interleaved(x.data_ptr(), y.data_ptr(), y.numel() / I, I, cur_stream());
 }
 
+void gemv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, int64_t epi,
+          const optional<Tensor>& out, const optional<Tensor>& res) {
+  check_bf16(x, "x");
+  check_bf16(W, "W");
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1) && x.is_contiguous() && W.is_contiguous(),
+              "gemv: x [M, K], W [N, K] contiguous");
+  const int M = x.size(0), N = W.size(0), K = W.size(1);
+  TORCH_CHECK(gai_gemv_ok(M, N, K, gamma.has_value()), "gemv: shape not supported");
+  if (gamma) {
+    check_bf16(*gamma, "gamma");
+    TORCH_CHECK(gamma->numel() == K, "gemv: gamma [K]");
+  }
+  void* o = nullptr;
+  void* r = nullptr;
+  if (epi == 1) {
+    TORCH_CHECK(res && res->scalar_type() == at::kBFloat16 && res->is_contiguous() && res->numel() == (int64_t)M * N,
+                "gemv: residual [M, N] bf16");
+    r = res->data_ptr();
+  } else {
+    TORCH_CHECK(out && out->is_contiguous(), "gemv: out");
+    const int64_t cols = epi == 2 ? N / 2 : N;
+    TORCH_CHECK(out->numel() == (int64_t)M * cols, "gemv: out size");
+    TORCH_CHECK(out->scalar_type() == (epi == 4 ? at::kFloat : at::kBFloat16), "gemv: out dtype");
+    o = out->data_ptr();
+  }
+  gai_gemv(x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), M, N, K, (int)epi, o, r,
+           cur_stream());
+}
+
+void gemv_rope_kv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, const Tensor& pos,
+                  const Tensor& cos_sin, const Tensor& slots, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
+                  int64_t Hq, int64_t Hkv) {
+  check_bf16(x, "x");
+  check_bf16(W, "W");
+  check_i32(pos, "pos");
+  check_i32(slots, "slots");
+  check_f32(cos_sin, "cos_sin");
+  check_bf16(q_out, "q_out");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(x.dim() == 2 && W.size(1) == x.size(1) && W.size(0) == (Hq + 2 * Hkv) * 128 && cos_sin.size(-1) == 128,
+              "gemv_rope_kv: head_dim 128, W [(Hq + 2 Hkv) * 128, K]");
+  TORCH_CHECK(pos.numel() == x.size(0) && slots.numel() == x.size(0), "gemv_rope_kv: pos / slots [M]");
+  if (gamma) check_bf16(*gamma, "gamma");
+  gai_gemv_rope_kv(x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), x.size(0), x.size(1),
+                   pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
+                   k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv, cur_stream());
+}
+
 void custom_all_to_all(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
                        const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
                        int64_t slot_bytes) {
@@ -762,6 +811,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ep_pack", &ep_pack);
   m.def("ep_combine", &ep_combine);
   m.def("custom_all_to_all", &custom_all_to_all);
+  m.def("gemv", &gemv);
+  m.def("gemv_rope_kv", &gemv_rope_kv);
   m.def("embedding", &embedding);
   m.def("decode_advance", &decode_advance);
   m.def("pool", &pool);

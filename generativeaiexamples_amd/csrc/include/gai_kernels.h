@@ -94,6 +94,13 @@ void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N
 // moe.hip
 void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* offs, int* pos, hipStream_t st,
                       int div = 1, int* a_pairs = nullptr);
+// gemv.hip: decode GEMV for 1..4 token rows with the RMSNorm staged in and the epilogue fused
+int gai_gemv_ok(int M, int N, int K, int normed);
+void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
+              void* res, hipStream_t st);
+void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W, int M, int K, const int* pos,
+                      const float* cos_sin, const int* slots, void* q_out, void* k_cache, void* v_cache, int Hq,
+                      int Hkv, hipStream_t st);
 // expert parallelism (moe.hip): fixed-capacity send slabs and the weighted combine of the returned slabs
 void gai_ep_pack(const void* x, const int* ids, const int* offs, const int* a_pairs, int W, int C, int k, int D,
                  int ld, int e_local, void* send, int* send_eid, hipStream_t st);

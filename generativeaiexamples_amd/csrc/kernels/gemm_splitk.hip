@@ -406,6 +406,32 @@ __device__ __forceinline__ void sum_slabs(const float* p, size_t stride, int KS,
   }
 }
 
+// The same sum with the slab count known at compile time (the decode tails: KS = 4 for down, 8 for QKV / O):
+// every slab load is issued before the first add - one memory round trip instead of KS / 4.
+template <int W, int KSC>
+__device__ __forceinline__ void sum_slabs_c(const float* p, size_t stride, float (&v)[W]) {
+  float x[KSC][W];
+#pragma unroll
+  for (int u = 0; u < KSC; ++u) {
+    const float* q = p + (size_t)u * stride;
+#pragma unroll
+    for (int c = 0; c < W; c += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(q + c);
+      x[u][c] = t.x; x[u][c + 1] = t.y; x[u][c + 2] = t.z; x[u][c + 3] = t.w;  // NOLINT
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < KSC; ++u)
+#pragma unroll
+    for (int c = 0; c < W; ++c) v[c] += x[u][c];
+}
+
+template <int W, int KSC>
+__device__ __forceinline__ void sum_slabs_any(const float* p, size_t stride, int KS, float (&v)[W]) {
+  if constexpr (KSC > 0) sum_slabs_c<W, KSC>(p, stride, v);
+  else sum_slabs<W>(p, stride, KS, v);
+}
+
 // Sum the KS partial slabs and apply the epilogue. One thread per output element.
 template <int EPI, bool OUTF32>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int KS, int M, int N,
@@ -649,6 +675,7 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(const float* __
 // The same tail with 1024 threads x 4 columns (N <= 4096): one workgroup per row is all the parallelism
 // a batch-64 decode step has, so the row's slab loads are spread over 4x the waves to keep more of them
 // in flight per CU.
+template <int KSC>
 __global__ __launch_bounds__(1024) void splitk_add_rmsnorm_w4_kernel(const float* __restrict__ part, int KS, int M,
                                                                      int N, const bf16* __restrict__ bias, bf16* res,
                                                                      const bf16* __restrict__ g, float eps,
@@ -661,7 +688,7 @@ __global__ __launch_bounds__(1024) void splitk_add_rmsnorm_w4_kernel(const float
   if (live) {
     rr = *reinterpret_cast<const bf16x4*>(res + (size_t)m * N + idx);
     gg = *reinterpret_cast<const bf16x4*>(g + idx);
-    sum_slabs<4>(part + (size_t)m * N + idx, (size_t)M * N, KS, v);
+    sum_slabs_any<4, KSC>(part + (size_t)m * N + idx, (size_t)M * N, KS, v);
   }
   float ss = 0.f;
   if (live) {
@@ -708,8 +735,11 @@ void gai_gemm_splitk_add_rmsnorm(const void* A, const void* B, const void* bias,
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
   if (!ks2) launch_partials(A, B, M, N, K, KS, ws, psw, st);
   if (N <= 4096 && N % 4 == 0 && getenv("GAI_NORM_TAIL_256") == nullptr) {
-    splitk_add_rmsnorm_w4_kernel<<<M, 1024, 0, st>>>(ws, KS, M, N, (const bf16*)bias, (bf16*)res, (const bf16*)g,
-                                                     eps, (bf16*)out);
+#define GAI_W4(KC)                                                                                              \
+    splitk_add_rmsnorm_w4_kernel<KC><<<M, 1024, 0, st>>>(ws, KS, M, N, (const bf16*)bias, (bf16*)res,          \
+                                                         (const bf16*)g, eps, (bf16*)out);
+    if (KS == 4) GAI_W4(4) else if (KS == 8) GAI_W4(8) else GAI_W4(0)
+#undef GAI_W4
     GAI_LAUNCH_CHECK();
     return;
   }
@@ -733,7 +763,7 @@ namespace {
 // Fused decode QKV tail: sum the KS partial slabs of the QKV projection (+ bias), round to bf16 exactly as
 // the unfused GEMM output, then RoPE + q store + paged K / V^T cache write (gai_rope.h) - replaces the
 // split-K reduce launch, the bf16 qkv round trip and the rope_kv launch. Thread mapping as rope_kv_kernel.
-template <int D, typename KV>
+template <int D, typename KV, int KSC>
 __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(const float* __restrict__ part, int KS, int M, int N,
                                                              const bf16* __restrict__ bias, const int* __restrict__ pos,
                                                              const float* __restrict__ cos_sin,
@@ -749,8 +779,8 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_kernel(const float* __rest
   const int i0 = (threadIdx.x % LPH) * 4;
   const int c1 = h * D + i0, c2 = c1 + D / 2;
   float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
-  sum_slabs<4>(part + (size_t)t * N + c1, (size_t)M * N, KS, a);
-  sum_slabs<4>(part + (size_t)t * N + c2, (size_t)M * N, KS, b);
+  sum_slabs_any<4, KSC>(part + (size_t)t * N + c1, (size_t)M * N, KS, a);
+  sum_slabs_any<4, KSC>(part + (size_t)t * N + c2, (size_t)M * N, KS, b);
   bf16x4 x1, x2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -832,13 +862,17 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
     constexpr int HPB = 256 / (DD / 8);                                                                           \
     const unsigned grid = (unsigned)((items + HPB - 1) / HPB);                                                    \
     if (kv_fp8)                                                                                                   \
-      splitk_rope_kv_kernel<DD, fp8><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin, slots,  \
-                                                           (bf16*)q_out, (fp8*)k_cache, (fp8*)v_cache, Hq, Hkv,     \
-                                                           iks, ivs);                                              \
+      splitk_rope_kv_kernel<DD, fp8, 0><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,      \
+                                                              slots, (bf16*)q_out, (fp8*)k_cache, (fp8*)v_cache,  \
+                                                              Hq, Hkv, iks, ivs);                                 \
+    else if (KS == 8)                                                                                             \
+      splitk_rope_kv_kernel<DD, bf16, 8><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,     \
+                                                               slots, (bf16*)q_out, (bf16*)k_cache,               \
+                                                               (bf16*)v_cache, Hq, Hkv, iks, ivs);                \
     else                                                                                                          \
-      splitk_rope_kv_kernel<DD, bf16><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin, slots, \
-                                                            (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv,  \
-                                                            iks, ivs);                                             \
+      splitk_rope_kv_kernel<DD, bf16, 0><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,     \
+                                                               slots, (bf16*)q_out, (bf16*)k_cache,               \
+                                                               (bf16*)v_cache, Hq, Hkv, iks, ivs);                \
     GAI_LAUNCH_CHECK();                                                                                           \
     return 1;                                                                                                     \
   }

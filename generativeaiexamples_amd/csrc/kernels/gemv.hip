@@ -1,0 +1,311 @@
+// Small-batch decode GEMV (M = 1..4 token rows): C[M, N] = A[M, K] . W[N, K]^T with the layer's neighbours fused.
+//
+// At batch 1 a decode layer is a pure weight stream (Llama-3-8B: 436 MB per layer, 16 KB of activations). The
+// MFMA decode kernels (gemm_splitk / gemm_decode) load 16 weight rows x 64 B per instruction and split K over
+// workgroups, so every projection also pays an fp32 partial-slab round trip and a tail launch (split-K reduce +
+// RoPE / residual add + RMSNorm): four tails per layer at batch 1, each latency-bound. Here:
+//  * a wave owns two weight rows and streams each as whole 1 KiB rows pieces (64 lanes x 16 B contiguous,
+//    non-temporal: read once), kG = 4 pieces per row in flight ahead of the arithmetic (v_dot2_f32_bf16);
+//  * the activation rows are staged ONCE per workgroup in LDS; with `gamma` the kernel stages the RMSNorm of the
+//    residual stream instead (sum of squares reduced in the workgroup, x_hat * gamma rounded to bf16 exactly as
+//    the norm kernel does) - the norm launch disappears, its input is the residual the previous projection's
+//    epilogue updated in place;
+//  * the wave's row pair is chosen so the epilogue has everything it needs: (2p, 2p+1) for plain / fp32 /
+//    residual outputs, the interleaved (gate, up) rows for SwiGLU, and the rotate-half partners (d, d + 64) of
+//    one head for RoPE + q / paged K / V^T stores - no split-K, no slabs, no tail launch.
+// A Llama decode layer at batch <= 4 is then five launches: QKV(+norm, +RoPE/KV) -> attention -> O(+residual)
+// -> gate_up(+norm, +SwiGLU) -> down(+residual).
+#include "gai_common.h"
+#include "gai_kernels.h"
+
+using namespace gai;
+
+namespace {
+
+constexpr int kGvWaves = 8;
+constexpr int kGvThreads = 64 * kGvWaves;
+constexpr int kPiece = 512;  // K elements of one wave load (64 lanes x 8 bf16)
+constexpr int kG = 4;        // pieces per row per pipeline group
+
+enum { GV_PLAIN = 0, GV_RESIDUAL = 1, GV_SWIGLU = 2, GV_ROPE = 3, GV_F32 = 4 };
+
+struct GemvArgs {
+  const bf16* x;      // [M, K] activations, or the residual stream to normalise when gamma != null
+  const bf16* gamma;  // RMSNorm weight [K] (null: x is used as is)
+  float eps;
+  const bf16* W;      // [N, K]
+  int M, N, K;
+  void* out;          // GV_PLAIN / GV_SWIGLU: bf16 [M, N or N / 2]; GV_F32: fp32 [M, N]
+  bf16* res;          // GV_RESIDUAL: [M, N], res = bf16(bf16(acc) + res) in place
+  const int* pos;     // GV_ROPE
+  const float* cos_sin;
+  const int* slots;
+  bf16* q_out;
+  bf16* k_cache;
+  bf16* v_cache;
+  int Hq, Hkv;
+};
+
+__device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    acc = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a[2 * i], a[2 * i + 1]}, bf16x2{b[2 * i], b[2 * i + 1]}, acc, false);
+  return acc;
+}
+
+template <int MR, int EPI>
+__global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
+  __shared__ float red[kGvWaves][MR];
+  __shared__ float inv_s[MR];
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int K = a.K, nch = K / 8;
+
+  // ---- stage the activation rows (normalised when gamma is given); the host keeps K <= 8192 for the norm form
+  if (a.gamma != nullptr) {
+    constexpr int kMaxC = 2;  // chunks per thread per row: K <= 2 * 8 * 512
+    bf16x8 v[MR][kMaxC];
+    float ss[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      ss[m] = 0.f;
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const int ch = c * kGvThreads + tid;
+        if (ch < nch) {
+          v[m][c] = load8(a.x + (size_t)m * K + 8 * ch);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss[m] += (float)v[m][c][e] * (float)v[m][c][e];
+        }
+      }
+      ss[m] = wave_sum(ss[m]);
+      if (lane == 0) red[wid][m] = ss[m];
+    }
+    __syncthreads();
+    if (tid < MR) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < kGvWaves; ++w) t += red[w][tid];
+      inv_s[tid] = rsqrtf(t / K + a.eps);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const float inv = inv_s[m];
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const int ch = c * kGvThreads + tid;
+        if (ch < nch) {
+          const bf16x8 g = load8(a.gamma + 8 * ch);
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[m][c][e] * inv * (float)g[e]);
+          *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * ch) = o;
+        }
+      }
+    }
+  } else {
+    for (int ch = tid; ch < MR * nch; ch += kGvThreads) {
+      const int m = ch / nch, c = ch % nch;
+      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * c) = load8(a.x + (size_t)m * K + 8 * c);
+    }
+  }
+  __syncthreads();
+
+  // ---- this wave's row pair
+  const int p = blockIdx.x * kGvWaves + wid;
+  const int npairs = a.N / 2;
+  if (p >= npairs) return;  // no barrier below
+  int r0, r1;
+  if (EPI == GV_SWIGLU) {  // rows interleaved per 16: [gate16 | up16]; output column p
+    r0 = 32 * (p >> 4) + (p & 15);
+    r1 = r0 + 16;
+  } else if (EPI == GV_ROPE) {  // head p / 64, rotate-half pair (i, i + 64)
+    r0 = 128 * (p >> 6) + (p & 63);
+    r1 = r0 + 64;
+  } else {
+    r0 = 2 * p;
+    r1 = r0 + 1;
+  }
+  const bf16* w0 = a.W + (size_t)r0 * K + 8 * lane;
+  const bf16* w1 = a.W + (size_t)r1 * K + 8 * lane;
+  const int ngroups = K / (kPiece * kG);  // host: K % 2048 == 0
+
+  float acc[MR][2];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = 0.f;
+  bf16x8 cur0[kG], cur1[kG], nxt0[kG], nxt1[kG];
+  auto load_group = [&](int g, bf16x8(&b0)[kG], bf16x8(&b1)[kG]) {
+#pragma unroll
+    for (int c = 0; c < kG; ++c) {
+      const int off = (g * kG + c) * kPiece;
+      b0[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + off));
+      b1[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + off));
+    }
+  };
+  auto compute_group = [&](int g, const bf16x8(&b0)[kG], const bf16x8(&b1)[kG]) {
+#pragma unroll
+    for (int c = 0; c < kG; ++c) {
+      const int k0 = (g * kG + c) * kPiece + 8 * lane;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
+        acc[m][0] = dot8(xv, b0[c], acc[m][0]);
+        acc[m][1] = dot8(xv, b1[c], acc[m][1]);
+      }
+    }
+  };
+  load_group(0, cur0, cur1);
+  int g = 0;
+  for (; g + 2 <= ngroups; g += 2) {
+    load_group(g + 1, nxt0, nxt1);
+    compute_group(g, cur0, cur1);
+    if (g + 2 < ngroups) load_group(g + 2, cur0, cur1);
+    compute_group(g + 1, nxt0, nxt1);
+  }
+  if (g < ngroups) compute_group(g, cur0, cur1);
+
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    acc[m][0] = wave_sum(acc[m][0]);
+    acc[m][1] = wave_sum(acc[m][1]);
+  }
+  if (lane >= MR) return;
+  // lane m finishes token row m
+  float v0 = acc[0][0], v1 = acc[0][1];
+#pragma unroll
+  for (int m = 1; m < MR; ++m)
+    if (lane == m) {
+      v0 = acc[m][0];
+      v1 = acc[m][1];
+    }
+  const int m = lane;
+  const int N = a.N;
+  if constexpr (EPI == GV_PLAIN) {
+    bf16* o = reinterpret_cast<bf16*>(a.out) + (size_t)m * N;
+    o[r0] = (bf16)v0;
+    o[r1] = (bf16)v1;
+  } else if constexpr (EPI == GV_F32) {
+    float* o = reinterpret_cast<float*>(a.out) + (size_t)m * N;
+    o[r0] = v0;
+    o[r1] = v1;
+  } else if constexpr (EPI == GV_RESIDUAL) {  // the rounding of the split-K add + norm tail: bf16(bf16(h) + r)
+    bf16* r = a.res + (size_t)m * N;
+    r[r0] = (bf16)((float)(bf16)v0 + (float)r[r0]);
+    r[r1] = (bf16)((float)(bf16)v1 + (float)r[r1]);
+  } else if constexpr (EPI == GV_SWIGLU) {
+    reinterpret_cast<bf16*>(a.out)[(size_t)m * (N / 2) + p] = (bf16)(silu(v0) * v1);
+  } else {  // GV_ROPE: x = bf16(qkv) as the unfused GEMM output, then rotate (neox halves), store
+    constexpr int D = 128, kBS = 16;
+    const int h = p >> 6, i = p & 63;
+    float x1 = (float)(bf16)v0, x2 = (float)(bf16)v1;
+    if (h < a.Hq + a.Hkv) {
+      const int ps = a.pos[m];
+      const float c = a.cos_sin[(size_t)ps * D + i], s = a.cos_sin[(size_t)ps * D + D / 2 + i];
+      const float y1 = x1 * c - x2 * s, y2 = x2 * c + x1 * s;
+      x1 = y1;
+      x2 = y2;
+    }
+    if (h < a.Hq) {
+      bf16* q = a.q_out + ((size_t)m * a.Hq + h) * D;
+      q[i] = (bf16)x1;
+      q[i + D / 2] = (bf16)x2;
+      return;
+    }
+    const int slot = a.slots[m];
+    if (slot < 0) return;
+    const int blk = slot / kBS, off = slot % kBS;
+    if (h < a.Hq + a.Hkv) {
+      bf16* kd = a.k_cache + (((size_t)blk * a.Hkv + (h - a.Hq)) * kBS + off) * D;
+      kd[i] = (bf16)x1;
+      kd[i + D / 2] = (bf16)x2;
+    } else {
+      bf16* vd = a.v_cache + ((size_t)blk * a.Hkv + (h - a.Hq - a.Hkv)) * D * kBS + off;
+      vd[(size_t)i * kBS] = (bf16)x1;
+      vd[(size_t)(i + D / 2) * kBS] = (bf16)x2;
+    }
+  }
+}
+
+template <int EPI>
+void gemv_launch(const GemvArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)a.M * a.K * sizeof(bf16);
+  const int grid = (a.N / 2 + kGvWaves - 1) / kGvWaves;
+#define GAI_GV(MRV)                                                                                           \
+  if (a.M == MRV) {                                                                                           \
+    static bool once = false;                                                                                 \
+    if (!once) {                                                                                              \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_kernel<MRV, EPI>),                              \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      once = true;                                                                                            \
+    }                                                                                                         \
+    gemv_kernel<MRV, EPI><<<grid, kGvThreads, lds, st>>>(a);                                                  \
+    GAI_LAUNCH_CHECK();                                                                                       \
+    return;                                                                                                   \
+  }
+  GAI_GV(1)
+  GAI_GV(2)
+  GAI_GV(3)
+  GAI_GV(4)
+#undef GAI_GV
+  gai_launch_error(__FILE__, __LINE__, "gemv: 1 <= M <= 4");
+}
+
+}  // namespace
+
+int gai_gemv_ok(int M, int N, int K, int normed) {
+  if (M < 1 || M > 4 || N % 2 || K % (kPiece * kG)) return 0;
+  if ((size_t)M * K * sizeof(bf16) > 160 * 1024) return 0;
+  if (normed && K > 2 * 8 * kGvThreads) return 0;
+  return 1;
+}
+
+// epi: 0 plain bf16, 1 residual in place (res), 2 SwiGLU on the [gate16 | up16] interleave, 4 fp32 out.
+void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
+              void* res, hipStream_t st) {
+  if (!gai_gemv_ok(M, N, K, gamma != nullptr)) gai_launch_error(__FILE__, __LINE__, "gemv: shape");
+  if (epi == GV_SWIGLU && N % 32) gai_launch_error(__FILE__, __LINE__, "gemv: SwiGLU needs N % 32 == 0");
+  GemvArgs a{};
+  a.x = (const bf16*)x;
+  a.gamma = (const bf16*)gamma;
+  a.eps = eps;
+  a.W = (const bf16*)W;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.out = out;
+  a.res = (bf16*)res;
+  switch (epi) {
+    case GV_PLAIN: gemv_launch<GV_PLAIN>(a, st); return;
+    case GV_RESIDUAL: gemv_launch<GV_RESIDUAL>(a, st); return;
+    case GV_SWIGLU: gemv_launch<GV_SWIGLU>(a, st); return;
+    case GV_F32: gemv_launch<GV_F32>(a, st); return;
+    default: gai_launch_error(__FILE__, __LINE__, "gemv: unknown epilogue");
+  }
+}
+
+// QKV projection + RoPE + q / paged K, V^T stores (head_dim 128, bf16 cache), normalised input when gamma.
+void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W, int M, int K, const int* pos,
+                      const float* cos_sin, const int* slots, void* q_out, void* k_cache, void* v_cache, int Hq,
+                      int Hkv, hipStream_t st) {
+  const int N = (Hq + 2 * Hkv) * 128;
+  if (!gai_gemv_ok(M, N, K, gamma != nullptr)) gai_launch_error(__FILE__, __LINE__, "gemv_rope_kv: shape");
+  GemvArgs a{};
+  a.x = (const bf16*)x;
+  a.gamma = (const bf16*)gamma;
+  a.eps = eps;
+  a.W = (const bf16*)W;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.pos = pos;
+  a.cos_sin = cos_sin;
+  a.slots = slots;
+  a.q_out = (bf16*)q_out;
+  a.k_cache = (bf16*)k_cache;
+  a.v_cache = (bf16*)v_cache;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  gemv_launch<GV_ROPE>(a, st);
+}

@@ -519,10 +519,52 @@ class LlamaModel:
             part = q3[:, sl].reshape(-1, hd)
             q3[:, sl] = ops.rms_norm(part, self.w[p + key], self.cfg.rms_eps).view(T, -1, hd)
 
+    def _gemv_ok(self, fb: ForwardBatch, kv) -> bool:
+        """Batch <= 4 pure decode on the small-batch GEMV path (gemv.hip): five launches per layer, the norms
+        staged into the consumer projections, no split-K slabs or tail kernels."""
+        c, w = self.cfg, self.w
+        T = fb.num_tokens
+        if not (fb.token_ids.is_cuda and fb.num_prefill_tokens == 0 and 1 <= T <= 4 and self.ctx.tp_size == 1):
+            return False
+        if (c.norm != "rms" or c.mlp != "swiglu" or c.qk_norm or c.head_dim != 128 or self.lora_names
+                or c.qkv_bias or c.o_bias or c.mlp_bias or os.environ.get("GAI_GEMV", "1") != "1"):
+            return False
+        if kv.layer(0)[0].dtype != torch.bfloat16 or not isinstance(w["l0.qkv"], torch.Tensor):
+            return False
+        D, I = c.hidden_size, self.inter
+        return (ops.gemv_ok(T, w["l0.qkv"].shape[0], D, True) and ops.gemv_ok(T, D, self.hq * c.head_dim)
+                and ops.gemv_ok(T, 2 * I, D, True) and ops.gemv_ok(T, D, I) and ops.gemv_ok(T, w["lm_head"].shape[0], D, True))
+
+    def _forward_gemv(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
+        c, w = self.cfg, self.w
+        T, hd = fb.num_tokens, c.head_dim
+        res = ops.embedding(fb.token_ids, w["embed"], self.vstart, self.vstart + self.vocab_local)
+        if c.embed_scale:
+            res.mul_(self.embed_multiplier)
+        q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
+        attn = torch.empty_like(q)
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            kc, vc = kv.layer(i)
+            ks, vs = kv.scales(i)
+            ops.gemv_rope_kv(res, w[p + "qkv"], w[p + "attn_norm"], c.rms_eps, fb.positions, self.cos_sin, fb.slots, q,
+                             kc, vc, self.hq, self.hkv)
+            ops.attention_decode(q, kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
+                                 max_ctx=fb.max_decode_ctx, out=attn, k_scale=ks, v_scale=vs)
+            ops.gemv(attn.view(T, -1), w[p + "o"], epi="residual", res=res)
+            g = ops.gemv(res, w[p + "gate_up"], gamma=w[p + "mlp_norm"], eps=c.rms_eps, epi="swiglu")
+            ops.gemv(g, w[p + "down"], epi="residual", res=res)
+        if fb.sample_rows is not None:
+            res = res.index_select(0, fb.sample_rows)
+        logits = ops.gemv(res, w["lm_head"], gamma=w["norm"], eps=c.rms_eps, epi="f32")
+        return logits[:, : c.vocab_size]
+
     def forward(self, fb: ForwardBatch, kv, decode_ws=None) -> torch.Tensor:
         """Returns fp32 logits [len(sample_rows), vocab] (gathered over TP)."""
         if self.ctx.tp_size > 1 and self.ctx.sequence_parallel and fb.num_prefill_tokens > 0:
             return self._forward_sp(fb, kv, decode_ws)
+        if self._gemv_ok(fb, kv):
+            return self._forward_gemv(fb, kv, decode_ws)
         c, w, ctx = self.cfg, self.w, self.ctx
         T, P = fb.num_tokens, fb.num_prefill_tokens
         hd = c.head_dim

@@ -664,6 +664,39 @@ def moe_dispatch(ids: torch.Tensor, num_experts: int):
     return a_rows, offs, pos.view(T, k)
 
 
+_GEMV_EPI = {"plain": 0, "residual": 1, "swiglu": 2, "f32": 4}
+
+
+def gemv_ok(M: int, N: int, K: int, normed: bool = False) -> bool:
+    """Shapes the small-batch decode GEMV (gemv.hip) takes: 1..4 rows, K a multiple of 2048, the staged activation
+    rows within LDS, K <= 8192 when it normalises its input."""
+    return (1 <= M <= 4 and N % 2 == 0 and K % 2048 == 0 and M * K * 2 <= 160 * 1024
+            and (not normed or K <= 8192))
+
+
+def gemv(x, W, gamma=None, eps: float = 1e-5, epi: str = "plain", res=None, out=None):
+    """Decode GEMV for 1..4 token rows with the consumer's RMSNorm staged in (``gamma``) and the epilogue fused:
+    plain bf16, ``residual`` (res = bf16(bf16(x W^T) + res) in place), ``swiglu`` on the [gate16 | up16]
+    interleave, ``f32`` logits."""
+    if not x.is_cuda:
+        return ref.gemv(x, W, gamma, eps, epi, res)
+    M, N = x.shape[0], W.shape[0]
+    if epi == "residual":
+        native().gemv(x.contiguous(), gamma, eps, W, 1, None, res)
+        return res
+    if out is None:
+        cols = N // 2 if epi == "swiglu" else N
+        out = torch.empty(M, cols, dtype=torch.float32 if epi == "f32" else x.dtype, device=x.device)
+    native().gemv(x.contiguous(), gamma, eps, W, _GEMV_EPI[epi], out, None)
+    return out
+
+
+def gemv_rope_kv(x, W, gamma, eps, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq: int, Hkv: int):
+    """QKV GEMV (+ the attention RMSNorm staged in) + RoPE + q / paged K, V^T stores: the batch <= 4 decode
+    counterpart of linear_rope_kv, no split-K slabs and no tail launch."""
+    native().gemv_rope_kv(x.contiguous(), gamma, eps, W, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv)
+
+
 def ep_dispatch_plan(ids: torch.Tensor, world: int, e_local: int):
     """Expert-parallel send plan of the (token, choice) pairs: (offs [W+1], pos [T, k], a_pairs [T*k]) = the pairs
     counting-sorted by destination rank id // e_local (moe_dispatch's kernel with a bucket divisor), sync-free."""

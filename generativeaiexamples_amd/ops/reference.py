@@ -281,6 +281,23 @@ def moe_combine(Y, pos, w, residual=None):
     return y.to(Y.dtype)
 
 
+def gemv(x, W, gamma=None, eps=1e-5, epi="plain", res=None):
+    """Small-batch decode GEMV oracle (gemv.hip): optional RMSNorm of x (rounded to bf16), fp32 product, epilogue."""
+    xf = x.float()
+    if gamma is not None:
+        xf = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(torch.bfloat16).float()
+    y = xf @ W.float().t()
+    if epi == "f32":
+        return y
+    if epi == "residual":
+        res.copy_((y.to(torch.bfloat16).float() + res.float()).to(res.dtype))
+        return res
+    if epi == "swiglu":
+        g = y.view(y.shape[0], -1, 2, 16)
+        return (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(y.shape[0], -1).to(torch.bfloat16)
+    return y.to(torch.bfloat16)
+
+
 def ep_dispatch_plan(ids, world, e_local):
     """(offs [W+1], pos [T, k], a_pairs [T*k]): the pairs stably sorted by destination rank id // e_local."""
     T, k = ids.shape
