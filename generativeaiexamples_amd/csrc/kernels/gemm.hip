@@ -24,7 +24,7 @@
 
 #include <utility>
 
-// every AGPR, for the asm-MFMA kernel (see gemm_w4_kernel)
+// every AGPR, for the asm-MFMA persistent kernels (w4p / w4d / w4r)
 #define GAI_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127","a128","a129","a130","a131","a132","a133","a134","a135","a136","a137","a138","a139","a140","a141","a142","a143","a144","a145","a146","a147","a148","a149","a150","a151","a152","a153","a154","a155","a156","a157","a158","a159","a160","a161","a162","a163","a164","a165","a166","a167","a168","a169","a170","a171","a172","a173","a174","a175","a176","a177","a178","a179","a180","a181","a182","a183","a184","a185","a186","a187","a188","a189","a190","a191","a192","a193","a194","a195","a196","a197","a198","a199","a200","a201","a202","a203","a204","a205","a206","a207","a208","a209","a210","a211","a212","a213","a214","a215","a216","a217","a218","a219","a220","a221","a222","a223","a224","a225","a226","a227","a228","a229","a230","a231","a232","a233","a234","a235","a236","a237","a238","a239","a240","a241","a242","a243","a244","a245","a246","a247","a248","a249","a250","a251","a252","a253","a254","a255"
 #define GAI_AGPR_ZERO "v_accvgpr_write_b32 a0, 0\n\t""v_accvgpr_write_b32 a1, 0\n\t""v_accvgpr_write_b32 a2, 0\n\t""v_accvgpr_write_b32 a3, 0\n\t""v_accvgpr_write_b32 a4, 0\n\t""v_accvgpr_write_b32 a5, 0\n\t""v_accvgpr_write_b32 a6, 0\n\t""v_accvgpr_write_b32 a7, 0\n\t""v_accvgpr_write_b32 a8, 0\n\t""v_accvgpr_write_b32 a9, 0\n\t""v_accvgpr_write_b32 a10, 0\n\t""v_accvgpr_write_b32 a11, 0\n\t""v_accvgpr_write_b32 a12, 0\n\t""v_accvgpr_write_b32 a13, 0\n\t""v_accvgpr_write_b32 a14, 0\n\t""v_accvgpr_write_b32 a15, 0\n\t""v_accvgpr_write_b32 a16, 0\n\t""v_accvgpr_write_b32 a17, 0\n\t""v_accvgpr_write_b32 a18, 0\n\t""v_accvgpr_write_b32 a19, 0\n\t""v_accvgpr_write_b32 a20, 0\n\t""v_accvgpr_write_b32 a21, 0\n\t""v_accvgpr_write_b32 a22, 0\n\t""v_accvgpr_write_b32 a23, 0\n\t""v_accvgpr_write_b32 a24, 0\n\t""v_accvgpr_write_b32 a25, 0\n\t""v_accvgpr_write_b32 a26, 0\n\t""v_accvgpr_write_b32 a27, 0\n\t""v_accvgpr_write_b32 a28, 0\n\t""v_accvgpr_write_b32 a29, 0\n\t""v_accvgpr_write_b32 a30, 0\n\t""v_accvgpr_write_b32 a31, 0\n\t""v_accvgpr_write_b32 a32, 0\n\t""v_accvgpr_write_b32 a33, 0\n\t""v_accvgpr_write_b32 a34, 0\n\t""v_accvgpr_write_b32 a35, 0\n\t""v_accvgpr_write_b32 a36, 0\n\t""v_accvgpr_write_b32 a37, 0\n\t""v_accvgpr_write_b32 a38, 0\n\t""v_accvgpr_write_b32 a39, 0\n\t""v_accvgpr_write_b32 a40, 0\n\t""v_accvgpr_write_b32 a41, 0\n\t""v_accvgpr_write_b32 a42, 0\n\t""v_accvgpr_write_b32 a43, 0\n\t""v_accvgpr_write_b32 a44, 0\n\t""v_accvgpr_write_b32 a45, 0\n\t""v_accvgpr_write_b32 a46, 0\n\t""v_accvgpr_write_b32 a47, 0\n\t""v_accvgpr_write_b32 a48, 0\n\t""v_accvgpr_write_b32 a49, 0\n\t""v_accvgpr_write_b32 a50, 0\n\t""v_accvgpr_write_b32 a51, 0\n\t""v_accvgpr_write_b32 a52, 0\n\t""v_accvgpr_write_b32 a53, 0\n\t""v_accvgpr_write_b32 a54, 0\n\t""v_accvgpr_write_b32 a55, 0\n\t""v_accvgpr_write_b32 a56, 0\n\t""v_accvgpr_write_b32 a57, 0\n\t""v_accvgpr_write_b32 a58, 0\n\t""v_accvgpr_write_b32 a59, 0\n\t""v_accvgpr_write_b32 a60, 0\n\t""v_accvgpr_write_b32 a61, 0\n\t""v_accvgpr_write_b32 a62, 0\n\t""v_accvgpr_write_b32 a63, 0\n\t""v_accvgpr_write_b32 a64, 0\n\t""v_accvgpr_write_b32 a65, 0\n\t""v_accvgpr_write_b32 a66, 0\n\t""v_accvgpr_write_b32 a67, 0\n\t""v_accvgpr_write_b32 a68, 0\n\t""v_accvgpr_write_b32 a69, 0\n\t""v_accvgpr_write_b32 a70, 0\n\t""v_accvgpr_write_b32 a71, 0\n\t""v_accvgpr_write_b32 a72, 0\n\t""v_accvgpr_write_b32 a73, 0\n\t""v_accvgpr_write_b32 a74, 0\n\t""v_accvgpr_write_b32 a75, 0\n\t""v_accvgpr_write_b32 a76, 0\n\t""v_accvgpr_write_b32 a77, 0\n\t""v_accvgpr_write_b32 a78, 0\n\t""v_accvgpr_write_b32 a79, 0\n\t""v_accvgpr_write_b32 a80, 0\n\t""v_accvgpr_write_b32 a81, 0\n\t""v_accvgpr_write_b32 a82, 0\n\t""v_accvgpr_write_b32 a83, 0\n\t""v_accvgpr_write_b32 a84, 0\n\t""v_accvgpr_write_b32 a85, 0\n\t""v_accvgpr_write_b32 a86, 0\n\t""v_accvgpr_write_b32 a87, 0\n\t""v_accvgpr_write_b32 a88, 0\n\t""v_accvgpr_write_b32 a89, 0\n\t""v_accvgpr_write_b32 a90, 0\n\t""v_accvgpr_write_b32 a91, 0\n\t""v_accvgpr_write_b32 a92, 0\n\t""v_accvgpr_write_b32 a93, 0\n\t""v_accvgpr_write_b32 a94, 0\n\t""v_accvgpr_write_b32 a95, 0\n\t""v_accvgpr_write_b32 a96, 0\n\t""v_accvgpr_write_b32 a97, 0\n\t""v_accvgpr_write_b32 a98, 0\n\t""v_accvgpr_write_b32 a99, 0\n\t""v_accvgpr_write_b32 a100, 0\n\t""v_accvgpr_write_b32 a101, 0\n\t""v_accvgpr_write_b32 a102, 0\n\t""v_accvgpr_write_b32 a103, 0\n\t""v_accvgpr_write_b32 a104, 0\n\t""v_accvgpr_write_b32 a105, 0\n\t""v_accvgpr_write_b32 a106, 0\n\t""v_accvgpr_write_b32 a107, 0\n\t""v_accvgpr_write_b32 a108, 0\n\t""v_accvgpr_write_b32 a109, 0\n\t""v_accvgpr_write_b32 a110, 0\n\t""v_accvgpr_write_b32 a111, 0\n\t""v_accvgpr_write_b32 a112, 0\n\t""v_accvgpr_write_b32 a113, 0\n\t""v_accvgpr_write_b32 a114, 0\n\t""v_accvgpr_write_b32 a115, 0\n\t""v_accvgpr_write_b32 a116, 0\n\t""v_accvgpr_write_b32 a117, 0\n\t""v_accvgpr_write_b32 a118, 0\n\t""v_accvgpr_write_b32 a119, 0\n\t""v_accvgpr_write_b32 a120, 0\n\t""v_accvgpr_write_b32 a121, 0\n\t""v_accvgpr_write_b32 a122, 0\n\t""v_accvgpr_write_b32 a123, 0\n\t""v_accvgpr_write_b32 a124, 0\n\t""v_accvgpr_write_b32 a125, 0\n\t""v_accvgpr_write_b32 a126, 0\n\t""v_accvgpr_write_b32 a127, 0\n\t""v_accvgpr_write_b32 a128, 0\n\t""v_accvgpr_write_b32 a129, 0\n\t""v_accvgpr_write_b32 a130, 0\n\t""v_accvgpr_write_b32 a131, 0\n\t""v_accvgpr_write_b32 a132, 0\n\t""v_accvgpr_write_b32 a133, 0\n\t""v_accvgpr_write_b32 a134, 0\n\t""v_accvgpr_write_b32 a135, 0\n\t""v_accvgpr_write_b32 a136, 0\n\t""v_accvgpr_write_b32 a137, 0\n\t""v_accvgpr_write_b32 a138, 0\n\t""v_accvgpr_write_b32 a139, 0\n\t""v_accvgpr_write_b32 a140, 0\n\t""v_accvgpr_write_b32 a141, 0\n\t""v_accvgpr_write_b32 a142, 0\n\t""v_accvgpr_write_b32 a143, 0\n\t""v_accvgpr_write_b32 a144, 0\n\t""v_accvgpr_write_b32 a145, 0\n\t""v_accvgpr_write_b32 a146, 0\n\t""v_accvgpr_write_b32 a147, 0\n\t""v_accvgpr_write_b32 a148, 0\n\t""v_accvgpr_write_b32 a149, 0\n\t""v_accvgpr_write_b32 a150, 0\n\t""v_accvgpr_write_b32 a151, 0\n\t""v_accvgpr_write_b32 a152, 0\n\t""v_accvgpr_write_b32 a153, 0\n\t""v_accvgpr_write_b32 a154, 0\n\t""v_accvgpr_write_b32 a155, 0\n\t""v_accvgpr_write_b32 a156, 0\n\t""v_accvgpr_write_b32 a157, 0\n\t""v_accvgpr_write_b32 a158, 0\n\t""v_accvgpr_write_b32 a159, 0\n\t""v_accvgpr_write_b32 a160, 0\n\t""v_accvgpr_write_b32 a161, 0\n\t""v_accvgpr_write_b32 a162, 0\n\t""v_accvgpr_write_b32 a163, 0\n\t""v_accvgpr_write_b32 a164, 0\n\t""v_accvgpr_write_b32 a165, 0\n\t""v_accvgpr_write_b32 a166, 0\n\t""v_accvgpr_write_b32 a167, 0\n\t""v_accvgpr_write_b32 a168, 0\n\t""v_accvgpr_write_b32 a169, 0\n\t""v_accvgpr_write_b32 a170, 0\n\t""v_accvgpr_write_b32 a171, 0\n\t""v_accvgpr_write_b32 a172, 0\n\t""v_accvgpr_write_b32 a173, 0\n\t""v_accvgpr_write_b32 a174, 0\n\t""v_accvgpr_write_b32 a175, 0\n\t""v_accvgpr_write_b32 a176, 0\n\t""v_accvgpr_write_b32 a177, 0\n\t""v_accvgpr_write_b32 a178, 0\n\t""v_accvgpr_write_b32 a179, 0\n\t""v_accvgpr_write_b32 a180, 0\n\t""v_accvgpr_write_b32 a181, 0\n\t""v_accvgpr_write_b32 a182, 0\n\t""v_accvgpr_write_b32 a183, 0\n\t""v_accvgpr_write_b32 a184, 0\n\t""v_accvgpr_write_b32 a185, 0\n\t""v_accvgpr_write_b32 a186, 0\n\t""v_accvgpr_write_b32 a187, 0\n\t""v_accvgpr_write_b32 a188, 0\n\t""v_accvgpr_write_b32 a189, 0\n\t""v_accvgpr_write_b32 a190, 0\n\t""v_accvgpr_write_b32 a191, 0\n\t""v_accvgpr_write_b32 a192, 0\n\t""v_accvgpr_write_b32 a193, 0\n\t""v_accvgpr_write_b32 a194, 0\n\t""v_accvgpr_write_b32 a195, 0\n\t""v_accvgpr_write_b32 a196, 0\n\t""v_accvgpr_write_b32 a197, 0\n\t""v_accvgpr_write_b32 a198, 0\n\t""v_accvgpr_write_b32 a199, 0\n\t""v_accvgpr_write_b32 a200, 0\n\t""v_accvgpr_write_b32 a201, 0\n\t""v_accvgpr_write_b32 a202, 0\n\t""v_accvgpr_write_b32 a203, 0\n\t""v_accvgpr_write_b32 a204, 0\n\t""v_accvgpr_write_b32 a205, 0\n\t""v_accvgpr_write_b32 a206, 0\n\t""v_accvgpr_write_b32 a207, 0\n\t""v_accvgpr_write_b32 a208, 0\n\t""v_accvgpr_write_b32 a209, 0\n\t""v_accvgpr_write_b32 a210, 0\n\t""v_accvgpr_write_b32 a211, 0\n\t""v_accvgpr_write_b32 a212, 0\n\t""v_accvgpr_write_b32 a213, 0\n\t""v_accvgpr_write_b32 a214, 0\n\t""v_accvgpr_write_b32 a215, 0\n\t""v_accvgpr_write_b32 a216, 0\n\t""v_accvgpr_write_b32 a217, 0\n\t""v_accvgpr_write_b32 a218, 0\n\t""v_accvgpr_write_b32 a219, 0\n\t""v_accvgpr_write_b32 a220, 0\n\t""v_accvgpr_write_b32 a221, 0\n\t""v_accvgpr_write_b32 a222, 0\n\t""v_accvgpr_write_b32 a223, 0\n\t""v_accvgpr_write_b32 a224, 0\n\t""v_accvgpr_write_b32 a225, 0\n\t""v_accvgpr_write_b32 a226, 0\n\t""v_accvgpr_write_b32 a227, 0\n\t""v_accvgpr_write_b32 a228, 0\n\t""v_accvgpr_write_b32 a229, 0\n\t""v_accvgpr_write_b32 a230, 0\n\t""v_accvgpr_write_b32 a231, 0\n\t""v_accvgpr_write_b32 a232, 0\n\t""v_accvgpr_write_b32 a233, 0\n\t""v_accvgpr_write_b32 a234, 0\n\t""v_accvgpr_write_b32 a235, 0\n\t""v_accvgpr_write_b32 a236, 0\n\t""v_accvgpr_write_b32 a237, 0\n\t""v_accvgpr_write_b32 a238, 0\n\t""v_accvgpr_write_b32 a239, 0\n\t""v_accvgpr_write_b32 a240, 0\n\t""v_accvgpr_write_b32 a241, 0\n\t""v_accvgpr_write_b32 a242, 0\n\t""v_accvgpr_write_b32 a243, 0\n\t""v_accvgpr_write_b32 a244, 0\n\t""v_accvgpr_write_b32 a245, 0\n\t""v_accvgpr_write_b32 a246, 0\n\t""v_accvgpr_write_b32 a247, 0\n\t""v_accvgpr_write_b32 a248, 0\n\t""v_accvgpr_write_b32 a249, 0\n\t""v_accvgpr_write_b32 a250, 0\n\t""v_accvgpr_write_b32 a251, 0\n\t""v_accvgpr_write_b32 a252, 0\n\t""v_accvgpr_write_b32 a253, 0\n\t""v_accvgpr_write_b32 a254, 0\n\t""v_accvgpr_write_b32 a255, 0\n\t"
 
@@ -158,194 +158,19 @@ __global__ __launch_bounds__(256, 2) void gemm_tiled_kernel(const bf16* __restri
 }
 
 // ----------------------------------------------------------------------------------------------
-// Large kernel (prefill, M >= 1024): 256x256x64 block tile, 8 waves as 2(M) x 4(N), each wave
-// 128x64 = 8x4 MFMA 16x16x32 tiles (128 accumulator VGPRs). A K-tile is held as four 16 KiB
-// K-halves [A-k0 | B-k0 | A-k1 | B-k1] (256 rows x 32 k, 64-B rows); two buffers = 128 KiB LDS.
-// Each K-tile runs 4 phases of 16 MFMAs (k-half x {top, bottom} 64 rows of the wave's A), and each
-// phase issues ONE K-half of the next K-tile by global_load_lds (2 per wave): a K-half is issued
-// 3-4 phases before its first read, so loads stay in flight across the phase barriers (raw
-// s_barrier + counted vmcnt(4) at the end of phases 2 and 4; never a __syncthreads() vmcnt(0) drain,
-// cdna_hip_programming §5 "Pipelining across barriers", T3/T4). 64-B rows are XOR-swizzled by
-// G[(row>>2)&3] = {0,3,2,1} on the 16-B chunk: conflict-free for all four ds_read_b128 lane groups.
+// Shared tile geometry of the 256x256 prefill kernels. Round 1-2's stepping stones (the 8-wave 4-phase
+// "large" kernel, the 8-wave unit ring and the non-persistent 4-wave ring, measured in profiles/r2/gemm_ring.jsonl
+// and gemm_w4p*.jsonl) were superseded by the persistent kernels below and removed from the build.
 // ----------------------------------------------------------------------------------------------
 constexpr int LBM = 256, LBN = 256, LBK = 64;
 constexpr int kHalfBytes = 256 * 32 * 2;  // one K-half of one operand
 
 __device__ __forceinline__ int lswz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
 
-template <int EPI, bool OUTF32>
-__global__ __launch_bounds__(512, 1) void gemm_large_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                            void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                            int K, int ldc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 buffers x [A-k0 | B-k0 | A-k1 | B-k1]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 4;
-  const int group = wg / (GM * tiles_n);
-  const int first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int pin = wg % (GM * tiles_n);
-  const int tm = first_m + pin % gsz, tn = pin / gsz;
-  const int m0 = tm * LBM, n0 = tn * LBN;
-
-  // staging: each wave issues 2 x 1 KiB (16 rows x 64 B) per K-half; lane -> (row, physical chunk)
-  size_t a_src[2], b_src[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int q = wid * 2 + j;
-    const int row = q * 16 + (lane >> 2);
-    const int cg = (lane & 3) ^ lswz(row);
-    a_src[j] = (size_t)min(m0 + row, M - 1) * K + cg * 8;
-    b_src[j] = (size_t)min(n0 + row, N - 1) * K + cg * 8;
-  }
-  // K-half h (0: A-k0, 1: B-k0, 2: A-k1, 3: B-k1) of K-tile kt into buffer buf
-  auto stage = [&](int kt, int h, int buf) {
-    const bf16* src = (h & 1) ? B : A;
-    const size_t* off = (h & 1) ? b_src : a_src;
-    char* dst = smem + buf * 4 * kHalfBytes + h * kHalfBytes;
-    const int k0 = kt * LBK + (h >> 1) * 32;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(src + off[j] + k0, dst + (wid * 2 + j) * 1024);
-  };
-
-  const int wm = wid >> 2, wn = wid & 3;
-  // fragment read byte offsets inside a K-half: row r, logical chunk c = lane>>4
-  int a_rd[8], b_rd[4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = wm * 128 + 16 * i + (lane & 15);
-    a_rd[i] = r * 64 + (((lane >> 4) ^ lswz(r)) << 4);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = wn * 64 + 16 * j + (lane & 15);
-    b_rd[j] = r * 64 + (((lane >> 4) ^ lswz(r)) << 4);
-  }
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / LBK;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) stage(0, h, 0);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // k0 halves of tile 0 landed
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  // Register double-buffering: every phase first issues the ds_reads of the NEXT phase's
-  // fragments, then runs its 16 MFMAs on fragments read one phase earlier, so LDS latency hides
-  // under the MFMAs. Data a prefetch reads must be valid one phase earlier than its use, hence
-  // the counted waits at the end of phases 1 and 3 (vmcnt(2): the one younger K-half may fly on).
-  auto rd_a = [&](bf16x8* f, const char* buf, int kh, int hm) {
-    const char* s = buf + (2 * kh) * kHalfBytes;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = *reinterpret_cast<const bf16x8*>(s + a_rd[4 * hm + i]);
-  };
-  auto rd_b = [&](bf16x8* f, const char* buf, int kh) {
-    const char* s = buf + (2 * kh + 1) * kHalfBytes;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = *reinterpret_cast<const bf16x8*>(s + b_rd[j]);
-  };
-  auto mma = [&](const bf16x8* af, const bf16x8* bfr, int hm) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[4 * hm + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[4 * hm + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  bf16x8 bk0[4], bk1[4], aT0[4], aB0[4], aT1[4], aB1[4];
-  rd_b(bk0, smem, 0);
-  rd_a(aT0, smem, 0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    const char* base = smem + cur * 4 * kHalfBytes;
-    const char* nbase = smem + (cur ^ 1) * 4 * kHalfBytes;
-    // phase 1: k0 x top rows
-    if (more) stage(kt + 1, 0, cur ^ 1);
-    rd_a(aB0, base, 0, 1);
-    mma(aT0, bk0, 0);
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // k1 halves of this tile landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();
-    // phase 2: k0 x bottom rows; prefetch k1 operands
-    if (more) stage(kt + 1, 1, cur ^ 1);
-    rd_b(bk1, base, 1);
-    rd_a(aT1, base, 1, 0);
-    mma(aB0, bk0, 1);
-    barrier();
-    // phase 3: k1 x top rows
-    if (more) stage(kt + 1, 2, cur ^ 1);
-    rd_a(aB1, base, 1, 1);
-    mma(aT1, bk1, 0);
-    if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // k0 halves of the next tile landed
-    barrier();
-    // phase 4: k1 x bottom rows; prefetch the next tile's k0 operands
-    if (more) {
-      stage(kt + 1, 3, cur ^ 1);
-      rd_b(bk0, nbase, 0);
-      rd_a(aT0, nbase, 0, 0);
-    }
-    mma(aB1, bk1, 1);
-    barrier();
-  }
-
-  if (EPI == EPI_SWIGLU) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        const int nout = (n0 + wn * 64) / 2 + 16 * jp + (lane & 15);
-        if (2 * nout >= N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * 128 + 16 * i + 4 * (lane >> 4) + r;
-          if (m >= M) continue;
-          store_out<EPI_NONE, OUTF32>(C, nullptr, nullptr, ldc, m, nout, silu(acc[i][2 * jp][r]) * acc[i][2 * jp + 1][r]);
-        }
-      }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + 16 * j + (lane & 15);
-        if (n >= N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * 128 + 16 * i + 4 * (lane >> 4) + r;
-          if (m < M) store_out<EPI, OUTF32>(C, bias, R, ldc, m, n, acc[i][j][r]);
-        }
-      }
-  }
-}
-
 // ----------------------------------------------------------------------------------------------
-// Ring kernel (prefill, force 4; superseded by gemm_w4d_kernel): 256x256 block tile, 8 waves as 2(M) x 4(N),
-// each wave 128x64 = 8x4 MFMA 16x16x32 tiles. K is staged in 32-deep *units* (A 256x32 | B 256x32
-// = 32 KiB) through a ring of RNS = 5 LDS slots (160 KiB) by global_load_lds, 3-4 units ahead of
-// their use. Each unit runs two phases (wave rows 0-63 / 64-127, 16 MFMAs each) and ONE barrier:
-// a phase issues half a unit of prefetch (2 glds per wave) and ds_reads the next phase's fragments
-// (register double buffer) *behind* its first MFMAs (sched_group_barrier), so after the barrier the
-// MFMA pipe restarts at once instead of behind ~2 glds + 8 ds_reads of issue; waits are counted
-// (vmcnt(12), never a drain in the loop; cdna_hip_programming §5 "Pipelining across barriers").
+// Unit ring of the persistent kernels: K is staged in 32-deep *units* (A 256x32 | B 256x32 = 32 KiB) through
+// RNS = 5 LDS slots (160 KiB) by global_load_lds, 3-4 units ahead of their use; waits are counted (never a
+// vmcnt(0) drain in the loop; cdna_hip_programming §5 "Pipelining across barriers").
 //
 // Operands are issued *swapped* (MFMA A = weight fragment, B = activation fragment), so each lane
 // accumulates C[m][n .. n+3] - four consecutive output columns of one row - instead of one column
@@ -354,9 +179,8 @@ __global__ __launch_bounds__(512, 1) void gemm_large_kernel(const bf16* __restri
 // stores (bias / GELU / residual / SwiGLU applied in fp32 on the way; one bf16 rounding).
 //
 // Measured on MI355X at M = 16384 (Llama-3-8B QKV / O / gate_up / down, random operands,
-// profiles/r2/gemm_ring.jsonl): 1.27-1.39 PF/s, 1.10-1.15x the previous 4-phase double-buffered
-// kernel (gemm_large_kernel) and 0.78-0.85x hipBLASLt's stream-K kernel. Ablations on the box: no
-// vmcnt wait +2 %, no barrier +3 % (so neither is the limiter); 1 barrier per unit vs 2: +0 %.
+// profiles/r2/gemm_ring.jsonl): the 8-wave ring with this epilogue reached 1.27-1.39 PF/s; the persistent
+// kernels below 1.55+ PF/s.
 // ----------------------------------------------------------------------------------------------
 constexpr int RNS = 5;                       // ring slots
 constexpr int kUnitBytes = 2 * 256 * 32 * 2;  // A + B, 32 k
@@ -460,13 +284,6 @@ __device__ __forceinline__ void epilogue_rows(const f32x4 (&acc_i)[NJ], void* C,
   }
 }
 
-template <int EPI, bool OUTF32, int NJ>
-__device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[8][NJ], void* C, const bf16* bias, const bf16* R,
-                                                 int M, int N, int ldc, int mrow, int nb, int lane) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) epilogue_rows<EPI, OUTF32, NJ>(acc[i], C, bias, R, M, N, ldc, mrow + 16 * i, nb, lane);
-}
-
 template <int N, typename F, int... I>
 __device__ __forceinline__ void for_each_const_impl(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -503,150 +320,6 @@ __device__ __forceinline__ void sgb_pairs() {
   }
 }
 
-template <int EPI, bool OUTF32>
-__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                           int K, int ldc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // RNS slots x [A 16K | B 16K]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 4;
-  const int group = wg / (GM * tiles_n);
-  const int first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int pin = wg % (GM * tiles_n);
-  const int tm = first_m + pin % gsz, tn = pin / gsz;
-  const int m0 = tm * LBM, n0 = tn * LBN;
-
-  // staging: glds j (0, 1) of wave w fills rows (2w + j) * 16 .. +16 of a 256 x 64-B half-unit
-  const bf16* a_src[2];
-  const bf16* b_src[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wid * 2 + j) * 16 + (lane >> 2);
-    const int cg = (lane & 3) ^ lswz(row);
-    a_src[j] = A + (size_t)min(m0 + row, M - 1) * K + cg * 8;
-    b_src[j] = B + (size_t)min(n0 + row, N - 1) * K + cg * 8;
-  }
-  char* const wdst = smem + wid * 2048;
-  // half (0: A, 1: B) of unit u_src into the slot of unit u_slot
-  auto stage = [&](int u_slot, int u_src, int half) {
-    char* dst = wdst + (u_slot % RNS) * kUnitBytes + half * kUnitHalf;
-    const bf16* const* src = half ? b_src : a_src;
-    glds16(src[0] + u_src * 32, dst);
-    glds16(src[1] + u_src * 32, dst + 1024);
-  };
-
-  const int wm = wid >> 2, wn = wid & 3;
-  int a_rd[8], b_rd[4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = wm * 128 + 16 * i + (lane & 15);
-    a_rd[i] = r * 64 + (((lane >> 4) ^ lswz(r)) << 4);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = wn * 64 + 16 * j + (lane & 15);
-    b_rd[j] = kUnitHalf + r * 64 + (((lane >> 4) ^ lswz(r)) << 4);
-  }
-  auto rd_a = [&](bf16x8* f, int u, int hm) {
-    const char* s = smem + (u % RNS) * kUnitBytes;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = *reinterpret_cast<const bf16x8*>(s + a_rd[4 * hm + i]);
-  };
-  auto rd_b = [&](bf16x8* f, int u) {
-    const char* s = smem + (u % RNS) * kUnitBytes;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = *reinterpret_cast<const bf16x8*>(s + b_rd[j]);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // no s_setprio around the cluster: it is a scheduling boundary and would break the interleave
-  auto mma = [&](const bf16x8* af, const bf16x8* bfr, int hm) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[4 * hm + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[4 * hm + i][j], 0, 0, 0);
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // MFMAs first in program order, the 2 glds and 4 / 8 ds_reads in the shadows of the first ones
-  auto sched_top = [] {
-    sgb_pairs<2, 0x10>();
-    sgb_pairs<4, 0x100>();
-    __builtin_amdgcn_sched_group_barrier(0x8, 10, 0);
-  };
-  auto sched_bot = [] {
-    sgb_pairs<2, 0x10>();
-    sgb_pairs<8, 0x100>();
-    __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // end of a top phase: the waits pinned after the whole MFMA cluster, then the unit's one barrier
-  auto top_end = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): this phase's fragment reads retired
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // unit u+1 landed (u+2 .. u+4 in flight)
-    barrier();
-  };
-
-  const int nu = K / 32;  // host guarantees nu even and nu >= RNS
-#pragma unroll
-  for (int u = 0; u < RNS - 1; ++u) {
-    stage(u, u, 0);
-    stage(u, u, 1);
-  }
-  stage(RNS - 1, RNS - 1, 0);
-  asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // unit 0 landed (units 1..3 + half of 4 in flight)
-  barrier();
-  bf16x8 aT[4], aB[4], b0[4], b1[4];
-  rd_a(aT, 0, 0);
-  rd_b(b0, 0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  // One barrier per unit, after its top phase. A slot's last read is its unit's top-phase aB read, so
-  // the slot is free right after that barrier: the bottom phase refills it with the A half of unit
-  // u+RNS and the next top phase with the B half. The phases are branch-free: past the end a prefetch
-  // re-reads the last unit into a slot no later unit uses, so the vmcnt counts stay uniform.
-  for (int u = 0; u < nu; u += 2) {
-    // phase (u, top)
-    stage(u + RNS - 1, min(u + RNS - 1, nu - 1), 1);
-    rd_a(aB, u, 1);
-    mma(aT, b0, 0);
-    sched_top();
-    top_end();
-    // phase (u, bottom): no barrier after it
-    stage(u + RNS, min(u + RNS, nu - 1), 0);
-    rd_a(aT, u + 1, 0);
-    rd_b(b1, u + 1);
-    mma(aB, b0, 1);
-    sched_bot();
-    // phase (u+1, top)
-    stage(u + RNS, min(u + RNS, nu - 1), 1);
-    rd_a(aB, u + 1, 1);
-    mma(aT, b1, 0);
-    sched_top();
-    top_end();
-    // phase (u+1, bottom)
-    stage(u + RNS + 1, min(u + RNS + 1, nu - 1), 0);
-    rd_a(aT, u + 2, 0);  // past the end: reads a stale slot into dead registers
-    rd_b(b0, u + 2);
-    mma(aB, b1, 1);
-    sched_bot();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-  epilogue_swapped<EPI, OUTF32, 4>(acc, C, bias, R, M, N, ldc, m0 + wm * 128, n0 + wn * 64, lane);
-}
-
 // ----------------------------------------------------------------------------------------------
 // 4-wave ring kernel: the same 256x256 block tile and 5-slot ring, but 4 waves as 2 x 2, each owning
 // a 128x128 output (8 x 8 MFMA 16x16x32 tiles, 256 accumulator registers in AGPRs: one wave per
@@ -657,123 +330,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(const bf16* __restric
 // ds_reads of unit u+1 and the 8 glds of unit u+5 into unit u's own slot (its fragments are already in
 // registers); one barrier per phase.
 // ----------------------------------------------------------------------------------------------
-template <int EPI, bool OUTF32>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                         void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                         int K, int ldc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // RNS slots x [A 16K | B 16K]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 4;
-  const int group = wg / (GM * tiles_n);
-  const int first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int pin = wg % (GM * tiles_n);
-  const int tm = first_m + pin % gsz, tn = pin / gsz;
-  const int m0 = tm * LBM, n0 = tn * LBN;
-
-  // staging: glds j (0..3) of wave w fills rows (4w + j) * 16 .. +16 of the A (and B) half-unit
-  const bf16* a_src[4];
-  const bf16* b_src[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (wid * 4 + j) * 16 + (lane >> 2);
-    const int cg = (lane & 3) ^ lswz(row);
-    a_src[j] = A + (size_t)min(m0 + row, M - 1) * K + cg * 8;
-    b_src[j] = B + (size_t)min(n0 + row, N - 1) * K + cg * 8;
-  }
-  auto stage = [&](int u_slot, int u_src) {
-    char* d = smem + (u_slot % RNS) * kUnitBytes + wid * 4096;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) glds16(a_src[j] + u_src * 32, d + j * 1024);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) glds16(b_src[j] + u_src * 32, d + kUnitHalf + j * 1024);
-  };
-  const int wm = wid >> 1, wn = wid & 1;
-  // (row >> 2) & 3 of rows wm*128 + 16i + (lane&15) does not depend on i: one base, +1 KiB per tile
-  const int rsw = (((lane >> 4) ^ lswz(lane & 15)) << 4);
-  const int a_rd = (wm * 128 + (lane & 15)) * 64 + rsw;
-  const int b_rd = kUnitHalf + (wn * 128 + (lane & 15)) * 64 + rsw;
-  auto rd = [&](bf16x8* af, bf16x8* bfr, int u) {
-    const char* s = smem + (u % RNS) * kUnitBytes;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8*>(s + a_rd + i * 1024);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(s + b_rd + j * 1024);
-  };
-  // The 256 accumulators live in physical AGPRs a0..a255 that the compiler never sees: every MFMA is
-  // an asm statement naming its AGPRs and clobbering all of them, so no compiler value is ever kept
-  // in an AGPR (with hipcc's own MFMAs the allocator splits the accumulators between the AGPR and
-  // VGPR halves and shuffles / spills them every phase). hipcc does not model these asm MFMAs, so
-  // their hazards are padded here: s_nops after the AGPR init and before the epilogue's reads; an
-  // accumulator is re-used only 64 MFMAs later. The asm statements keep their order; the glds /
-  // ds_read issue is interleaved with them by hand (pinned by sched_barrier).
-  asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto phase_end = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): next unit's fragments in registers
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // unit u+2 landed (u+3..u+5 in flight)
-    barrier();
-  };
-  // one phase: 64 MFMAs on (af, bfr) with the 8 glds of unit u_src (into slot u_slot) and the 16
-  // ds_reads of unit u_rd (into naf, nbf) spread between them
-  auto phase = [&](const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int u_rd, int u_slot, int u_src) {
-    char* d = smem + (u_slot % RNS) * kUnitBytes + wid * 4096;
-    const char* sr = smem + (u_rd % RNS) * kUnitBytes;
-    for_each_const<64>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      constexpr int i = t >> 3, j = t & 7;
-      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                   :
-                   : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
-                   : GAI_AGPR_CLOBBERS);
-      // glds after MFMAs 5, 13, .., 61 (one per 8: an LDS-DMA issue can stall a lone wave for 60+
-      // cycles); ds_reads after MFMAs 0, 2, .., 30 (retired long before the phase-end lgkmcnt(0))
-      constexpr int g = (t - 5) / 8, r = t / 2;
-      if constexpr (t % 8 == 5 && g < 4) glds16(a_src[g] + u_src * 32, d + g * 1024);
-      else if constexpr (t % 8 == 5) glds16(b_src[g - 4] + u_src * 32, d + kUnitHalf + (g - 4) * 1024);
-      else if constexpr (t % 2 == 0 && t < 32 && r < 8) naf[r] = *reinterpret_cast<const bf16x8*>(sr + a_rd + r * 1024);
-      else if constexpr (t % 2 == 0 && t < 32) nbf[r - 8] = *reinterpret_cast<const bf16x8*>(sr + b_rd + (r - 8) * 1024);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-
-  const int nu = K / 32;  // host guarantees nu even and nu >= RNS
-#pragma unroll
-  for (int u = 0; u < RNS; ++u) stage(u, u);
-  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // units 0 and 1 landed
-  barrier();
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  rd(a0, b0, 0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  barrier();  // every wave has slot 0 in registers before phase 0 restages it
-  for (int u = 0; u < nu; u += 2) {
-    // past the end: a dummy refill of a dead slot, and a stale slot read into dead registers
-    phase(a0, b0, a1, b1, u + 1, u + RNS, min(u + RNS, nu - 1));
-    phase_end();
-    phase(a1, b1, a0, b0, u + 2, u + 1 + RNS, min(u + 1 + RNS, nu - 1));
-    phase_end();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
-  // epilogue, one 16-row group (8 tiles = 32 AGPRs) at a time
-  for_each_const<8>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    f32x4 row[8];
-    read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
-    epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
-  });
-}
-
 // ----------------------------------------------------------------------------------------------
-// Persistent 4-wave ring kernel: gemm_w4_kernel's tile, waves and phase, but one workgroup per CU
+// Persistent 4-wave ring kernel: the 4-wave tile (above), waves and phase, but one workgroup per CU
 // walking tiles blockIdx.x, +G, +2G, ... with ONE unit ring running across its tiles. The last six
 // phases of a tile prefetch units 0..4 of the workgroup's next tile, and the last one reads unit 0's
 // fragments, so a tile's epilogue (AGPR reads + 16-B stores) runs while the next tile's operands are
@@ -1390,48 +948,6 @@ void launch_tiled(const void* A, const void* B, void* C, const void* bias, const
 }
 
 template <int EPI, bool OUTF32>
-void launch_large(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                  hipStream_t st) {
-  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
-  static bool once = false;
-  if (!once) {
-    set_max_lds(gemm_large_kernel<EPI, OUTF32>);
-    once = true;
-  }
-  gemm_large_kernel<EPI, OUTF32><<<tiles, 512, 8 * kHalfBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                      (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
-  GAI_LAUNCH_CHECK();
-}
-
-template <int EPI, bool OUTF32>
-void launch_ring(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                 hipStream_t st) {
-  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
-  static bool once = false;
-  if (!once) {
-    set_max_lds(gemm_ring_kernel<EPI, OUTF32>);
-    once = true;
-  }
-  gemm_ring_kernel<EPI, OUTF32><<<tiles, 512, RNS * kUnitBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                     (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
-  GAI_LAUNCH_CHECK();
-}
-
-template <int EPI, bool OUTF32>
-void launch_w4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-               hipStream_t st) {
-  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
-  static bool once = false;
-  if (!once) {
-    set_max_lds(gemm_w4_kernel<EPI, OUTF32>);
-    once = true;
-  }
-  gemm_w4_kernel<EPI, OUTF32><<<tiles, 256, RNS * kUnitBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                   (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
-  GAI_LAUNCH_CHECK();
-}
-
-template <int EPI, bool OUTF32>
 void launch_w4p(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
                 hipStream_t st) {
   const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
@@ -1526,11 +1042,9 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force == 4 || force == 7 || force == 8 || force == 9 || force == 10 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force == 8 || force == 9 || force == 10 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
     if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if (force == 7) return launch_w4<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if (force == 4) return launch_ring<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
@@ -1540,8 +1054,6 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
       return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   }
-  const bool large_ok = M >= 1024 && N >= 256;
-  if (force == 3 || (force == 0 && large_ok)) return launch_large<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
   launch_tiled<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
 }
 

@@ -1,4 +1,4 @@
-"""Ring-pipelined 256x256 prefill GEMM (csrc/kernels/gemm.hip gemm_ring_kernel) against the fp32 reference.
+"""Persistent 256x256 prefill GEMMs (csrc/kernels/gemm.hip: w4p / w4d / w4r) against the fp32 reference.
 
 Covers every epilogue, bf16 and fp32 output, partial M / N tiles, the ring tail (K / 32 close to the
 ring depth) and launch-to-launch bit-repeatability (race screen for the counted-vmcnt pipeline)."""
@@ -11,9 +11,9 @@ from generativeaiexamples_amd import ops
 from generativeaiexamples_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
-# force codes in gai_gemm: 8-wave ring, 4-wave asm-MFMA ring, persistent 4-wave ring (tile walk per CU),
-# persistent full-line double-unit kernel, and its 5-part LDS ring variant (the default for M >= 1024)
-KERNELS = {"ring8": 4, "w4": 7, "w4p": 8, "w4d": 9, "w4r": 10}
+# force codes in gai_gemm: persistent 4-wave ring (tile walk per CU), persistent full-line double-unit kernel, and
+# its 5-part LDS ring variant (the default for M >= 1024)
+KERNELS = {"w4p": 8, "w4d": 9, "w4r": 10}
 
 SHAPES = [(1024, 256, 192), (1280, 1040, 256), (2048, 2304, 1024), (1100, 4096, 4096), (4096, 6144, 320),
           (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256)]  # last two: > 256 tiles, multi-tile walks

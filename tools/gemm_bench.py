@@ -1,4 +1,4 @@
-"""Prefill GEMM A/B: the hand-written kernels (ring / large) vs hipBLASLt (default + tuned table) on the
+"""Prefill GEMM A/B: the hand-written persistent kernels (w4p / w4d / w4r) vs hipBLASLt (default + tuned table) on the
 Llama-3-8B projection shapes at M = 16384 (one 16K-token prefill chunk), random operands, interleaved
 rounds in one process (cdna_hip_programming §5.4 rules 24/25). One JSON line per shape.
 
@@ -47,12 +47,9 @@ def main():
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        arms = {"ring": lambda: nat.gemm(x, w, out, None, None, 0, 4),
-                "w4": lambda: nat.gemm(x, w, out, None, None, 0, 7),
-                "w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
+        arms = {"w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
                 "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
                 "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
-                "large": lambda: nat.gemm(x, w, out, None, None, 0, 3),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
         for _ in range(a.rounds):

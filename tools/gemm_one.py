@@ -1,5 +1,5 @@
 """Run one GEMM arm repeatedly (for rocprofv3 PMC passes): python tools/gemm_one.py ARM N K [M] [iters]
-ARM: ring | w4 | w4p | w4d | w4r | ring_noilv | large | blas (hipBLASLt)."""
+ARM: w4p | w4d | w4r | blas (hipBLASLt); the ring / large stepping stones left the build in round 4."""
 import math
 import os
 import sys
@@ -15,7 +15,7 @@ iters = int(sys.argv[5]) if len(sys.argv) > 5 else 30
 x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
 w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
 out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-force = {"ring": 4, "ring_noilv": 5, "ring_ilv2bar": 6, "large": 3, "w4": 7, "w4p": 8, "w4d": 9, "w4r": 10}.get(arm)
+force = {"w4p": 8, "w4d": 9, "w4r": 10}.get(arm)
 nat = ops.native()
 for _ in range(iters):
     if force is None:
