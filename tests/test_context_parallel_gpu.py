@@ -30,6 +30,7 @@ def test_prefill_kernel_lse(cuda, causal, D):
     assert (lse.cpu() - lse_ref).abs().max() < 1e-2
 
 
+@pytest.mark.multirank
 def test_ring_attention_gpu_two_ranks(tmp_path, cuda):
     sock = socket.socket()
     sock.bind(("127.0.0.1", 0))

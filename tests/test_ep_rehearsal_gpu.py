@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 
 from tests import _dist_workers as W
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.multirank]
 
 
 def _port():

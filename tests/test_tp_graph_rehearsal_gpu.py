@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 
 from tests import _dist_workers as W
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.multirank]
 
 
 def _port():
