@@ -22,6 +22,9 @@
 #include "gai_epilogue.h"
 #include "gai_rope.h"
 
+#include <algorithm>
+#include <map>
+#include <mutex>
 #include <utility>
 
 // every AGPR, for the asm-MFMA persistent kernels (w4p / w4d / w4r)
@@ -304,6 +307,16 @@ __device__ __forceinline__ void read_acc_tile(f32x4& v) {
       : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
       : "i"(BASE), "i"(BASE + 1), "i"(BASE + 2), "i"(BASE + 3));
   v = f32x4{x0, x1, x2, x3};
+}
+// v -> AGPRs a[BASE .. BASE+3]
+template <int BASE>
+__device__ __forceinline__ void write_acc_tile(const f32x4& v) {
+  asm volatile(
+      "v_accvgpr_write_b32 a%c0, %4\n\tv_accvgpr_write_b32 a%c1, %5\n\t"
+      "v_accvgpr_write_b32 a%c2, %6\n\tv_accvgpr_write_b32 a%c3, %7"
+      :
+      : "i"(BASE), "i"(BASE + 1), "i"(BASE + 2), "i"(BASE + 3), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])
+      : GAI_AGPR_CLOBBERS);
 }
 template <int I, int... J>
 __device__ __forceinline__ void read_acc_row(f32x4 (&row)[8], std::integer_sequence<int, J...>) {
@@ -707,27 +720,60 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
 // per double as in w4d (even phase end, after vmcnt(8): double D+1 landed, A(D+2) may fly).
 // M = 16384 (profiles/r2/gemm_w4p_ab.jsonl): 1.55-1.56 PF/s on O / down / gate_up; the longer A cover
 // lifts the deep-K down projection (activations streamed from HBM) from 1.41 (w4d) to 1.56 PF/s.
+//
+// SK = true: the stream-K walk, for grids the 256x256 tiles fill badly (a 2406-token prefill has 160 O / down
+// tiles for 256 CUs: one 62 %-full wave; gate_up 1120 tiles: 4.4 waves). The k-doubles of all tiles form one
+// tile-major sequence of units; logical workgroup g (XCD-contiguous, so neighbouring runs share an L2) owns an
+// equal run of unit pairs and walks it as *segments*, one per tile it touches, through the same ring (which
+// runs on across segments as it runs across tiles in the tile walk). A tile covered by one segment takes the
+// normal epilogue. A split tile's contributors hand fp32 partials over without ever waiting on each other
+// (nothing assumes co-residency): each wave stores its 128x128 quadrant write-through (sc1) in fragment order,
+// vmcnt(0), then draws one relaxed agent-scope ticket for (tile, wave); the wave that draws the last ticket
+// sums the quadrants in contributor order - bitwise the same result whichever contributor finishes - and runs
+// the epilogue. The tile's first contributor reaches it at the END of its run, after the others stored theirs
+// at the start of theirs, so it first peeks the counter and usually sums without storing its own.
+// Workspace [G][2 slots][4 waves][16384] fp32 (slot 0: a run's unaligned first segment, slot 1: a first
+// contributor that was not last); counters [tiles][4], zero between launches (the last ticket resets its own).
 // ----------------------------------------------------------------------------------------------
 constexpr int kPart = 256 * 64 * 2;  // one operand of a double unit
 
-template <int EPI, bool OUTF32>
+constexpr int kSkQuad = 128 * 128;  // fp32 of one wave's quadrant partial
+
+template <int EPI, bool OUTF32, bool SK = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc) {
+                                                          int K, int ldc, float* ws = nullptr, int* cnt = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 5 parts x 32 KiB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
   const int tiles = tiles_m * tiles_n;
   const int G = gridDim.x;
-  const int n_my = (tiles - (int)blockIdx.x + G - 1) / G;
-  auto coords = [&](int it, int& m0, int& n0) {
-    const int wg = xcd_remap((int)blockIdx.x + it * G, tiles);
+  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2 (SK: K % 128 == 0)
+  // walk positions: tile walk index it (tile blockIdx.x + it * G through the XCD remap), or SK unit index
+  const long long P = (long long)tiles * (nd / 2);  // SK: unit pairs
+  const int lg = SK ? xcd_remap((int)blockIdx.x, G) : 0;
+  const int s_beg = SK ? 2 * (int)(lg * P / G) : 0;
+  const int s_end = SK ? 2 * (int)((lg + 1) * P / G) : (tiles - (int)blockIdx.x + G - 1) / G;
+  auto owner = [&](int pair) { return (int)(((pair + 1LL) * G - 1) / P); };  // SK: logical wg of a unit pair
+  // position -> tile t (grouped-raster index) and k-double range [kb, kb + len), len even (SK) and >= 2
+  auto segment = [&](int s, int& t, int& kb, int& len) {
+    if constexpr (SK) {
+      t = s / nd;
+      kb = s - t * nd;
+      len = min(s_end, (t + 1) * nd) - s;
+    } else {
+      t = xcd_remap((int)blockIdx.x + s * G, tiles);
+      kb = 0;
+      len = nd;
+    }
+  };
+  auto raster = [&](int t, int& m0, int& n0) {
     constexpr int GM = 4;
-    const int group = wg / (GM * tiles_n);
+    const int group = t / (GM * tiles_n);
     const int first_m = group * GM;
     const int gsz = min(tiles_m - first_m, GM);
-    const int pin = wg % (GM * tiles_n);
+    const int pin = t % (GM * tiles_n);
     m0 = (first_m + pin % gsz) * LBM;
     n0 = (pin / gsz) * LBN;
   };
@@ -790,21 +836,23 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
   using OddT = std::integral_constant<bool, true>;
   auto sl = [](int q) { return q % 5; };
 
-  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2
-  int m0, n0;
-  coords(0, m0, n0);
+  int s = s_beg;
+  if (s >= s_end) return;  // (the host sizes the grid so that every run is non-empty)
+  int t, kb, len, m0, n0;
+  segment(s, t, kb, len);
+  raster(t, m0, n0);
   int ca[8], cb[8], xa[8], xb[8];
   offsets(m0, n0, ca, cb);
   asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {  // parts A0 B0 A1 B1 -> slots 0..3
+  for (int q = 0; q < 4; ++q) {  // parts A(kb) B(kb) A(kb+1) B(kb+1) -> slots 0..3
     char* dst = smem + q * kPart + wid * 8192;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(q & 1 ? rb : ra, GAI_LDS(dst + j * 1024), 16, q & 1 ? cb[j] : ca[j],
-                                               (q >> 1) * 128, 0, 0);
+                                               (kb + (q >> 1)) * 128, 0, 0);
   }
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double kb landed
   barrier();
   bf16x8 a0[8], b0[8], a1[8], b1[8];
 #pragma unroll
@@ -813,30 +861,111 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
   for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + kPart + b_rd0 + j * 2048);
   __builtin_amdgcn_s_waitcnt(0xC07F);
 
-  for (int it = 0, gd = 0; it < n_my; ++it, gd += nd) {
-    int nm0 = m0, nn0 = n0;
-    if (it + 1 < n_my) coords(it + 1, nm0, nn0);
+  for (int gd = 0; s < s_end;) {
+    // next segment's sources; past the last one, dummy re-loads of this segment's first double pair into a
+    // slot no later phase reads
+    const int sn = SK ? s + len : s + 1;
+    int tn = t, kbn = kb, lenn = len, nm0 = m0, nn0 = n0;
+    if (sn < s_end) {
+      segment(sn, tn, kbn, lenn);
+      raster(tn, nm0, nn0);
+    }
     offsets(nm0, nn0, xa, xb);
     int D = 0;
-    for (; D < nd - 2; ++D) {
+    for (; D < len - 2; ++D) {
       const int q = 2 * (gd + D);
-      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), ca, D + 2);
-      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), cb, D + 2);
+      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), ca, kb + D + 2);
+      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), cb, kb + D + 2);
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e, ++D) {
       const int q = 2 * (gd + D);
-      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), xa, e);
-      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), xb, e);
+      phase(EvenT{}, a0, b0, a1, b1, sl(q), sl(q + 1), sl(q + 4), xa, kbn + e);
+      phase(OddT{}, a1, b1, a0, b0, sl(q + 2), sl(q + 3), sl(q + 5), xb, kbn + e);
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
-    for_each_const<8>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      f32x4 row[8];
-      read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
-      epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
-    });
+    bool epi = true;
+    if constexpr (SK) {
+      if (kb != 0 || len != nd) {  // split tile: hand the partial over, or (last ticket) sum them into the AGPRs
+        const int hp = nd / 2;
+        const int cf = owner(t * hp), cl = owner(t * hp + hp - 1);
+        int* ctr = cnt + t * 4 + wid;
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
+        // (contributor c, slot, this wave, fragment ij) -> scalar byte offset; the lane's 16 B is the one voffset
+        const unsigned vo = lane * 16;
+        auto woff = [&](int c, int slot, int ij) {
+          return (unsigned)__builtin_amdgcn_readfirstlane(((c * 2 + slot) * 4 + wid) * (kSkQuad * 4) + ij * 1024);
+        };
+        bool last = false;
+        if (kb == 0)  // first contributor: everyone else (who started their runs here) is usually done
+          last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
+                 cl - cf;
+        if (!last) {
+          const int slot = kb == 0 ? 1 : 0;
+          for_each_const<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            f32x4 row[8];
+            read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, row[j]), rw,
+                  vo, woff(lg, slot, i * 8 + j), 16);
+          });
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partial has landed
+          int tk = 0;
+          if (lane == 0) tk = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = __builtin_amdgcn_readfirstlane(tk) == cl - cf;
+        }
+        if (last) {
+          if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+          // sum in contributor order (this wave's own value in its place), 4 fragments at a time, back into the AGPRs
+          for_each_const<16>([&](auto qc) {
+            constexpr int q4 = decltype(qc)::value;
+            f32x4 own[4], pre[4];
+            read_acc_tile<16 * q4 + 0>(own[0]);
+            read_acc_tile<16 * q4 + 4>(own[1]);
+            read_acc_tile<16 * q4 + 8>(own[2]);
+            read_acc_tile<16 * q4 + 12>(own[3]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pre[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int c = cf; c < lg; ++c) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                pre[j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, c == cf, 4 * q4 + j), 16));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) own[j] = pre[j] + own[j];
+            for (int c = lg + 1; c <= cl; ++c) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                own[j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, 0, 4 * q4 + j), 16));
+            }
+            write_acc_tile<16 * q4 + 0>(own[0]);
+            write_acc_tile<16 * q4 + 4>(own[1]);
+            write_acc_tile<16 * q4 + 8>(own[2]);
+            write_acc_tile<16 * q4 + 12>(own[3]);
+          });
+          asm volatile("s_nop 7" ::: "memory");
+        }
+        epi = last;
+      }
+    }
+    if (epi) {
+      for_each_const<8>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        f32x4 row[8];
+        read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
+        epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+      });
+    }
     asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+    gd += len;
+    s = sn;
+    t = tn;
+    kb = kbn;
+    len = lenn;
     m0 = nm0;
     n0 = nn0;
 #pragma unroll
@@ -1002,6 +1131,87 @@ void launch_w4r(const void* A, const void* B, void* C, const void* bias, const v
   GAI_LAUNCH_CHECK();
 }
 
+// Stream-K workspace of one (device, stream): partial quadrants [G][2][4][16384] fp32 and per-(tile, wave)
+// tickets. Two streams never share one (their launches could overlap). Grown outside graph capture only;
+// a captured launch that would need a bigger one takes the tile walk instead.
+struct SkWorkspace {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  size_t ws_bytes = 0, cnt_n = 0;
+};
+
+bool sk_workspace(hipStream_t st, size_t ws_bytes, size_t cnt_n, SkWorkspace& out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> pool;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(mu);
+  SkWorkspace& w = pool[{dev, st}];
+  if (w.ws_bytes < ws_bytes || w.cnt_n < cnt_n) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    if (hipStreamSynchronize(st) != hipSuccess) return false;  // earlier launches may still use the old one
+    if (w.ws) (void)hipFree(w.ws);
+    if (w.cnt) (void)hipFree(w.cnt);
+    w = SkWorkspace{};
+    const size_t nb = std::max(ws_bytes, w.ws_bytes), nc = std::max<size_t>(cnt_n, 4096);
+    if (hipMalloc(&w.ws, nb) != hipSuccess) return false;
+    if (hipMalloc(&w.cnt, nc * sizeof(int)) != hipSuccess || hipMemset(w.cnt, 0, nc * sizeof(int)) != hipSuccess) {
+      (void)hipFree(w.ws);
+      w = SkWorkspace{};
+      return false;
+    }
+    w.ws_bytes = nb;
+    w.cnt_n = nc;
+  }
+  out = w;
+  return true;
+}
+
+int sk_grid() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      gai_launch_error(__FILE__, __LINE__, "gemm_w4s: cannot query the CU count");
+  }
+  return ncu & ~7;
+}
+
+// The stream-K walk pays where the tile walk's last wave leaves > 15 % of the grid idle (2406-token prefill:
+// O / down 38 %, gate_up 12.5 % -> tile walk; M = 16384: 0 %). Needs K % 128 == 0 (whole unit pairs).
+bool sk_pays(int M, int N, int K) {
+  if (K % 128) return false;
+  const int G = sk_grid();
+  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+  const int waves = (tiles + G - 1) / G;
+  return (long long)(waves * G - tiles) * 100 > 15LL * G;
+}
+
+template <int EPI, bool OUTF32>
+bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                hipStream_t st) {
+  if (K % 128) return false;
+  static bool once = false;
+  if (!once) {
+    set_max_lds(gemm_w4r_kernel<EPI, OUTF32, true>);
+    once = true;
+  }
+  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+  const long long pairs = (long long)tiles * (K / 128);
+  // every run non-empty (pairs >= G); a multiple of 8 keeps the logical -> XCD map contiguous
+  const int grid = (int)std::min<long long>(sk_grid(), pairs) & ~7;
+  if (grid < 8) return false;
+  SkWorkspace w;
+  if (!sk_workspace(st, (size_t)grid * 2 * 4 * kSkQuad * sizeof(float), (size_t)tiles * 4, w)) return false;
+  gemm_w4r_kernel<EPI, OUTF32, true><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                   (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
+                                                                   w.ws, w.cnt);
+  GAI_LAUNCH_CHECK();
+  return true;
+}
+
 template <int MT, int NF, int EPI, bool OUTF32>
 void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                       int ldc, hipStream_t st) {
@@ -1042,11 +1252,13 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force == 8 || force == 9 || force == 10 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force >= 8 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
     if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    if ((force == 11 || (force == 0 && sk_pays(M, N, K))) && launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st))
+      return;
     // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
     // part ring's longer A-operand latency cover wins (+7 % / +1-5 %); otherwise the double-slot kernel
     // (+2-4 % on O / e5), profiles/r2/gemm_w4r.jsonl, gemm_rule.jsonl, gemm_w4p_ab.jsonl

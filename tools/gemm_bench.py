@@ -1,8 +1,9 @@
 """Prefill GEMM A/B: the hand-written persistent kernels (w4p / w4d / w4r) vs hipBLASLt (default + tuned table) on the
-Llama-3-8B projection shapes at M = 16384 (one 16K-token prefill chunk), random operands, interleaved
+Llama-3-8B projection shapes at M = 16384 (one 16K-token prefill chunk; --m 2406 = one RAG query), plus the
+stream-K walk (w4s) and the 128x128 tiled kernel, random operands, interleaved
 rounds in one process (cdna_hip_programming §5.4 rules 24/25). One JSON line per shape.
 
-usage: python tools/gemm_bench.py [--m 16384] [--rounds 5] [--out FILE]
+usage: python tools/gemm_bench.py [--m 16384[,2406,...]] [--rounds 5] [--out FILE]
 """
 import argparse
 import json
@@ -34,22 +35,23 @@ def timeit(fn, iters=10):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--m", type=int, default=16384)
+    ap.add_argument("--m", default="16384", help="comma-separated M values")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     nat = ops.native()
     rows = []
-    for name in a.shapes.split(","):
+    for M, name in [(int(m), n) for m in str(a.m).split(",") for n in a.shapes.split(",")]:
         N, K = SHAPES[name]
-        M = a.m
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         arms = {"w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
                 "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
                 "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
+                "w4s": lambda: nat.gemm(x, w, out, None, None, 0, 11),
+                "tiled": lambda: nat.gemm(x, w, out, None, None, 0, 2),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
         for _ in range(a.rounds):
@@ -61,11 +63,10 @@ def main():
             v.sort()
             r[f"{k}_ms"] = round(v[len(v) // 2], 4)
             r[f"{k}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
-        r["ring_vs_blas"] = round(r["hipblaslt_ms"] / r["ring_ms"], 3)
-        r["w4_vs_blas"] = round(r["hipblaslt_ms"] / r["w4_ms"], 3)
         r["w4p_vs_blas"] = round(r["hipblaslt_ms"] / r["w4p_ms"], 3)
         r["w4d_vs_blas"] = round(r["hipblaslt_ms"] / r["w4d_ms"], 3)
         r["w4r_vs_blas"] = round(r["hipblaslt_ms"] / r["w4r_ms"], 3)
+        r["w4s_vs_blas"] = round(r["hipblaslt_ms"] / r["w4s_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if enable_tuned_blas():
