@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
         auto woff = [&](int c, int slot, int ij) {
           return (unsigned)__builtin_amdgcn_readfirstlane(((c * 2 + slot) * 4 + wid) * (kSkQuad * 4) + ij * 1024);
         };
-        bool last = false;
+        bool last = false, stored = false;
         if (kb == 0)  // first contributor: everyone else (who started their runs here) is usually done
           last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
                  cl - cf;
@@ -913,6 +913,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
                   vo, woff(lg, slot, i * 8 + j), 16);
           });
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partial has landed
+          stored = true;
           int tk = 0;
           if (lane == 0) tk = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           last = __builtin_amdgcn_readfirstlane(tk) == cl - cf;
@@ -920,33 +921,45 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
         if (last) {
           if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-          // sum in contributor order (this wave's own value in its place), 4 fragments at a time, back into the AGPRs
-          for_each_const<16>([&](auto qc) {
-            constexpr int q4 = decltype(qc)::value;
-            f32x4 own[4], pre[4];
-            read_acc_tile<16 * q4 + 0>(own[0]);
-            read_acc_tile<16 * q4 + 4>(own[1]);
-            read_acc_tile<16 * q4 + 8>(own[2]);
-            read_acc_tile<16 * q4 + 12>(own[3]);
+          // sum in contributor order into the AGPRs: after a successful peek they hold the first term (this wave's
+          // own, never stored); after the last ticket every partial, this wave's included, is in the workspace
+          int c0 = cf + 1;
+          if (stored) {
+            asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
+            c0 = cf;
+          }
+          // 16-fragment batches; the next batch's 16 loads are in flight while one is added (a serial walk pays one
+          // memory latency per few fragments: measured 0.62 vs 1.0 PF/s for the whole GEMM)
+          f32x4 bufa[16], bufb[16];
+          auto load_batch = [&](int c, int b, f32x4 (&buf)[16]) {
+            const int slot = c == cf ? 1 : 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) pre[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int c = cf; c < lg; ++c) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                pre[j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, c == cf, 4 * q4 + j), 16));
+            for (int j = 0; j < 16; ++j)
+              buf[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, slot, 16 * b + j), 16));
+          };
+          auto add_batch = [&](auto bc, const f32x4 (&buf)[16]) {
+            constexpr int b = decltype(bc)::value;
+            for_each_const<16>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              f32x4 v;
+              read_acc_tile<4 * (16 * b + j)>(v);
+              v += buf[j];
+              write_acc_tile<4 * (16 * b + j)>(v);
+            });
+          };
+          if (c0 <= cl) {
+            load_batch(c0, 0, bufa);
+            for (int c = c0; c <= cl; ++c) {
+              load_batch(c, 1, bufb);
+              add_batch(std::integral_constant<int, 0>{}, bufa);
+              load_batch(c, 2, bufa);
+              add_batch(std::integral_constant<int, 1>{}, bufb);
+              load_batch(c, 3, bufb);
+              add_batch(std::integral_constant<int, 2>{}, bufa);
+              if (c < cl) load_batch(c + 1, 0, bufa);
+              add_batch(std::integral_constant<int, 3>{}, bufb);
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) own[j] = pre[j] + own[j];
-            for (int c = lg + 1; c <= cl; ++c) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                own[j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, 0, 4 * q4 + j), 16));
-            }
-            write_acc_tile<16 * q4 + 0>(own[0]);
-            write_acc_tile<16 * q4 + 4>(own[1]);
-            write_acc_tile<16 * q4 + 8>(own[2]);
-            write_acc_tile<16 * q4 + 12>(own[3]);
-          });
+          }
           asm volatile("s_nop 7" ::: "memory");
         }
         epi = last;
@@ -1180,12 +1193,15 @@ int sk_grid() {
 }
 
 // The stream-K walk pays where the tile walk's last wave leaves > 15 % of the grid idle (2406-token prefill:
-// O / down 38 %, gate_up 12.5 % -> tile walk; M = 16384: 0 %). Needs K % 128 == 0 (whole unit pairs).
+// O / down 38 %, gate_up 12.5 % -> tile walk; M = 16384: 0 %) and every workgroup still gets >= 32 k-doubles
+// (~45 us of MFMA work) to amortise its partial hand-off (the e5 projections at K = 1024 get 10: tile walk).
+// Needs K % 128 == 0 (whole unit pairs).
 bool sk_pays(int M, int N, int K) {
   if (K % 128) return false;
   const int G = sk_grid();
   const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
   const int waves = (tiles + G - 1) / G;
+  if ((long long)tiles * (K / 64) < 32LL * G) return false;
   return (long long)(waves * G - tiles) * 100 > 15LL * G;
 }
 

@@ -26,6 +26,9 @@ constexpr int kGvWaves = 8;
 constexpr int kGvThreads = 64 * kGvWaves;
 constexpr int kPiece = 512;  // K elements of one wave load (64 lanes x 8 bf16)
 constexpr int kG = 4;        // pieces per row per pipeline group
+// dynamic LDS cap: the 160 KiB of a CU minus the kernel's static reduction arrays (asking for all 160 KiB fails the
+// attribute call, and its error would surface at the next launch check)
+constexpr int kGvMaxDyn = 160 * 1024 - 1024;
 
 enum { GV_PLAIN = 0, GV_RESIDUAL = 1, GV_SWIGLU = 2, GV_ROPE = 3, GV_F32 = 4 };
 
@@ -237,7 +240,7 @@ void gemv_launch(const GemvArgs& a, hipStream_t st) {
     static bool once = false;                                                                                 \
     if (!once) {                                                                                              \
       hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_kernel<MRV, EPI>),                              \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kGvMaxDyn);                             \
       once = true;                                                                                            \
     }                                                                                                         \
     gemv_kernel<MRV, EPI><<<grid, kGvThreads, lds, st>>>(a);                                                  \
@@ -256,7 +259,7 @@ void gemv_launch(const GemvArgs& a, hipStream_t st) {
 
 int gai_gemv_ok(int M, int N, int K, int normed) {
   if (M < 1 || M > 4 || N % 2 || K % (kPiece * kG)) return 0;
-  if ((size_t)M * K * sizeof(bf16) > 160 * 1024) return 0;
+  if ((size_t)M * K * sizeof(bf16) > (size_t)kGvMaxDyn) return 0;
   if (normed && K > 2 * 8 * kGvThreads) return 0;
   return 1;
 }

@@ -484,7 +484,8 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ multi-step decode
     def _multi_step_capable(self) -> bool:
-        return (self.cfg.decode_steps > 1 and not hasattr(self.model, "graph_static_inputs")
+        # EP lockstep steps one token at a time: every rank must enter the same number of exchanges per step
+        return (self.cfg.decode_steps > 1 and self.ep_group is None and not hasattr(self.model, "graph_static_inputs")
                 and not getattr(self.model, "lora_names", None))
 
     def _capture_multi(self, bs: int):
@@ -701,7 +702,11 @@ class LLMEngine:
         """(plan, seq_order) of a one-token step: a captured decode graph when the batch is pure decode and
         fits a bucket, otherwise an eager (prefill / mixed) forward. Sampling parameters ride along."""
         P, nd = b.num_prefill_tokens, len(b.decode_seq_ids)
-        if (P == 0 and self.device.type == "cuda" and self.cfg.use_graphs
+        # EP lockstep: a pure-decode rank replays its graph only in a step every rank agreed to graph (_ep_bucket);
+        # while a peer prefills, every rank runs eager with the exact-count exchange (the captured peer-memory
+        # all-to-all would wait for a rank that is inside a different collective)
+        ep_ok = self.ep_group is None or self._ep_bucket is not None
+        if (P == 0 and ep_ok and self.device.type == "cuda" and self.cfg.use_graphs
                 and self._graph_bucket(max(nd, self._ep_bucket or 0)) is not None):
             seq_order = [int(x) for x in b.decode_seq_ids]
             plan = dict(op="graph", n=nd, arr=[b.token_ids, b.positions, b.slots, b.decode_ctx,

@@ -107,16 +107,17 @@ def test_stream_k_split_tiles(cuda, M, N, K, act):
     x = torch.randint(-2, 3, (M, K), device=cuda).to(torch.bfloat16)
     w = torch.randint(-2, 3, (N, K), device=cuda).to(torch.bfloat16)
     res = torch.randint(-8, 9, (M, N), device=cuda).to(torch.bfloat16) if act == "residual" else None
-    y = _run(x, w, None, res, act, torch.float32, force=11)
+    out_dtype = torch.bfloat16 if act == "swiglu" else torch.float32  # the SwiGLU epilogue writes bf16
+    y = _run(x, w, None, res, act, out_dtype, force=11)
     acc = x.float().cpu() @ w.float().cpu().t()
     if act == "swiglu":
         g = acc.view(M, N // 32, 2, 16)
         ref_y = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, N // 2)
-        torch.testing.assert_close(y.cpu(), ref_y, rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(y.float().cpu(), ref_y, rtol=1e-2, atol=1e-2)
     else:
         assert torch.equal(y.cpu(), acc + (0 if res is None else res.float().cpu()))
     for _ in range(5):
-        assert torch.equal(_run(x, w, None, res, act, torch.float32, force=11), y)
+        assert torch.equal(_run(x, w, None, res, act, out_dtype, force=11), y)
 
 
 @pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(1024, 512, 4, 2, False), (1300, 4096, 32, 8, False),
@@ -144,7 +145,9 @@ def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
                                              torch.empty(0, device=cuda), False, None)
         else:
             qkv = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-            ops.native().gemm(x, w, qkv, bias, None, ops.EPI["bias"] if with_bias else 0, 0)
+            # the fused kernel's tile walk (w4d): same accumulation order (the auto policy may pick the stream-K
+            # walk, whose partial sums round differently)
+            ops.native().gemm(x, w, qkv, bias, None, ops.EPI["bias"] if with_bias else 0, KERNELS["w4d"])
             ops.rope_kv_write(qkv, pos, cs, slots, q, kc, vc, Hq, Hkv, D, True)
         outs.append((q, kc, vc))
     # same accumulators and roundings; hipcc may contract the rotation's mul-sub into an FMA differently at
