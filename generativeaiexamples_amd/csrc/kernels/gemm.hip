@@ -1192,18 +1192,20 @@ int sk_grid() {
   return ncu & ~7;
 }
 
-// The stream-K walk pays where the tile walk's last wave leaves > 15 % of the grid idle (2406-token prefill:
-// O / down 38 %, gate_up 12.5 % -> tile walk; M = 16384: 0 %) and every workgroup still gets >= 32 k-doubles
-// (~45 us of MFMA work) to amortise its partial hand-off (the e5 projections at K = 1024 get 10: tile walk).
-// Needs K % 128 == 0 (whole unit pairs).
-bool sk_pays(int M, int N, int K) {
-  if (K % 128) return false;
-  const int G = sk_grid();
-  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
-  const int waves = (tiles + G - 1) / G;
-  if ((long long)tiles * (K / 64) < 32LL * G) return false;
-  return (long long)(waves * G - tiles) * 100 > 15LL * G;
-}
+int ring_tiles(int M, int N) { return ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN); }
+
+// Auto policy of the 256x256 kernels (profiles/r4/gemm_policy: Llama-3-8B projections at M = 512 / 1024 / 2406,
+// interleaved rounds against the 128x128 tiled kernel):
+//  * tile walk when its tiles fill at least half of the grid (M = 2406: 160-1120 tiles, 1.0-1.3 PF/s vs 0.8-0.95
+//    tiled; M = 512 gate_up: 224 tiles, 1.29 vs 0.87 PF/s);
+//  * stream-K walk when they do not and K is deep (down at M = 512 / 1024: 32 / 64 tiles, 0.79 / 1.15 PF/s vs
+//    0.40 / 0.74 tiled, 0.26 / 0.51 tile walk); at K = 4096 the tiled kernel wins there (O at M = 1024: 0.72 vs
+//    0.66 stream-K);
+//  * never stream-K just to fill the last wave of a well-filled walk: its runs reach the tiles at unrelated k
+//    offsets, so the 32 workgroups of an XCD no longer stream the same k-window through their L2 (O at M = 2406:
+//    0.64 PF/s stream-K vs 1.0 tile walk, although the walk leaves 38 % of the CUs idle).
+bool sk_auto(int M, int N, int K) { return K >= 8192 && K % 128 == 0 && 2 * ring_tiles(M, N) < sk_grid(); }
+bool ring_auto(int M, int N, int K) { return M >= 256 && (2 * ring_tiles(M, N) >= sk_grid() || sk_auto(M, N, K)); }
 
 template <int EPI, bool OUTF32>
 bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
@@ -1268,12 +1270,12 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
-  if (force >= 8 || (force == 0 && M >= 1024 && N >= 256 && ring_ok)) {
+  if (force >= 8 || (force == 0 && N >= 256 && ring_ok && ring_auto(M, N, K))) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
     if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if ((force == 11 || (force == 0 && sk_pays(M, N, K))) && launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st))
+    if ((force == 11 || (force == 0 && sk_auto(M, N, K))) && launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st))
       return;
     // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
     // part ring's longer A-operand latency cover wins (+7 % / +1-5 %); otherwise the double-slot kernel

@@ -851,10 +851,12 @@ def ep_gpu_rehearsal_worker(rank, world, port, out_dir):
                 t.copy_(src)
         assert m.ep_xchg is not None, "peer-memory all-to-all not created"
         tok = small_byte_tokenizer(4096)
-        ecfg = dict(num_blocks=160, max_model_len=256, use_graphs=True, max_num_seqs=8, max_batched_tokens=64,
+        graphs = os.environ.get("GAI_EP_REHEARSE_GRAPHS", "1") == "1"  # "0": eager decode (A/B of a failure)
+        ecfg = dict(num_blocks=160, max_model_len=256, use_graphs=graphs, max_num_seqs=8, max_batched_tokens=64,
                     prefill_chunk=32, prefix_cache=False, graph_batch_sizes=(1, 2, 4, 8), kv_memory_fraction=0.02)
         eng = LLMEngine(m, tok, EngineConfig(**ecfg))
-        eng.capture_graphs(max_bs=8)
+        if graphs:
+            eng.capture_graphs(max_bs=8)
         progress(f"graphs captured {sorted(eng.graphs)}")
         n_req = 1 + 2 * rank  # ranks carry different loads: idle ranks replay padding-only graphs
         prompts = [list(range(11 + 5 * rank + 3 * i, 11 + 5 * rank + 3 * i + 7 + 9 * ((i + rank) % 3)))
@@ -874,7 +876,9 @@ def ep_gpu_rehearsal_worker(rank, world, port, out_dir):
                 total += 1
                 row = lg[i]
                 if float(row[t]) < float(row.max()) - 0.02 * max(1.0, float(row.abs().max())):
-                    bad.append((i, t, int(row.argmax())))
+                    # (position, token, fp32 argmax, logit gap, tolerance, step kinds seen so far)
+                    bad.append((i, t, int(row.argmax()), round(float(row.max() - row[t]), 4),
+                                round(0.02 * max(1.0, float(row.abs().max())), 4)))
         with open(os.path.join(out_dir, f"epg_{rank}.json"), "w") as f:
             json.dump({"bad": bad, "total": total, "stats": dict(eng.stats), "graphs": sorted(eng.graphs),
                        "lens": [len(r.output_ids) for r in reqs], "err": int(m.ep_xchg.err.item())}, f)

@@ -3,6 +3,7 @@ decode steps are captured HIP graphs whose token exchanges are the peer-memory o
 (csrc/comm/custom_ar.hip) between the native EP pack / combine kernels (moe.hip). Every rank's greedy tokens must
 be fp32-consistent with a single-rank Mixtral of the same weights."""
 import json
+import os
 import socket
 import time
 
@@ -47,12 +48,15 @@ def test_ep_decode_graph_one_gpu(tmp_path, world, cuda):
     errs = [f.read_text() for f in tmp_path.glob("epg_err_*.txt")]
     assert not errs, errs[0]
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    for r in range(world):
-        res = json.loads((tmp_path / f"epg_{r}.json").read_text())
+    results = [json.loads((tmp_path / f"epg_{r}.json").read_text()) for r in range(world)]
+    for r, res in enumerate(results):  # every rank's record first, then the checks
         print(f"EP={world} rank {r}: {res['total'] - len(res['bad'])}/{res['total']} tokens fp32-consistent, "
-              f"stats {res['stats']}, err {res['err']}")
+              f"stats {res['stats']}, err {res['err']}, bad (pos, tok, argmax, gap, tol) {res['bad'][:6]}")
+    graphs = os.environ.get("GAI_EP_REHEARSE_GRAPHS", "1") == "1"
+    for r, res in enumerate(results):
         assert res["err"] == 0
-        assert res["graphs"], "no decode graph captured"
-        assert res["stats"]["graph_steps"] > 0, "decode never replayed a graph"
+        if graphs:
+            assert res["graphs"], "no decode graph captured"
+            assert res["stats"]["graph_steps"] > 0, "decode never replayed a graph"
         assert not res["bad"], res["bad"][:5]
         assert res["lens"] == [6 + 4 * r] * (1 + 2 * r)

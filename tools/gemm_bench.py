@@ -47,7 +47,8 @@ def main():
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        arms = {"w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
+        arms = {"auto": lambda: nat.gemm(x, w, out, None, None, 0, 0),
+                "w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
                 "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
                 "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
                 "w4s": lambda: nat.gemm(x, w, out, None, None, 0, 11),
