@@ -8,7 +8,7 @@
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I generativeaiexamples_amd/csrc/include \
 //          -o /tmp/gemm_w4p_ab tools/microbench/gemm_w4p_ab.hip
 #define GAI_GEMM_KERNELS_ONLY
-#include "../../generativeaiexamples_amd/csrc/kernels/gemm.hip"
+#include "../../generativeaiexamples_amd/csrc/kernels/gemm_impl.h"
 
 #include <cstdio>
 #include <cstdlib>
