@@ -26,6 +26,7 @@
 #include "gai_rope.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -737,34 +738,54 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
 // at the start of theirs, so it first peeks the counter and usually sums without storing its own.
 // Workspace [G][2 slots][4 waves][16384] fp32 (slot 0: a run's unaligned first segment, slot 1: a first
 // contributor that was not last); counters [tiles][4], zero between launches (the last ticket resets its own).
+//
+// WALK = 2: the split walk. Stream-K's runs reach their tiles at unrelated k offsets, so the 32 workgroups of an XCD
+// stop streaming one k-window through their shared L2 (O at M = 2406: 0.64 PF/s stream-K vs 1.0 tile walk). Here
+// every tile is cut into S k-parts (even double counts) and the walk goes over the S x tiles items part-major,
+// through the same XCD remap as the tile walk: the items a wave of workgroups runs together are neighbouring tiles
+// at the SAME part, all starting at its first double, so they share their k-windows in L2 exactly as the tile walk
+// does, while S x tiles items fill the grid's last wave far better (160 tiles, S = 3: 480 items = 94 % of two
+// waves instead of 62 % of one). Every part stores its quadrants (slot = item) and draws the (tile, wave)
+// ticket; the last one sums the S parts in part order.
 // ----------------------------------------------------------------------------------------------
 constexpr int kPart = 256 * 64 * 2;  // one operand of a double unit
 
 constexpr int kSkQuad = 128 * 128;  // fp32 of one wave's quadrant partial
 
-template <int EPI, bool OUTF32, bool SK = false>
+template <int EPI, bool OUTF32, int WALK = 0>
 __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc, float* ws = nullptr, int* cnt = nullptr) {
+                                                          int K, int ldc, float* ws = nullptr, int* cnt = nullptr,
+                                                          int S = 1) {
+  constexpr bool SK = WALK == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 5 parts x 32 KiB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
   const int tiles = tiles_m * tiles_n;
   const int G = gridDim.x;
-  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2 (SK: K % 128 == 0)
+  const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2 (WALK 1 / 2: K % 128 == 0; WALK 2: S <= nd / 2)
+  const int hp = nd / 2;
+  const int items = WALK == 2 ? tiles * S : tiles;
   // walk positions: tile walk index it (tile blockIdx.x + it * G through the XCD remap), or SK unit index
   const long long P = (long long)tiles * (nd / 2);  // SK: unit pairs
   const int lg = SK ? xcd_remap((int)blockIdx.x, G) : 0;
   const int s_beg = SK ? 2 * (int)(lg * P / G) : 0;
-  const int s_end = SK ? 2 * (int)((lg + 1) * P / G) : (tiles - (int)blockIdx.x + G - 1) / G;
+  const int s_end = SK ? 2 * (int)((lg + 1) * P / G) : (items - (int)blockIdx.x + G - 1) / G;
   auto owner = [&](int pair) { return (int)(((pair + 1LL) * G - 1) / P); };  // SK: logical wg of a unit pair
-  // position -> tile t (grouped-raster index) and k-double range [kb, kb + len), len even (SK) and >= 2
-  auto segment = [&](int s, int& t, int& kb, int& len) {
+  // position -> tile t (grouped-raster index), k-double range [kb, kb + len) (len even for WALK 1 / 2, >= 2) and
+  // (WALK 2) the part pt
+  auto segment = [&](int s, int& t, int& kb, int& len, int& pt) {
     if constexpr (SK) {
       t = s / nd;
       kb = s - t * nd;
       len = min(s_end, (t + 1) * nd) - s;
+    } else if constexpr (WALK == 2) {
+      const int item = xcd_remap((int)blockIdx.x + s * G, items);
+      pt = item / tiles;
+      t = item - pt * tiles;
+      kb = 2 * ((pt * hp) / S);
+      len = 2 * (((pt + 1) * hp) / S) - kb;
     } else {
       t = xcd_remap((int)blockIdx.x + s * G, tiles);
       kb = 0;
@@ -841,8 +862,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
 
   int s = s_beg;
   if (s >= s_end) return;  // (the host sizes the grid so that every run is non-empty)
-  int t, kb, len, m0, n0;
-  segment(s, t, kb, len);
+  int t, kb, len, m0, n0, pt = 0;
+  segment(s, t, kb, len, pt);
   raster(t, m0, n0);
   int ca[8], cb[8], xa[8], xb[8];
   offsets(m0, n0, ca, cb);
@@ -868,9 +889,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
     // next segment's sources; past the last one, dummy re-loads of this segment's first double pair into a
     // slot no later phase reads
     const int sn = SK ? s + len : s + 1;
-    int tn = t, kbn = kb, lenn = len, nm0 = m0, nn0 = n0;
+    int tn = t, kbn = kb, lenn = len, nm0 = m0, nn0 = n0, ptn = pt;
     if (sn < s_end) {
-      segment(sn, tn, kbn, lenn);
+      segment(sn, tn, kbn, lenn, ptn);
       raster(tn, nm0, nn0);
     }
     offsets(nm0, nn0, xa, xb);
@@ -888,23 +909,25 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
     bool epi = true;
-    if constexpr (SK) {
-      if (kb != 0 || len != nd) {  // split tile: hand the partial over, or (last ticket) sum them into the AGPRs
-        const int hp = nd / 2;
-        const int cf = owner(t * hp), cl = owner(t * hp + hp - 1);
+    if constexpr (WALK != 0) {
+      if (SK ? (kb != 0 || len != nd) : S > 1) {  // split tile: hand the partial over, or (last ticket) sum them
+        // contributors cf..cl (stream-K: logical workgroups, this one = lg; split: the parts, this one = pt)
+        const int cf = SK ? owner(t * hp) : 0, cl = SK ? owner(t * hp + hp - 1) : S - 1;
+        const int me = SK ? lg : pt;
         int* ctr = cnt + t * 4 + wid;
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
-        // (contributor c, slot, this wave, fragment ij) -> scalar byte offset; the lane's 16 B is the one voffset
+        // (contributor c, this wave, fragment ij) -> scalar byte offset; the lane's 16 B is the one voffset.
+        // Quadrant slot: stream-K [workgroup][first-contributor?], split [part][tile]
         const unsigned vo = lane * 16;
-        auto woff = [&](int c, int slot, int ij) {
-          return (unsigned)__builtin_amdgcn_readfirstlane(((c * 2 + slot) * 4 + wid) * (kSkQuad * 4) + ij * 1024);
+        auto woff = [&](int c, int ij) {
+          const int q = SK ? c * 2 + (c == cf ? 1 : 0) : c * tiles + t;
+          return (unsigned)__builtin_amdgcn_readfirstlane((q * 4 + wid) * (kSkQuad * 4) + ij * 1024);
         };
         bool last = false, stored = false;
-        if (kb == 0)  // first contributor: everyone else (who started their runs here) is usually done
+        if (SK && kb == 0)  // stream-K first contributor: everyone else (who started their runs here) is usually done
           last = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
                  cl - cf;
         if (!last) {
-          const int slot = kb == 0 ? 1 : 0;
           for_each_const<8>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             f32x4 row[8];
@@ -913,7 +936,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
             for (int j = 0; j < 8; ++j)
               __builtin_amdgcn_raw_buffer_store_b128(
                   __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, row[j]), rw,
-                  vo, woff(lg, slot, i * 8 + j), 16);
+                  vo, woff(me, i * 8 + j), 16);
           });
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partial has landed
           stored = true;
@@ -935,10 +958,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
           // memory latency per few fragments: measured 0.62 vs 1.0 PF/s for the whole GEMM)
           f32x4 bufa[16], bufb[16];
           auto load_batch = [&](int c, int b, f32x4 (&buf)[16]) {
-            const int slot = c == cf ? 1 : 0;
 #pragma unroll
             for (int j = 0; j < 16; ++j)
-              buf[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, slot, 16 * b + j), 16));
+              buf[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, woff(c, 16 * b + j), 16));
           };
           auto add_batch = [&](auto bc, const f32x4 (&buf)[16]) {
             constexpr int b = decltype(bc)::value;
@@ -982,6 +1004,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
     t = tn;
     kb = kbn;
     len = lenn;
+    pt = ptn;
     m0 = nm0;
     n0 = nn0;
 #pragma unroll
@@ -1195,7 +1218,7 @@ bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const v
   if (K % 128) return false;
   static bool once = false;
   if (!once) {
-    set_max_lds(gemm_w4r_kernel<EPI, OUTF32, true>);
+    set_max_lds(gemm_w4r_kernel<EPI, OUTF32, 1>);
     once = true;
   }
   const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
@@ -1205,9 +1228,51 @@ bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const v
   if (grid < 8) return false;
   SkWorkspace w;
   if (!sk_workspace(st, (size_t)grid * 2 * 4 * kSkQuad * sizeof(float), (size_t)tiles * 4, w)) return false;
-  gemm_w4r_kernel<EPI, OUTF32, true><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
+  gemm_w4r_kernel<EPI, OUTF32, 1><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
                                                                    (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
                                                                    w.ws, w.cnt);
+  GAI_LAUNCH_CHECK();
+  return true;
+}
+
+// Parts per tile of the split walk: the S in 2..8 (S <= K / 128) with the lowest modelled time, in k-doubles per
+// workgroup: waves x doubles per part, plus ~3.5 doubles per 256 KiB quadrant set a workgroup stores (each item)
+// or loads (the last part of a tile loads all S); 1 when no split beats the tile walk. GAI_GEMM_SPLIT_S overrides.
+int split_parts(int M, int N, int K) {
+  if (K % 128) return 1;
+  const int G = sk_grid(), T = ring_tiles(M, N), hp = K / 128;
+  static const int env = getenv("GAI_GEMM_SPLIT_S") ? atoi(getenv("GAI_GEMM_SPLIT_S")) : 0;
+  if (env > 0) return std::min(env, hp);
+  auto cost = [&](int S) {
+    const double waves = (double)((T * S + G - 1) / G);
+    const double dbl = 2.0 * ((hp + S - 1) / S);
+    return waves * dbl + (S > 1 ? 3.5 * (waves + (double)S * T / G) : 0.0);
+  };
+  int best = 1;
+  for (int S = 2; S <= std::min(8, hp); ++S)
+    if (cost(S) < cost(best)) best = S;
+  return best;
+}
+
+template <int EPI, bool OUTF32>
+bool launch_w4x(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
+                hipStream_t st, int S) {
+  if (K % 128 || S < 2 || S > K / 128) return false;
+  static bool once = false;
+  if (!once) {
+    set_max_lds(gemm_w4r_kernel<EPI, OUTF32, 2>);
+    once = true;
+  }
+  const int tiles = ring_tiles(M, N);
+  const long long items = (long long)tiles * S;
+  if (items * 4 * kSkQuad * sizeof(float) >= (1ull << 31)) return false;  // 32-bit workspace offsets
+  const int ncu = sk_grid();
+  const int grid = items <= ncu ? (int)items : ncu;
+  SkWorkspace w;
+  if (!sk_workspace(st, (size_t)items * 4 * kSkQuad * sizeof(float), (size_t)tiles * 4, w)) return false;
+  gemm_w4r_kernel<EPI, OUTF32, 2><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
+                                                                w.ws, w.cnt, S);
   GAI_LAUNCH_CHECK();
   return true;
 }
@@ -1258,6 +1323,8 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
     if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
       return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     if ((force == 11 || (force == 0 && sk_auto(M, N, K))) && launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st))
+      return;
+    if (force == 12 && launch_w4x<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, std::max(2, split_parts(M, N, K))))
       return;
     // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
     // part ring's longer A-operand latency cover wins (+7 % / +1-5 %); otherwise the double-slot kernel

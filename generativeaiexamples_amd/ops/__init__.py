@@ -56,7 +56,7 @@ def native_available() -> bool:
 
 
 EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6, "quick_gelu": 7}
-_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
+_GEMM_FORCE = {"auto": 0, "skinny": 1, "tiled": 2, "w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12}[os.environ.get("GAI_GEMM_KERNEL", "auto")]
 
 
 # ---------------------------------------------------------------------------------------------

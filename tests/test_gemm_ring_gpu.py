@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 # force codes in gai_gemm: persistent 4-wave ring (tile walk per CU), persistent full-line double-unit kernel, and
 # its 5-part LDS ring variant (the default for M >= 1024), and that ring on the stream-K walk (K % 128 == 0; forced
 # onto shapes with K % 128 != 0 it takes the tile walk)
-KERNELS = {"w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11}
+KERNELS = {"w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12}  # w4x: the split walk (k-parts per tile)
 
 SHAPES = [(1024, 256, 192), (1280, 1040, 256), (2048, 2304, 1024), (1100, 4096, 4096), (4096, 6144, 320),
           (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256)]  # last two: > 256 tiles, multi-tile walks
@@ -94,13 +94,15 @@ def test_ring_gemm_repeatable(cuda, M, N, K, kern):
     assert ((y0.float().cpu() - y_ref.float()).abs() <= 3e-2 + 2e-2 * y_ref.float().abs()).all()
 
 
+@pytest.mark.parametrize("walk", ["w4s", "w4x"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 8192), (300, 512, 1024), (2406, 4096, 14336), (1111, 1040, 640)])
 @pytest.mark.parametrize("act", [None, "residual", "swiglu"])
-def test_stream_k_split_tiles(cuda, M, N, K, act):
+def test_stream_k_split_tiles(cuda, M, N, K, act, walk):
     """Stream-K walk with tiles split many ways (64 contributors on the single tile of the first shape, 8 per tile
     on the second, the 2406-token down projection, odd tile edges on the last): small-integer operands make the
     fp32 partial sums exact, so any lost, doubled or misplaced partial quadrant shows as a wrong integer; then
-    launch-to-launch bit equality (the sum order does not depend on which contributor finishes last)."""
+    launch-to-launch bit equality (the sum order does not depend on which contributor finishes last). The split walk
+    (w4x) cuts each tile into up to 8 k-parts over the same hand-off."""
     if act == "swiglu" and N % 32:
         pytest.skip("SwiGLU weights interleave in 32-row groups")
     torch.manual_seed(M + N + K)
@@ -108,7 +110,7 @@ def test_stream_k_split_tiles(cuda, M, N, K, act):
     w = torch.randint(-2, 3, (N, K), device=cuda).to(torch.bfloat16)
     res = torch.randint(-8, 9, (M, N), device=cuda).to(torch.bfloat16) if act == "residual" else None
     out_dtype = torch.bfloat16 if act == "swiglu" else torch.float32  # the SwiGLU epilogue writes bf16
-    y = _run(x, w, None, res, act, out_dtype, force=11)
+    y = _run(x, w, None, res, act, out_dtype, force=KERNELS[walk])
     acc = x.float().cpu() @ w.float().cpu().t()
     if act == "swiglu":
         g = acc.view(M, N // 32, 2, 16)
@@ -117,7 +119,7 @@ def test_stream_k_split_tiles(cuda, M, N, K, act):
     else:
         assert torch.equal(y.cpu(), acc + (0 if res is None else res.float().cpu()))
     for _ in range(5):
-        assert torch.equal(_run(x, w, None, res, act, out_dtype, force=11), y)
+        assert torch.equal(_run(x, w, None, res, act, out_dtype, force=KERNELS[walk]), y)
 
 
 @pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(1024, 512, 4, 2, False), (1300, 4096, 32, 8, False),

@@ -52,6 +52,7 @@ def main():
                 "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
                 "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
                 "w4s": lambda: nat.gemm(x, w, out, None, None, 0, 11),
+                "w4x": lambda: nat.gemm(x, w, out, None, None, 0, 12),
                 "tiled": lambda: nat.gemm(x, w, out, None, None, 0, 2),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
@@ -68,6 +69,7 @@ def main():
         r["w4d_vs_blas"] = round(r["hipblaslt_ms"] / r["w4d_ms"], 3)
         r["w4r_vs_blas"] = round(r["hipblaslt_ms"] / r["w4r_ms"], 3)
         r["w4s_vs_blas"] = round(r["hipblaslt_ms"] / r["w4s_ms"], 3)
+        r["w4x_vs_blas"] = round(r["hipblaslt_ms"] / r["w4x_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if enable_tuned_blas():
