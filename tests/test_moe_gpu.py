@@ -27,8 +27,10 @@ def test_moe_route(cuda):
 
 # (2, 8, 2, 4096, 1024) / (32, 8, 2, 4096, 4096): decode-sized steps (<= 64 expert rows) on the weight-streaming
 # decode kernel, idle experts included; the others on the 128 x 128 grouped kernel
+# (12 | 20 | 24 | 32, 2-4 experts, D = I = 512): the expert-parallel rehearsal's per-rank slabs (e_local 2-4, 24-64 rows)
 @pytest.mark.parametrize("T,E,k,D,I", [(1, 8, 2, 256, 512), (37, 8, 2, 512, 256), (700, 4, 2, 1024, 1024),
-                                       (2, 8, 2, 4096, 1024), (32, 8, 2, 4096, 4096)])
+                                       (2, 8, 2, 4096, 1024), (32, 8, 2, 4096, 4096), (12, 2, 2, 512, 512),
+                                       (20, 4, 2, 512, 512), (24, 2, 2, 512, 512), (32, 3, 2, 512, 512)])
 def test_moe_gemm_and_combine(cuda, T, E, k, D, I):
     torch.manual_seed(T)
     x = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
@@ -204,3 +206,27 @@ def test_ep_pack_and_combine_match_reference(cuda, T, k, E, W):
         out = ops.ep_combine(back.to(cuda), ids.to(cuda), pos, offs, w.to(cuda), res.to(cuda), e_local, C)
         want = R.ep_combine(back, ids, r_pos, r_offs, w, res, e_local, C)
         _close(out.cpu(), want, 1e-2, 1e-2, "ep_combine")
+
+
+@pytest.mark.parametrize("W,C,D,I", [(4, 16, 512, 512), (2, 16, 512, 512), (4, 8, 512, 512), (4, 16, 4096, 1024)])
+def test_ep_local_experts_padded_matches_reference(cuda, W, C, D, I):
+    """The receiving side of a padded EP exchange: W slabs of C rows, padding rows carrying the sentinel expert id
+    e_local, through ops.moe_dispatch + the grouped GEMMs (the decode weight-stream kernel at <= 64 rows) == the
+    per-expert fp32 reference; padding rows come back as anything (never combined), live rows must match."""
+    from generativeaiexamples_amd.parallel import ep
+    g = torch.Generator().manual_seed(W * C + D)
+    e_local = 8 // W
+    R = W * C
+    rows = torch.randn(R, D, generator=g).to(torch.bfloat16)
+    eid = torch.randint(0, e_local + 1, (R,), generator=g, dtype=torch.int32)  # e_local = padding
+    w13 = (torch.randn(e_local, 2 * I, D, generator=g) / math.sqrt(D)).to(torch.bfloat16)
+    w2 = (torch.randn(e_local, D, I, generator=g) / math.sqrt(I)).to(torch.bfloat16)
+    y = ep.local_experts_padded(rows.to(cuda), eid.to(cuda), w13.to(cuda), w2.to(cuda)).cpu()
+    live = eid != e_local
+    want = torch.zeros(R, D)
+    for e in range(e_local):
+        sel = (eid == e).nonzero().flatten()
+        if sel.numel():
+            h = ref.linear(rows[sel], w13[e], act="swiglu")
+            want[sel] = ref.linear(h, w2[e]).float()
+    _close(y[live], want[live].to(torch.bfloat16), 3e-2, 2e-2, "local experts (padded)")
