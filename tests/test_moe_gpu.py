@@ -27,10 +27,11 @@ def test_moe_route(cuda):
 
 # (2, 8, 2, 4096, 1024) / (32, 8, 2, 4096, 4096): decode-sized steps (<= 64 expert rows) on the weight-streaming
 # decode kernel, idle experts included; the others on the 128 x 128 grouped kernel
-# (12 | 20 | 24 | 32, 2-4 experts, D = I = 512): the expert-parallel rehearsal's per-rank slabs (e_local 2-4, 24-64 rows)
+# (12 .. 50 tokens, 2-4 experts, D = I = 512): the expert-parallel rehearsal's per-rank shapes (e_local 2-4, 24-100 rows)
 @pytest.mark.parametrize("T,E,k,D,I", [(1, 8, 2, 256, 512), (37, 8, 2, 512, 256), (700, 4, 2, 1024, 1024),
                                        (2, 8, 2, 4096, 1024), (32, 8, 2, 4096, 4096), (12, 2, 2, 512, 512),
-                                       (20, 4, 2, 512, 512), (24, 2, 2, 512, 512), (32, 3, 2, 512, 512)])
+                                       (20, 4, 2, 512, 512), (24, 2, 2, 512, 512), (32, 3, 2, 512, 512),
+                                       (50, 2, 2, 512, 512), (40, 3, 2, 512, 512)])
 def test_moe_gemm_and_combine(cuda, T, E, k, D, I):
     torch.manual_seed(T)
     x = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
