@@ -231,3 +231,36 @@ def test_ep_local_experts_padded_matches_reference(cuda, W, C, D, I):
             h = ref.linear(rows[sel], w13[e], act="swiglu")
             want[sel] = ref.linear(h, w2[e]).float()
     _close(y[live], want[live].to(torch.bfloat16), 3e-2, 2e-2, "local experts (padded)")
+
+
+@pytest.mark.parametrize("rank", [2, 3])
+def test_mixtral_engine_matches_fp32_rehearsal_requests(cuda, rank):
+    """Single-rank Mixtral engine (no expert parallelism) on the request sets the EP = 4 rehearsal gives ranks 2 / 3
+    (5 / 7 prompts over several prefill chunks, mixed prefill + decode steps, decode batches of 5-8): every greedy
+    token is the fp32 reference argmax of its prefix up to the rehearsal's near-tie tolerance. Separates the
+    engine / attention / MoE path from the expert-parallel exchange when the rehearsal disagrees."""
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.mixtral import MixtralConfig, MixtralModel
+
+    cfg = MixtralConfig.tiny_moe(num_experts=8, hidden_size=512, intermediate_size=512, num_heads=8, num_kv_heads=4,
+                                 head_dim=64, vocab_size=4096)
+    m = MixtralModel(cfg, device=cuda).random_init(3)
+    eng = LLMEngine(m, small_byte_tokenizer(4096), EngineConfig(
+        num_blocks=160, max_model_len=256, use_graphs=True, max_num_seqs=8, max_batched_tokens=64, prefill_chunk=32,
+        prefix_cache=False, graph_batch_sizes=(1, 2, 4, 8), kv_memory_fraction=0.02))
+    n_req = 1 + 2 * rank
+    prompts = [list(range(11 + 5 * rank + 3 * i, 11 + 5 * rank + 3 * i + 7 + 9 * ((i + rank) % 3))) for i in range(n_req)]
+    sp = SamplingParams(temperature=0.0, max_tokens=6 + 4 * rank, ignore_eos=True)
+    reqs = [eng.add_request(p, sp) for p in prompts]
+    while eng.has_work():
+        eng.step()
+    bad = []
+    for p, r in zip(prompts, reqs):
+        lg = m.reference_forward(torch.tensor(p + r.output_ids[:-1]))[len(p) - 1:]
+        for i, t in enumerate(r.output_ids):
+            row = lg[i]
+            tol = 0.02 * max(1.0, float(row.abs().max()))
+            if float(row[t]) < float(row.max()) - tol:
+                bad.append((i, t, int(row.argmax()), round(float(row.max() - row[t]), 4), round(tol, 4)))
+    assert not bad, bad[:6]
