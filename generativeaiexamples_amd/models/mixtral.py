@@ -235,8 +235,10 @@ class MixtralModel(LlamaModel):
         return logits[:, : c.vocab_size]
 
     @torch.no_grad()
-    def reference_forward(self, token_ids: torch.Tensor) -> torch.Tensor:
-        """Dense fp32 oracle (TP=1)."""
+    def reference_forward(self, token_ids: torch.Tensor, router_margin: list | None = None) -> torch.Tensor:
+        """Dense fp32 oracle (TP=1). ``router_margin`` (a list) receives, per token, the smallest gap over the layers
+        between the router logits of its k-th and (k+1)-th expert: where that gap is within bf16 noise the bf16
+        engine may route the token to a different expert, a discontinuity no logit tolerance covers."""
         c = self.cfg
         wf = {k: v.float().cpu() for k, v in self.w.items()}
         T, hd = token_ids.numel(), c.head_dim
@@ -263,7 +265,12 @@ class MixtralModel(LlamaModel):
             att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1)[None], float("-inf"))
             h = h + torch.einsum("hqk,khd->qhd", att.softmax(-1), v).reshape(T, -1) @ wf[p + "o"].t()
             x = rms(h, wf[p + "mlp_norm"])
-            pr = (x @ wf[p + "router"].t()).softmax(-1)
+            rl = x @ wf[p + "router"].t()
+            if router_margin is not None:
+                top = torch.topk(rl, min(c.top_k + 1, rl.shape[-1]), -1).values
+                gap = top[:, c.top_k - 1] - top[:, -1] if top.shape[-1] > c.top_k else torch.full((T,), float("inf"))
+                margin = gap if i == 0 else torch.minimum(margin, gap)
+            pr = rl.softmax(-1)
             tw, ti = torch.topk(pr, c.top_k, -1)
             tw = tw / tw.sum(-1, keepdim=True)
             out = torch.zeros_like(x)
@@ -274,4 +281,6 @@ class MixtralModel(LlamaModel):
                     g = (torch.nn.functional.silu(gu[:, 0]) * gu[:, 1]).reshape(-1)
                     out[t] += tw[t, j] * (g @ wf[p + "w2"][e].t())
             h = h + out
+        if router_margin is not None:
+            router_margin.append(margin)
         return rms(h, wf["norm"]) @ wf["lm_head"].t()

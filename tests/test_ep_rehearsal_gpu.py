@@ -1,5 +1,7 @@
 """Expert parallelism on a GPU (VERDICT r3 "next" #4): 2 and 4 ranks share cuda:0 over a gloo control plane; the
-decode steps are captured HIP graphs whose token exchanges are the peer-memory one-shot all-to-all
+decode steps are captured HIP graphs whose token exchanges are the peer-memory one-shot all-to-all. A token that
+misses the fp32 argmax at a position whose top-k routing is itself a near-tie (router-logit gap < 0.05: the bf16
+engine may pick the other expert, with or without expert parallelism) is counted apart and must stay rare
 (csrc/comm/custom_ar.hip) between the native EP pack / combine kernels (moe.hip). Every rank's greedy tokens must
 be fp32-consistent with a single-rank Mixtral of the same weights."""
 import json
@@ -50,8 +52,9 @@ def test_ep_decode_graph_one_gpu(tmp_path, world, cuda):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     results = [json.loads((tmp_path / f"epg_{r}.json").read_text()) for r in range(world)]
     for r, res in enumerate(results):  # every rank's record first, then the checks
-        print(f"EP={world} rank {r}: {res['total'] - len(res['bad'])}/{res['total']} tokens fp32-consistent, "
-              f"stats {res['stats']}, err {res['err']}, bad (pos, tok, argmax, gap, tol) {res['bad'][:6]}")
+        print(f"EP={world} rank {r}: {res['total'] - len(res['bad']) - len(res['ties'])}/{res['total']} tokens "
+              f"fp32-consistent, {len(res['ties'])} at router near-ties {res['ties'][:4]}, stats {res['stats']}, "
+              f"err {res['err']}, bad (pos, tok, argmax, gap, tol, router margin) {res['bad'][:6]}")
     graphs = os.environ.get("GAI_EP_REHEARSE_GRAPHS", "1") == "1"
     for r, res in enumerate(results):
         assert res["err"] == 0
@@ -59,4 +62,5 @@ def test_ep_decode_graph_one_gpu(tmp_path, world, cuda):
             assert res["graphs"], "no decode graph captured"
             assert res["stats"]["graph_steps"] > 0, "decode never replayed a graph"
         assert not res["bad"], res["bad"][:5]
+        assert len(res["ties"]) <= max(1, res["total"] // 20), res["ties"]  # rare, or they would hide an error
         assert res["lens"] == [6 + 4 * r] * (1 + 2 * r)

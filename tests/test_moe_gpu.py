@@ -255,12 +255,9 @@ def test_mixtral_engine_matches_fp32_rehearsal_requests(cuda, rank):
     reqs = [eng.add_request(p, sp) for p in prompts]
     while eng.has_work():
         eng.step()
-    bad = []
-    for p, r in zip(prompts, reqs):
-        lg = m.reference_forward(torch.tensor(p + r.output_ids[:-1]))[len(p) - 1:]
-        for i, t in enumerate(r.output_ids):
-            row = lg[i]
-            tol = 0.02 * max(1.0, float(row.abs().max()))
-            if float(row[t]) < float(row.max()) - tol:
-                bad.append((i, t, int(row.argmax()), round(float(row.max() - row[t]), 4), round(tol, 4)))
+    from tests._dist_workers import moe_greedy_check
+
+    bad, ties, total = moe_greedy_check(m, prompts, [r.output_ids for r in reqs])
+    print(f"rank {rank} requests: {total - len(bad) - len(ties)}/{total} fp32-consistent, {len(ties)} at router near-ties")
     assert not bad, bad[:6]
+    assert len(ties) <= max(1, total // 20), ties  # near-ties are rare; many would hide a real error
