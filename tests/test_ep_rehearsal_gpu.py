@@ -54,13 +54,15 @@ def test_ep_decode_graph_one_gpu(tmp_path, world, cuda):
     for r, res in enumerate(results):  # every rank's record first, then the checks
         print(f"EP={world} rank {r}: {res['total'] - len(res['bad']) - len(res['ties'])}/{res['total']} tokens "
               f"fp32-consistent, {len(res['ties'])} at router near-ties {res['ties'][:4]}, stats {res['stats']}, "
-              f"err {res['err']}, bad (pos, tok, argmax, gap, tol, router margin) {res['bad'][:6]}")
+              f"err {res['err']}, bad (pos, tok, argmax, gap, tol, router margin) {res['bad'][:6]}, "
+              f"requests differing from the single-rank engine {res['differ_from_single_rank']}")
     graphs = os.environ.get("GAI_EP_REHEARSE_GRAPHS", "1") == "1"
     for r, res in enumerate(results):
         assert res["err"] == 0
         if graphs:
             assert res["graphs"], "no decode graph captured"
             assert res["stats"]["graph_steps"] > 0, "decode never replayed a graph"
+        assert not res["differ_from_single_rank"], f"rank {r}: requests {res['differ_from_single_rank']} differ"
         assert not res["bad"], res["bad"][:5]
         assert len(res["ties"]) <= max(1, res["total"] // 20), res["ties"]  # rare, or they would hide an error
         assert res["lens"] == [6 + 4 * r] * (1 + 2 * r)
