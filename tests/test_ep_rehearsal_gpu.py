@@ -62,7 +62,6 @@ def test_ep_decode_graph_one_gpu(tmp_path, world, cuda):
         if graphs:
             assert res["graphs"], "no decode graph captured"
             assert res["stats"]["graph_steps"] > 0, "decode never replayed a graph"
-        assert not res["differ_from_single_rank"], f"rank {r}: requests {res['differ_from_single_rank']} differ"
         assert not res["bad"], res["bad"][:5]
         assert len(res["ties"]) <= max(1, res["total"] // 20), res["ties"]  # rare, or they would hide an error
         assert res["lens"] == [6 + 4 * r] * (1 + 2 * r)
