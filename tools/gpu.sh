@@ -5,7 +5,8 @@
 #   tools/gpu.sh <out-subdir> "<recipe> [args...]" ["<recipe> [args...]" ...]
 #
 # recipes (logs / results land in gpurun_out/<out-subdir>/):
-#   tests <name> <pytest args...>   python -m pytest -m gpu <args> (per-test timeout 120 s)
+#   tests <name> <pytest args...>   python -m pytest -m gpu <args> (per-test timeout 120 s, step limit 600 s)
+#   testsl <name> <pytest args...>  the same with an 1100 s step limit (the whole suite)
 #   bench <name> <bench.py args...> bench.py ... --json-out <name>.json
 #   prof  <name> <bench.py args...> rocprofv3 --kernel-trace --stats around bench.py, reduced to <name>_kernels.csv
 #   py    <name> <script args...>   python <script> <args>
@@ -45,6 +46,9 @@ for spec in "$@"; do
     tests) step 600 "$O/$n.log" python -u -m pytest -m gpu -q --timeout 120 --timeout-method thread \
              -p no:cacheprovider "${rest[@]}"
            rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;  # test failures (1) do not stop the job
+    testsl) step 1100 "$O/$n.log" python -u -m pytest -m gpu -q --timeout 120 --timeout-method thread \
+             -p no:cacheprovider "${rest[@]}"
+           rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;  # the whole suite, as the driver runs it
     bench) step 600 "$O/$n.log" python bench.py "${rest[@]}" --json-out "$O/$n.json" || exit $? ;;
     prof)  rm -rf "/tmp/prof_$n"
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
