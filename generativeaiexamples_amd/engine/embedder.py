@@ -21,6 +21,7 @@ import torch
 
 from ..models.bert import BertModel
 from .tokenizer import Tokenizer
+from ..utils.graphs import hip_graph_capture
 from ..utils.profiling import roctx_range
 
 
@@ -76,7 +77,7 @@ class Embedder:
                 m.embed_padded(ids, lens, attn, B, L)  # warm-up (allocator, kernel attributes)
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            with hip_graph_capture(g, s):
                 out = m.embed_padded(ids, lens, attn, B, L)
             # the graph reads and writes attn's buffers (KV scratch, index tensors) by address: keep them alive
             self._graphs[key] = (g, ids, lens, out, attn)

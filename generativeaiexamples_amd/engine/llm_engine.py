@@ -36,6 +36,7 @@ from ..models.common import ForwardBatch
 from .kv_cache import KVCache, cache_dtype
 from .sampling import SamplingBatch, SamplingParams
 from .staging import HostStager
+from ..utils.graphs import hip_graph_capture
 from ..utils.profiling import roctx_range
 from .tokenizer import IncrementalDetokenizer, Tokenizer
 
@@ -466,7 +467,7 @@ class LLMEngine:
                 self.model.forward(fb, self.kv, self.decode_ws)
         torch.cuda.current_stream(d).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        with hip_graph_capture(g, s):
             logits = self.model.forward(fb, self.kv, self.decode_ws)
         self.graphs[bs] = (g, fb, logits)
 
@@ -528,7 +529,7 @@ class LLMEngine:
                 run()  # warm-up (n_valid = 0: the advance kernel touches no row)
             torch.cuda.current_stream(d).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            with hip_graph_capture(g, s):
                 run()
         self.multi_graphs[bs] = (g, run, fb, samp, n_valid, toks)
 
