@@ -13,20 +13,30 @@ ROOT = "/sys/class/kfd/kfd/proc"
 
 
 def census() -> dict:
-    """{'procs': n, 'queues': n, 'per_pid': {pid: queues}} (empty when KFD sysfs is not visible)."""
-    out = {"procs": 0, "queues": 0, "per_pid": {}}
+    """{'procs': n, 'queues': n, 'per_pid': {pid: queues}, 'per_gpu': {gpu_id: {pid: queues}}} over the whole node
+    (KFD lists every process of every GPU; queues/<q>/gpuid says which GPU a queue is on). Empty when KFD sysfs is
+    not visible."""
+    out = {"procs": 0, "queues": 0, "per_pid": {}, "per_gpu": {}}
     if not os.path.isdir(ROOT):
         out["error"] = "no KFD sysfs"
         return out
     for pid in os.listdir(ROOT):
         qd = os.path.join(ROOT, pid, "queues")
         try:
-            n = len(os.listdir(qd))
+            qs = os.listdir(qd)
         except OSError:
-            n = -1
-        out["per_pid"][pid] = n
+            qs = None
+        out["per_pid"][pid] = -1 if qs is None else len(qs)
         out["procs"] += 1
-        out["queues"] += max(n, 0)
+        out["queues"] += len(qs or [])
+        for q in qs or []:
+            try:
+                with open(os.path.join(qd, q, "gpuid")) as f:
+                    gid = f.read().strip()
+            except OSError:
+                continue
+            g = out["per_gpu"].setdefault(gid, {})
+            g[pid] = g.get(pid, 0) + 1
     return out
 
 
