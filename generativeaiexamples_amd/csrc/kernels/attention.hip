@@ -364,7 +364,9 @@ __device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_
   }
 }
 
-template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false>
+// NTL: the K / V cache loads are non-temporal (each decode step streams the cache once; keeps it from evicting the
+// L2-resident Q / block tables / split partials)
+template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false, bool NTL = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
@@ -442,13 +444,19 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
           const int key = 8 * (m >> 2) + 4 * i + (m & 3);  // 0..31 inside the half
           const size_t pb = key < 16 ? pb0 : pb1;
 #pragma unroll
-          for (int t = 0; t < D / 32; ++t)
-            c.k[h][i][t] = *reinterpret_cast<const Raw*>(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
+          for (int t = 0; t < D / 32; ++t) {
+            const Raw* kp = reinterpret_cast<const Raw*>(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
+            if constexpr (NTL) c.k[h][i][t] = __builtin_nontemporal_load(kp);
+            else c.k[h][i][t] = *kp;
+          }
         }
         const size_t pbv = gq < 2 ? pb0 : pb1;
 #pragma unroll
-        for (int dt = 0; dt < D / 16; ++dt)
-          c.v8[h][dt] = *reinterpret_cast<const Raw*>(vc + pbv + (size_t)(16 * dt + (lane & 15)) * kBS + 8 * (gq & 1));
+        for (int dt = 0; dt < D / 16; ++dt) {
+          const Raw* vp = reinterpret_cast<const Raw*>(vc + pbv + (size_t)(16 * dt + (lane & 15)) * kBS + 8 * (gq & 1));
+          if constexpr (NTL) c.v8[h][dt] = __builtin_nontemporal_load(vp);
+          else c.v8[h][dt] = *vp;
+        }
       } else if constexpr (sizeof(KV) == 2) {
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
@@ -705,7 +713,16 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   static const int variant = getenv("GAI_DECODE_VARIANT") ? atoi(getenv("GAI_DECODE_VARIANT")) : 1;
   // in-launch split merge (no attn_decode_reduce launch) when the caller passes the ticket counters
   const bool fuse = split_cnt != nullptr && max_splits > 1 && variant == 1;
+  // GAI_DECODE_NT=1: non-temporal K / V loads in the fused bf16 kernel (A/B)
+  static const bool ntl = getenv("GAI_DECODE_NT") && atoi(getenv("GAI_DECODE_NT")) == 1;
 #define GAI_DEC(DD)                                                                                             \
+  if (D == DD && fuse && ntl && !kv_fp8) {                                                                      \
+    attn_decode_kernel<DD, false, 1, true, bf16, true, true><<<grid, 256, 0, st>>>(                             \
+        (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, max_blocks, ctx_lens,         \
+        (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys, max_splits, k_scale, v_scale, split_cnt);       \
+    GAI_LAUNCH_CHECK();                                                                                         \
+    return;                                                                                                     \
+  }                                                                                                             \
   if (D == DD && fuse) {                                                                                        \
     if (kv_fp8)                                                                                                 \
       attn_decode_kernel<DD, false, 1, true, fp8, true><<<grid, 256, 0, st>>>(                                  \
