@@ -713,8 +713,9 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   static const int variant = getenv("GAI_DECODE_VARIANT") ? atoi(getenv("GAI_DECODE_VARIANT")) : 1;
   // in-launch split merge (no attn_decode_reduce launch) when the caller passes the ticket counters
   const bool fuse = split_cnt != nullptr && max_splits > 1 && variant == 1;
-  // GAI_DECODE_NT=1: non-temporal K / V loads in the fused bf16 kernel (A/B)
-  static const bool ntl = getenv("GAI_DECODE_NT") && atoi(getenv("GAI_DECODE_NT")) == 1;
+  // non-temporal K / V loads in the fused bf16 kernel (GAI_DECODE_NT=0: plain loads). Llama-3-8B B = 64, ctx 2535
+  // graph replay 7.84 -> 7.68 ms per step (profiles/r4/decode/decode_nt_split_ab.txt)
+  static const bool ntl = !(getenv("GAI_DECODE_NT") && atoi(getenv("GAI_DECODE_NT")) == 0);
 #define GAI_DEC(DD)                                                                                             \
   if (D == DD && fuse && ntl && !kv_fp8) {                                                                      \
     attn_decode_kernel<DD, false, 1, true, bf16, true, true><<<grid, 256, 0, st>>>(                             \

@@ -453,8 +453,8 @@ class DecodeWorkspace:
     @staticmethod
     def choose_split(max_ctx: int, batch: int = 1, hkv: int = 8, target_wgs: int | None = None) -> int:
         """Split length (multiple of 128) giving ~target_wgs workgroups of (split, kv-head, sequence).
-        The head_dim-128 kernel runs 3 workgroups per CU (VGPR-bound), i.e. 768 resident on 256 CUs,
-        so 1536 = exactly two waves of workgroups. Measured on MI355X (B=64, 8 KV heads, ctx
+        The head_dim-128 kernel runs 3 workgroups per CU (VGPR-bound), i.e. 768 resident on 256 CUs.
+        Round 4 (non-temporal K / V loads): 1024 target workgroups, i.e. 2 splits at B = 64, 8 kv heads. Measured on MI355X (B=64, 8 KV heads, ctx
         2.3-2.6k, profiles/r1/decode_attn_split_sweep_v2.jsonl): 896-key splits (1536 WGs) 5.34 TB/s vs
         768-key splits (2048 WGs = 2.67 waves, a 1/3-empty last wave) 5.04 TB/s; 256-key splits
         4.5 TB/s (per-workgroup prologue / combine not amortised)."""
@@ -471,7 +471,10 @@ class DecodeWorkspace:
         return self.choose_split(max_ctx, batch, hkv)
 
 
-_DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1536"))  # sweeps only
+# With the non-temporal K / V loads (attention.hip) two splits per (sequence, kv head) beat three at B = 64:
+# ctx 2535 graph replay 7.68 -> 7.47 ms per step at 1024 target workgroups (768 the same, 2048 7.71;
+# profiles/r4/decode/decode_nt_split_ab.txt). GAI_DECODE_TARGET_WGS overrides (sweeps).
+_DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1024"))
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
