@@ -463,7 +463,7 @@ class DecodeWorkspace:
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128
-        return int(min(max(s, 128), 2048))
+        return int(min(max(s, 128), _DECODE_MAX_SPLIT))
 
     def split_for(self, batch: int, hkv: int, max_ctx: int) -> int:
         if self.fixed_split:
@@ -475,6 +475,7 @@ class DecodeWorkspace:
 # ctx 2535 graph replay 7.68 -> 7.47 ms per step at 1024 target workgroups (768 the same, 2048 7.71;
 # profiles/r4/decode/decode_nt_split_ab.txt). GAI_DECODE_TARGET_WGS overrides (sweeps).
 _DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1024"))
+_DECODE_MAX_SPLIT = int(os.environ.get("GAI_DECODE_MAX_SPLIT", "2048"))  # keys per split, upper bound (sweeps)
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
