@@ -90,7 +90,8 @@ __device__ void rope_tail_reduce(const float* part, int KS, int M, int N, int h,
   }
 }
 
-template <int MB, bool PSW, int WPG, typename TAILKV = void>
+// NTW: the pre-shuffled weight stream is loaded non-temporally (read once per decode step), as gemm_dec2 does
+template <int MB, bool PSW, int WPG, typename TAILKV = void, bool NTW = false>
 __global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                                float* __restrict__ part, int M, int N, int K, int KL,
                                                                RopeTail tail = RopeTail{}) {
@@ -122,9 +123,13 @@ __global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __res
                        : W + (size_t)n * K + k0 + 8 * (lane >> 4);
   constexpr int kStepW = PSW ? 512 : 32;  // elements between consecutive k32 steps of one lane
   const int nsteps = KL / 32;  // multiple of kRing
+  auto wload = [&](const bf16* p) -> bf16x8 {
+    if constexpr (PSW && NTW) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+    else return load8(p);
+  };
   bf16x8 ring[kRing];
 #pragma unroll
-  for (int u = 0; u < kRing; ++u) ring[u] = load8(wp + u * kStepW);
+  for (int u = 0; u < kRing; ++u) ring[u] = wload(wp + u * kStepW);
 
   f32x4 acc[MB];
 #pragma unroll
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(64 * WPG) void gemm_splitk_kernel(const bf16* __res
 #pragma unroll
     for (int u = 0; u < kRing; ++u) {
       const bf16x8 b = ring[u];
-      ring[u] = load8(wp + (s + kRing + u) * kStepW);
+      ring[u] = wload(wp + (s + kRing + u) * kStepW);
       step(s + u, b);
     }
   }
@@ -574,6 +579,12 @@ void dispatch_stream_ks1(const void* A, const void* B, void* C, const void* bias
 namespace {
 
 // fp32 partials [KS, M, N] of A . W^T into ws (KS > 1), either kernel variant.
+// GAI_SPLITK_NT=1: non-temporal loads of the pre-shuffled weight stream in the LDS-staged split-K kernel (A/B)
+bool splitk_ntw() {
+  static const bool on = getenv("GAI_SPLITK_NT") && atoi(getenv("GAI_SPLITK_NT")) == 1;
+  return on;
+}
+
 void launch_partials(const void* A, const void* B, int M, int N, int K, int KS, float* ws, int psw, hipStream_t st) {
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   if (!use_legacy(N, K)) {
@@ -594,9 +605,14 @@ void launch_partials(const void* A, const void* B, int M, int N, int K, int KS, 
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                               \
       hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true, WPGV>),                    \
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                               \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_splitk_kernel<MBV, true, WPGV, void, true>),        \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                               \
       once = true;                                                                                               \
     }                                                                                                            \
-    if (psw)                                                                                                     \
+    if (psw && splitk_ntw())                                                                                     \
+      gemm_splitk_kernel<MBV, true, WPGV, void, true><<<grid, 64 * WPGV, lds, st>>>((const bf16*)A, (const bf16*)B, \
+                                                                                    ws, M, N, K, KL);            \
+    else if (psw)                                                                                                \
       gemm_splitk_kernel<MBV, true, WPGV><<<grid, 64 * WPGV, lds, st>>>((const bf16*)A, (const bf16*)B, ws, M, N, \
                                                                         K, KL);                                  \
     else                                                                                                         \
