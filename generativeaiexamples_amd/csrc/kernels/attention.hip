@@ -331,6 +331,16 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // separate reduce launch and the in-launch merge (SC1: write-through partials read with sc1 loads) share it,
 // so both round identically.
 constexpr int kMergeGroup = 8;
+
+// Keys per split. split_keys > 0: fixed. 0: adaptive - each sequence's context is cut into max_splits equal
+// 128-key-aligned parts at run time, so a graph captured for the longest context a replay may see (the split count)
+// still balances its splits on the contexts it actually runs (a fixed split sized for max_model_len = 3330 left
+// a 2500-key context as 1792 + 708 keys: the critical path of the step).
+__device__ __forceinline__ int split_len(int split_keys, int ctx, int max_splits) {
+  if (split_keys > 0) return split_keys;
+  const int per = (ctx + max_splits - 1) / max_splits;
+  return max(128, (per + 127) / 128 * 128);
+}
 template <bool SC1>
 __device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_ml, int B, int Hq, int D, int seq,
                                              int hq, int d, int ns, float& L, float& O) {
@@ -380,6 +390,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int split = blockIdx.x, g = blockIdx.y, seq = blockIdx.z;
   const int ratio = Hq / Hkv;
   const int ctx = ctx_lens[seq];
+  split_keys = split_len(split_keys, ctx, max_splits);
   const int kstart = split * split_keys;
   if (kstart >= ctx) return;
   const int kend = min(ctx, kstart + split_keys);
@@ -625,9 +636,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 template <int D>
 __global__ void attn_decode_reduce_kernel(const float* __restrict__ ws_o, const float* __restrict__ ws_ml,
                                           const int* __restrict__ ctx_lens, bf16* __restrict__ out, int B, int Hq,
-                                          int split_keys) {
+                                          int split_keys, int max_splits) {
   const int seq = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
   const int ctx = ctx_lens[seq];
+  split_keys = split_len(split_keys, ctx, max_splits);
   const int ns = (ctx + split_keys - 1) / split_keys;
   if (ns <= 1) return;
   float L, O;
@@ -706,7 +718,8 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                      float v_scale, hipStream_t st, int* split_cnt) {
   if (B == 0) return;
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
-  if (split_keys % 128) gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be a multiple of 128");
+  if (split_keys < 0 || split_keys % 128)
+    gai_launch_error(__FILE__, __LINE__, "attn_decode: split_keys must be 0 (adaptive) or a multiple of 128");
   const dim3 grid(max_splits, Hkv, B);
   // GAI_DECODE_VARIANT: 0 = 8-B V^T pieces, 1 = 16-B V^T loads (default), 2 = 16-B + 64 keys per wave step,
   // 3 = 16-B + register double buffer (software pipelined)
@@ -756,7 +769,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
     GAI_LAUNCH_CHECK();                                                                                         \
     if (max_splits > 1) {                                                                                       \
       attn_decode_reduce_kernel<DD><<<dim3(B, Hq), DD, 0, st>>>(ws_o, ws_ml, ctx_lens, (bf16*)out, B, Hq,       \
-                                                                 split_keys);                                   \
+                                                                 split_keys, max_splits);                       \
       GAI_LAUNCH_CHECK();                                                                                       \
     }                                                                                                           \
     return;                                                                                                     \

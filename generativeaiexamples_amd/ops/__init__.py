@@ -476,6 +476,7 @@ class DecodeWorkspace:
 # profiles/r4/decode/decode_nt_split_ab.txt). GAI_DECODE_TARGET_WGS overrides (sweeps).
 _DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1024"))
 _DECODE_MAX_SPLIT = int(os.environ.get("GAI_DECODE_MAX_SPLIT", "2048"))  # keys per split, upper bound (sweeps)
+_DECODE_ADAPTIVE = os.environ.get("GAI_DECODE_ADAPTIVE", "1") == "1"
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
@@ -490,8 +491,11 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
     nsplit = (mc + split - 1) // split
     assert nsplit <= ws.max_splits, "decode workspace too small for this context"
     out = torch.empty_like(q) if out is None else out
-    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale, split, nsplit, k_scale,
-                         v_scale, ws.cnt if _ATTN_FUSE else None)
+    # adaptive (split_keys 0): the kernel cuts each sequence's ACTUAL context into nsplit equal parts, so graphs
+    # captured for max_ctx balance their splits at every replay (GAI_DECODE_ADAPTIVE=0: fixed split_keys)
+    native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale,
+                         0 if (_DECODE_ADAPTIVE and ws.fixed_split is None) else split, nsplit, k_scale, v_scale,
+                         ws.cnt if _ATTN_FUSE else None)
     return out
 
 

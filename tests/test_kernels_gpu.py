@@ -175,6 +175,29 @@ def test_attention_decode(cuda, D, Hq, Hkv):
         _close(o, o_ref, 2e-2, 2e-2, f"decode split={ws.split_keys}")
 
 
+@pytest.mark.parametrize("nsplit", [1, 2, 3, 7])
+def test_attention_decode_adaptive_splits(cuda, nsplit):
+    """split_keys = 0: every sequence's actual context is cut into nsplit equal 128-key-aligned parts inside the
+    kernel (graphs captured for max_model_len stay balanced at every replay); fused in-launch merge == separate
+    reduce launch == the fp32 reference, on ragged contexts from 1 key to far past one split."""
+    torch.manual_seed(8)
+    D, Hq, Hkv = 128, 32, 8
+    ctx = [1, 100, 129, 700, 2535, 2663, 4097, 300]
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, cuda, seed=3)
+    q = torch.randn(len(ctx), Hq, D, device=cuda, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    ws = ops.DecodeWorkspace(len(ctx), Hq, D, 8192, cuda)
+    nat = ops.native()
+    c = torch.tensor(ctx, dtype=torch.int32, device=cuda)
+    o_f, o_u = torch.empty_like(q), torch.empty_like(q)
+    nat.attn_decode(q, kc, vc, bt, c, o_f, ws.o, ws.ml, scale, 0, nsplit, 1.0, 1.0, ws.cnt)
+    nat.attn_decode(q, kc, vc, bt, c, o_u, ws.o, ws.ml, scale, 0, nsplit, 1.0, 1.0, None)
+    assert int(ws.cnt.abs().sum()) == 0
+    o_ref = ref.attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), c.cpu(), scale)
+    _close(o_f, o_ref, 2e-2, 2e-2, "adaptive fused")
+    _close(o_u, o_ref, 2e-2, 2e-2, "adaptive reduce")
+
+
 def test_attention_decode_fused_merge_reuse(cuda):
     """In-launch split merge (ticket counters, last split combines): equal to the separate reduce launch, and
     the counters reset themselves - many back-to-back launches and graph replays on one workspace, with the
