@@ -579,9 +579,10 @@ void dispatch_stream_ks1(const void* A, const void* B, void* C, const void* bias
 namespace {
 
 // fp32 partials [KS, M, N] of A . W^T into ws (KS > 1), either kernel variant.
-// GAI_SPLITK_NT=1: non-temporal loads of the pre-shuffled weight stream in the LDS-staged split-K kernel (A/B)
+// Non-temporal loads of the pre-shuffled weight stream in the LDS-staged split-K kernel (GAI_SPLITK_NT=0: plain):
+// Llama-3-8B B = 64 decode step 7.466 -> 7.398 ms (QKV / O projections; profiles/r4/decode/decode_nt_split_ab.txt)
 bool splitk_ntw() {
-  static const bool on = getenv("GAI_SPLITK_NT") && atoi(getenv("GAI_SPLITK_NT")) == 1;
+  static const bool on = !(getenv("GAI_SPLITK_NT") && atoi(getenv("GAI_SPLITK_NT")) == 0);
   return on;
 }
 
