@@ -376,11 +376,11 @@ __device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_
 
 // NTL: the K / V cache loads are non-temporal (each decode step streams the cache once; keeps it from evicting the
 // L2-resident Q / block tables / split partials)
-// The default (NTL) instantiation is held to 3 workgroups per CU (138 VGPRs, no spill; unconstrained the compiler
-// used 138 VGPRs + 32 AGPRs = 2 per CU): 768 resident workgroups, so 3 splits per (sequence, kv head) at B = 64 fill
-// exactly two rounds
+// Occupancy: unconstrained, the compiler takes 138 VGPRs + 32 AGPRs (2 workgroups per CU, 512 resident), and two
+// splits per (sequence, kv head) at B = 64 are exactly two rounds. Held to 3 per CU (no spill) with three splits it
+// measured 7.424 vs 7.332 ms per step (profiles/r4/decode/decode_nt_split_ab.txt): kept at 2.
 template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false, bool NTL = false>
-__global__ __launch_bounds__(256, NTL ? 3 : 1) void attn_decode_kernel(
+__global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int Hq, int Hkv, float scale, int split_keys,
