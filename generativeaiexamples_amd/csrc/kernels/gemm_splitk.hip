@@ -486,7 +486,10 @@ int legacy_ks(int M, int N, int K) {
   const int kl_max = (128 * 1024) / (16 * MB * 2);  // LDS bytes / row bytes
   const int units = K / kKAlign;
   const int tiles = (N + 16 * splitk_wpg() - 1) / (16 * splitk_wpg());
-  static const int min_wg = getenv("GAI_SPLITK_LEGACY_MINWG") ? atoi(getenv("GAI_SPLITK_LEGACY_MINWG")) : 512;
+  // 192: Llama-3-8B B = 64 QKV takes 4 K-slices (192 workgroups, half the fp32 partial traffic of 8), O keeps 8
+  // (4 would leave 128 workgroups): decode step 7.325 -> 7.226 ms (512: 8 slices for both; 128: 4 for both, 7.294;
+  // profiles/r4/decode/decode_nt_split_ab.txt)
+  static const int min_wg = getenv("GAI_SPLITK_LEGACY_MINWG") ? atoi(getenv("GAI_SPLITK_LEGACY_MINWG")) : 192;
   int best = units;  // KS = units / d for a divisor d of units
   for (int d = units; d >= 1; --d) {
     if (units % d) continue;
