@@ -889,6 +889,10 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
       splitk_rope_kv_kernel<DD, bf16, 8><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,     \
                                                                slots, (bf16*)q_out, (bf16*)k_cache,               \
                                                                (bf16*)v_cache, Hq, Hkv, iks, ivs);                \
+    else if (KS == 4)  /* Llama-3-8B QKV at B = 64 (legacy_ks, min 192 workgroups) */                             \
+      splitk_rope_kv_kernel<DD, bf16, 4><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,     \
+                                                               slots, (bf16*)q_out, (bf16*)k_cache,               \
+                                                               (bf16*)v_cache, Hq, Hkv, iks, ivs);                \
     else                                                                                                          \
       splitk_rope_kv_kernel<DD, bf16, 0><<<grid, 256, 0, st>>>(ws, KS, M, N, (const bf16*)bias, pos, cos_sin,     \
                                                                slots, (bf16*)q_out, (bf16*)k_cache,               \
