@@ -56,10 +56,7 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
   return acc;
 }
 
-// GX: the activations are read from global memory (L2-resident, MR x K x 2 bytes) instead of an LDS image - for
-// the un-normalised deep-K projection at batch 2-4 (down: 4 x 14336 x 2 = 112 KiB of LDS would hold a CU to one
-// workgroup of 8 waves)
-template <int MR, int EPI, bool GX = false>
+template <int MR, int EPI>
 __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
   __shared__ float red[kGvWaves][MR];
@@ -69,8 +66,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
   const int K = a.K, nch = K / 8;
 
   // ---- stage the activation rows (normalised when gamma is given); the host keeps K <= 8192 for the norm form
-  if constexpr (GX) {
-  } else if (a.gamma != nullptr) {
+  if (a.gamma != nullptr) {
     constexpr int kMaxC = 2;  // chunks per thread per row: K <= 2 * 8 * 512
     bf16x8 v[MR][kMaxC];
     float ss[MR];
@@ -118,7 +114,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * c) = load8(a.x + (size_t)m * K + 8 * c);
     }
   }
-  if constexpr (!GX) __syncthreads();
+  __syncthreads();
 
   // ---- this wave's row pair
   const int p = blockIdx.x * kGvWaves + wid;
@@ -157,7 +153,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       const int k0 = (g * kG + c) * kPiece + 8 * lane;
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
-        const bf16x8 xv = GX ? load8(a.x + (size_t)m * K + k0) : *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
         acc[m][0] = dot8(xv, b0[c], acc[m][0]);
         acc[m][1] = dot8(xv, b1[c], acc[m][1]);
       }
@@ -237,9 +233,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
 
 template <int EPI>
 void gemv_launch(const GemvArgs& a, hipStream_t st) {
-  // activations from global (no LDS image) for an un-normalised input larger than 32 KiB (down at batch 2-4)
-  const bool gx = a.gamma == nullptr && (size_t)a.M * a.K * sizeof(bf16) > 32768;
-  const size_t lds = gx ? 0 : (size_t)a.M * a.K * sizeof(bf16);
+  const size_t lds = (size_t)a.M * a.K * sizeof(bf16);
   const int grid = (a.N / 2 + kGvWaves - 1) / kGvWaves;
 #define GAI_GV(MRV)                                                                                           \
   if (a.M == MRV) {                                                                                           \
@@ -249,10 +243,7 @@ void gemv_launch(const GemvArgs& a, hipStream_t st) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, kGvMaxDyn);                             \
       once = true;                                                                                            \
     }                                                                                                         \
-    if (gx)                                                                                                   \
-      gemv_kernel<MRV, EPI, true><<<grid, kGvThreads, 0, st>>>(a);                                            \
-    else                                                                                                      \
-      gemv_kernel<MRV, EPI><<<grid, kGvThreads, lds, st>>>(a);                                                \
+    gemv_kernel<MRV, EPI><<<grid, kGvThreads, lds, st>>>(a);                                                  \
     GAI_LAUNCH_CHECK();                                                                                       \
     return;                                                                                                   \
   }
