@@ -21,8 +21,8 @@
 //      bit-identical results)
 // Reuse of parity p at call e+2 is safe without a closing barrier: a peer's block b can only reach
 // e+2 after seeing our signal for e+1, which we send after finishing our reads of call e (same
-// stream, kernels serialised). Flags only ever hold e-1 or e while we wait for e (a peer cannot run
-// ahead of our own signal), so the equality test is wrap-safe.
+// stream, kernels serialised). Flags hold e-1, e or e+1 while we wait for e (a peer can finish call e and
+// signal the next call, but cannot reach e+2 without our e+1 signal), so the wait accepts any epoch >= e.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,6 +73,21 @@ static uint32_t ar_spin_limit() {
   return v;
 }
 
+// Poll a peer's signal until it reaches epoch e. "Reaches" is `flag - e >= 0` (wrap-safe), not equality: a peer
+// that saw OUR epoch-e signal may finish call e and the next collective on the same counters, storing e + 1 here
+// before this wave reads e (a rank descheduled mid-poll, e.g. ranks time-slicing one GPU). e + 1 implies the peer's
+// epoch-e data landed first (it signals in order), and it cannot reach e + 2 without our e + 1 signal.
+__device__ __forceinline__ void wait_epoch(uint32_t* f, uint32_t e, uint32_t limit, int* err) {
+  uint32_t spins = 0;
+  while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > limit) {
+      atomicOr(err, 1);
+      break;
+    }
+  }
+}
+
 template <int W, bool F32>
 __global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in, uint4* out,
                                                                 ArPtrs p, uint32_t* __restrict__ counters, int rank,
@@ -101,14 +116,7 @@ __global__ __launch_bounds__(kArThreads) void ar_oneshot_kernel(const uint4* in,
   // 4. wait for every peer's chunk
   if (tid < W) {
     uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > p.spin_limit) {  // ~seconds: a peer died or diverged; never hang the GPU
-        atomicOr(err, 1);
-        break;
-      }
-    }
+    wait_epoch(f, e, p.spin_limit, err);  // ~seconds bound: a peer died or diverged; never hang the GPU
   }
   __syncthreads();
   // 5. reduce the W local slots in rank order
@@ -166,14 +174,7 @@ __global__ __launch_bounds__(kArThreads) void ar_rmsnorm_kernel(const uint4* in,
                                   __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < W) {
     uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > p.spin_limit) {
-        atomicOr(err, 1);
-        break;
-      }
-    }
+    wait_epoch(f, e, p.spin_limit, err);
   }
   __syncthreads();
   const char* base = p.data[rank] + (int64_t)par * W * slot_bytes;
@@ -246,14 +247,7 @@ __global__ __launch_bounds__(kArThreads) void ar_twoshot_kernel(const uint4* in,
   auto wait_phase = [&](int ph) {
     if (tid < W) {
       uint32_t* f = p.sig[rank] + (b * 2 + ph) * GAI_AR_MAX_WORLD + tid;
-      uint32_t spins = 0;
-      while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > p.spin_limit) {
-          atomicOr(err, 1);
-          break;
-        }
-      }
+      wait_epoch(f, e, p.spin_limit, err);
     }
     __syncthreads();
   };
@@ -339,14 +333,7 @@ __global__ __launch_bounds__(kArThreads) void a2a_oneshot_kernel(const uint4* in
                                   __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < W) {
     uint32_t* f = p.sig[rank] + b * GAI_AR_MAX_WORLD + tid;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > p.spin_limit) {
-        atomicOr(err, 1);
-        break;
-      }
-    }
+    wait_epoch(f, e, p.spin_limit, err);
   }
   __syncthreads();
   const char* base = p.data[rank] + (int64_t)par * W * slot_bytes;

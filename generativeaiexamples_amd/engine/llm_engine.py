@@ -355,6 +355,7 @@ class LLMEngine:
                           decode_ctx=torch.ones(1, **i32), decode_block_tables=torch.full((1, 1), self.pad_block, **i32),
                           max_decode_ctx=1, sample_rows=None)
         self.model.forward(fb, self.kv, self.decode_ws)
+        self._step_done()
 
     # ------------------------------------------------------------------ batch construction
     def _to_device(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
@@ -428,11 +429,32 @@ class LLMEngine:
 
     def _step_done(self) -> None:
         """End of a step on every rank: (followers) wait for the step's GPU work so the staging buffers can
-        be reused, then poll the custom all-reduce's error word (RankFailure on a missed peer)."""
+        be reused, then poll the custom all-reduce's error word (RankFailure on a missed peer). Expert-parallel
+        ranks poll their peer-memory all-to-all's error word the same way: a peer that died or fell
+        out of lockstep makes the exchange give up after its bounded spin with stale slot data, so the step's
+        tokens are invalid; the exchange is retired (later exchanges go to RCCL, its captured graphs are
+        dropped) and RankFailure is raised."""
         if self.tp_size > 1:
             if not self.leader and self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
             self.model.ctx.check_comm()
+        xchg = getattr(self.model, "ep_xchg", None) if self.ep_group is not None else None
+        if xchg is not None:
+            from ..parallel.fault import RankFailure
+
+            if self.device.type == "cuda":  # EP steps are host-synchronous already (lockstep agreement)
+                torch.cuda.current_stream(self.device).synchronize()
+            try:
+                xchg.check()
+            except RankFailure:
+                import torch.distributed as dist
+
+                self.model.ep_xchg = None
+                self.graphs.clear()
+                self.multi_graphs.clear()
+                if dist.get_backend(self.ep_group) != "nccl":  # the fallback exchange is not capturable
+                    self.cfg.use_graphs = False
+                raise
 
     # ------------------------------------------------------------------ HIP graphs (decode)
     def _slot(self, sid: int) -> int:

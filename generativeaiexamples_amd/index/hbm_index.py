@@ -128,6 +128,23 @@ class HBMIndex:
             for key in self.partition_keys & d.metadata.keys():
                 self.parts.setdefault((key, _hashable(d.metadata[key])), []).append(r)
 
+    def _unindex_parts(self, rows: Sequence[int]):
+        """Drop deleted rows from their partitions (only the partitions those rows' documents name; the full
+        rebuild is for compact() and load(), which renumber rows)."""
+        gone: Dict[tuple, set] = {}
+        for r in rows:
+            d = self.docs[r]
+            if d is None:
+                continue
+            for key in self.partition_keys & d.metadata.keys():
+                gone.setdefault((key, _hashable(d.metadata[key])), set()).add(r)
+        for pk, rs in gone.items():
+            left = [r for r in self.parts.get(pk, []) if r not in rs]
+            if left:
+                self.parts[pk] = left
+            else:
+                self.parts.pop(pk, None)
+
     def _rebuild_parts(self):
         self.parts = {}
         self._index_parts(range(self.n), self.docs[: self.n])
@@ -168,6 +185,7 @@ class HBMIndex:
             if rows:
                 idx = torch.tensor(rows, device=self.device)
                 self.bias[idx] = float("-inf")
+                self._unindex_parts(rows)
                 for r in rows:
                     self.docs[r] = None
                 self.dead += len(rows)
@@ -176,8 +194,6 @@ class HBMIndex:
                     self.wal.flush()
                 if self.dead * 4 > self.n and self.n > 1024:
                     self.compact()
-                else:
-                    self._rebuild_parts()
             return len(rows)
 
     def delete_filename(self, filename: str) -> int:

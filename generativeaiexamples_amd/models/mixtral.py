@@ -235,15 +235,19 @@ class MixtralModel(LlamaModel):
         return logits[:, : c.vocab_size]
 
     @torch.no_grad()
-    def reference_forward(self, token_ids: torch.Tensor, router_margin: list | None = None) -> torch.Tensor:
-        """Dense fp32 oracle (TP=1). ``router_margin`` (a list) receives, per token, the smallest gap over the layers
-        between the router logits of its k-th and (k+1)-th expert: where that gap is within bf16 noise the bf16
-        engine may route the token to a different expert, a discontinuity no logit tolerance covers."""
+    def reference_forward(self, token_ids: torch.Tensor, router_margin: list | None = None,
+                          device: str | torch.device = "cpu") -> torch.Tensor:
+        """Dense fp32 oracle (TP=1), plain PyTorch ops on ``device`` (the GPU for full-width layers, where the CPU
+        would copy ~8 GB of fp32 experts per layer per call). ``router_margin`` (a list) receives, per token, the
+        smallest gap over the layers between the router logits of its k-th and (k+1)-th expert: where that gap is
+        within bf16 noise the bf16 engine may route the token to a different expert, a discontinuity no logit
+        tolerance covers. Returns CPU fp32 logits."""
         c = self.cfg
-        wf = {k: v.float().cpu() for k, v in self.w.items()}
+        dev = torch.device(device)
+        wf = {k: v.to(dev, torch.float32) for k, v in self.w.items()}
         T, hd = token_ids.numel(), c.head_dim
-        h = wf["embed"][token_ids.long().cpu()]
-        cs = self.cos_sin.cpu()[:T]
+        h = wf["embed"][token_ids.long().to(dev)]
+        cs = self.cos_sin.to(dev)[:T]
         cos, sin = cs[:, None, : hd // 2], cs[:, None, hd // 2:]
 
         def rope(t):
@@ -262,25 +266,28 @@ class MixtralModel(LlamaModel):
             rep = self.hq // self.hkv
             k_, v = k_.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1)
             att = torch.einsum("qhd,khd->hqk", q, k_) * self.scale
-            att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1)[None], float("-inf"))
+            att = att.masked_fill(torch.ones(T, T, dtype=torch.bool, device=dev).triu(1)[None], float("-inf"))
             h = h + torch.einsum("hqk,khd->qhd", att.softmax(-1), v).reshape(T, -1) @ wf[p + "o"].t()
             x = rms(h, wf[p + "mlp_norm"])
             rl = x @ wf[p + "router"].t()
             if router_margin is not None:
                 top = torch.topk(rl, min(c.top_k + 1, rl.shape[-1]), -1).values
-                gap = top[:, c.top_k - 1] - top[:, -1] if top.shape[-1] > c.top_k else torch.full((T,), float("inf"))
+                gap = top[:, c.top_k - 1] - top[:, -1] if top.shape[-1] > c.top_k else \
+                    torch.full((T,), float("inf"), device=dev)
                 margin = gap if i == 0 else torch.minimum(margin, gap)
             pr = rl.softmax(-1)
             tw, ti = torch.topk(pr, c.top_k, -1)
             tw = tw / tw.sum(-1, keepdim=True)
             out = torch.zeros_like(x)
-            for t in range(T):
-                for j in range(c.top_k):
-                    e = int(ti[t, j])
-                    gu = (x[t] @ wf[p + "w13"][e].t()).reshape(-1, 2, 16)
-                    g = (torch.nn.functional.silu(gu[:, 0]) * gu[:, 1]).reshape(-1)
-                    out[t] += tw[t, j] * (g @ wf[p + "w2"][e].t())
+            for e in range(c.num_experts):  # every expert over the tokens routed to it (same math per token)
+                sel = (ti == e).nonzero()
+                if sel.numel() == 0:
+                    continue
+                t_idx, j_idx = sel[:, 0], sel[:, 1]
+                gu = (x[t_idx] @ wf[p + "w13"][e].t()).reshape(len(t_idx), -1, 2, 16)
+                g = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(len(t_idx), -1)
+                out.index_add_(0, t_idx, tw[t_idx, j_idx][:, None] * (g @ wf[p + "w2"][e].t()))
             h = h + out
         if router_margin is not None:
-            router_margin.append(margin)
-        return rms(h, wf["norm"]) @ wf["lm_head"].t()
+            router_margin.append(margin.cpu())
+        return (rms(h, wf["norm"]) @ wf["lm_head"].t()).cpu()

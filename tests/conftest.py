@@ -26,6 +26,20 @@ def pytest_collection_modifyitems(session, config, items):
 
 
 @pytest.fixture(scope="session")
+def gpu_box():
+    """For the multi-rank rehearsals: a GPU is present and the extension loads, checked WITHOUT initialising HIP in
+    this (parent) process - device_count() does not on this image - so the parent holds no hardware queue while the
+    ranks it spawns spin-wait on each other."""
+    import torch
+
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    from generativeaiexamples_amd import ops
+
+    ops.native()
+
+
+@pytest.fixture(scope="session")
 def cuda():
     import torch
 

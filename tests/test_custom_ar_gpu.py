@@ -1,40 +1,26 @@
 """One-shot peer-memory all-reduce (csrc/comm/custom_ar.hip, parallel/custom_ar.py) on a one-GPU
 box: 2, 4 and 8 ranks (the Llama-3-70B TP8 instantiation) share cuda:0 and exchange IPC handles over gloo; the result must equal the
 fp32 sum of every rank's input (eager and HIP-graph replay). Multi-GPU xGMI runs go through the
-same kernel with peers on other devices."""
+same kernel with peers on other devices. Co-residency of the ranks is a checked precondition (a probe
+all-reduce per rank, tests/_multirank.py), so a time-sliced world fails with the queue census, not a timeout."""
 import json
-import socket
 
 import pytest
-import torch.multiprocessing as mp
 
 from tests import _dist_workers as W
+from tests import _multirank as M
 
 pytestmark = [pytest.mark.gpu, pytest.mark.multirank]
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_custom_allreduce_matches_sum(tmp_path, world, cuda):
-    ctx = mp.get_context("spawn")
-    port = _port()
-    procs = [ctx.Process(target=W.custom_ar_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(100)
-    for p in procs:
-        if p.is_alive():
-            p.kill()
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+def test_custom_allreduce_matches_sum(tmp_path, world, gpu_box):
+    run = M.run_ranks(W.custom_ar_worker, world, (M.free_port(), str(tmp_path)), 100)
+    pr = M.assert_coresident(tmp_path, "car", world, run)
+    assert not any(run.late), f"ranks still running at the deadline: {run.late}; census {run.peak}"
+    assert all(c == 0 for c in run.exitcodes), run.exitcodes
     for r in range(world):
         res = json.loads((tmp_path / f"car_{r}.json").read_text())
         assert res["errors"] == [], res["errors"]
-        print(f"world {world} rank {r}: 1 MiB all-reduce {res['us_1MiB']:.1f} us (shared GPU)")
+        print(f"world {world} rank {r}: probe {pr.get(r, float('nan')):.1f} us, 1 MiB all-reduce {res['us_1MiB']:.1f} us "
+              "(shared GPU)")

@@ -162,3 +162,42 @@ def test_watchdog_fails_new_admissions_fast():
     asyncio.run(go())
     assert not eng.healthy
     eng.shutdown()
+
+
+def test_ep_exchange_error_word_raises_and_retires(tmp_path):
+    """an expert-parallel engine polls its peer-memory all-to-all's error word at the end of
+    every step; a set word raises RankFailure and retires the exchange (no stale-slot tokens are returned)."""
+    import torch
+    import torch.distributed as dist
+
+    from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
+    from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
+    from generativeaiexamples_amd.models.mixtral import MixtralConfig, MixtralModel
+    from generativeaiexamples_amd.parallel.custom_ar import CustomAllReduce
+    from generativeaiexamples_amd.parallel.dist import DistContext
+    from generativeaiexamples_amd.parallel.fault import RankFailure
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        m = MixtralModel(MixtralConfig.tiny_moe(), device="cpu", dtype=torch.float32, dist_ctx=DistContext(),
+                         ep_group=dist.group.WORLD).random_init(1)
+
+        class FakeXchg:  # the error word of a CustomAllReduce after a peer missed the bounded spin
+            err = torch.ones(1, dtype=torch.int32)
+            rank = 0
+            check = CustomAllReduce.check
+
+        m.ep_xchg = FakeXchg()
+        eng = LLMEngine(m, small_byte_tokenizer(512), EngineConfig(num_blocks=32, max_model_len=64, use_graphs=False))
+        eng.add_request([5, 6, 7], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
+        with pytest.raises(RankFailure):
+            while eng.has_work():
+                eng.step()
+        assert m.ep_xchg is None
+        FakeXchg.err.zero_()
+    finally:
+        dist.destroy_process_group()
