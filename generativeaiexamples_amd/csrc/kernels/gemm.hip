@@ -60,6 +60,10 @@ int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, con
   if (D != 128 || kv_fp8 || M < 1024 || K % 64 || K < 192 || (size_t)M * K * 2 >= (1ull << 31) ||
       (size_t)N * K * 2 >= (1ull << 31))
     return 0;
+  // the fused epilogue rides on the 256x256 tile walk; when its tiles fill less than half the grid (QKV of a TP = 8
+  // Llama-3-70B shard: N 1280, 50 tiles at M = 2407 -> 169 us, 0.3 PF/s) the caller's plain GEMM (stream-K for deep K)
+  // plus the rope_kv kernel is faster
+  if (2 * ring_tiles(M, N) < sk_grid()) return 0;
   RopeKvArgs rk;
   rk.pos = pos;
   rk.cos_sin = cos_sin;

@@ -336,7 +336,9 @@ int dec2_pick_nt(int N, int K, bool swiglu) {
   // 64: measured on MI355X (profiles/r2/dec2_minwg_sweep.txt) the widest tile wins on the wide shapes
   // (gate_up+SwiGLU at M = 64: 54.9 us with 224 workgroups vs 66.4 us with 448): every workgroup re-stages
   // the whole activation K range, so fewer, wider workgroups move fewer bytes through the load path
-  static const int min_wg = getenv("GAI_DEC2_MINWG") ? atoi(getenv("GAI_DEC2_MINWG")) : 64;
+  // 128 since round 5: at TP = 8 shard widths (LM head N 16032, O / down N 8192) the 64-workgroup tile left half
+  // the CUs idle (LM head 53.2 -> 49.6 us, O 14.7 -> 10.5, down 28.8 -> 22.2; Llama-3-8B shapes pick the same tile)
+  static const int min_wg = getenv("GAI_DEC2_MINWG") ? atoi(getenv("GAI_DEC2_MINWG")) : 128;
   if (force) return dec2_shape_ok<MB>(force, K) && !(swiglu && force < 2) ? force : 0;
   // widest column tile (least activation re-staging) that still gives every CU a workgroup; at MB = 1
   // the NT = 8 body (64 unrolled steps, 186 VGPRs) ran 4.6x slower than NT = 4 (lm_head, M = 1)
@@ -362,12 +364,13 @@ bool dec2_run(const void* A, const void* W, void* C, const void* bias, const voi
 
 }  // namespace
 
-// Wide projections only (gate_up, LM head: N >= 16384 by default): there the activation re-staging is
+// Wide projections only (gate_up, LM head, TP-shard O / down: N >= 8192 by default): there the activation re-staging is
 // <= 1/2 of the weight bytes and this kernel beats the split-K kernels (gate_up+SwiGLU 54.9 vs 80.9 us,
 // LM head 233 vs 327 us at M = 64). On the narrow ones (QKV, O, down) every column tile needs the whole
 // activation K range, 2-4x the weight bytes, and the split-K kernels stay ahead.
 int gai_gemm_dec2_ok(int M, int N, int K, int epi) {
-  static const int min_n = getenv("GAI_DEC2_MINN") ? atoi(getenv("GAI_DEC2_MINN")) : 16384;
+  // N >= 8192 since round 5 (TP shards: O and down of Llama-3-70B at TP = 8, N 8192, run faster here than split-K)
+  static const int min_n = getenv("GAI_DEC2_MINN") ? atoi(getenv("GAI_DEC2_MINN")) : 8192;
   if (M < 1 || M > 64 || N % 16 || N < min_n || (epi == EPI_SWIGLU && N % 32)) return 0;
   static const bool off = getenv("GAI_DEC2") && atoi(getenv("GAI_DEC2")) == 0;
   if (off) return 0;
@@ -396,6 +399,10 @@ namespace {
 // streams; down at N = 4096: NT = 4 x KS = 4 = 256), else the smallest KS (2..16) whose per-workgroup K range
 // fits the unrolled loop and that gives >= 192 workgroups (a K range per CU long enough to stream, few slabs;
 // NT = 8 x KS = 7 = 224, 1/8 of the CUs idle).
+// The exact split is taken only while its fp32 slabs (written, then read by the tail: 8 KS M N bytes) stay within
+// 1/8 of the weight bytes (2 N K): a TP = 8 shard of Llama-3-70B gate_up (N 7168, K 8192) has its only exact split at
+// KS = 16, whose slabs are half the weight stream - 47.8 us vs 30.6 us at KS = 2 (224 workgroups;
+// profiles/r5/tp8_rank/dec_hbm_sweep.txt).
 template <int MB>
 int dec2_part_ks(int N, int K, int NT, bool exact) {
   const int blocks = (N + 16 * NT - 1) / (16 * NT);
@@ -404,7 +411,7 @@ int dec2_part_ks(int N, int K, int NT, bool exact) {
     return K % force_ks == 0 && (K / force_ks) % 32 == 0 && dec2_shape_ok<MB>(NT, K / force_ks) ? force_ks : 0;
   for (int KS = 2; KS <= 16; ++KS) {
     if (K % KS || (K / KS) % 32 || !dec2_shape_ok<MB>(NT, K / KS)) continue;
-    if (exact ? (blocks * KS) % 256 == 0 : blocks * KS >= 192) return KS;
+    if (exact ? (blocks * KS) % 256 == 0 && 4 * KS * 16 * MB * 8 <= K : blocks * KS >= 192) return KS;
   }
   return 0;
 }
@@ -419,7 +426,8 @@ template <int MB, bool PSW>
 int dec2_part_run(const void* A, const void* W, int M, int N, int K, float* ws, hipStream_t st, bool launch) {
   const int force = dec2_part_nt_env();
   if (MB > 1 && force != 8) {
-    const int KS4 = dec2_part_ks<MB>(N, K, 4, force != 4);
+    int KS4 = dec2_part_ks<MB>(N, K, 4, force != 4);
+    if (!KS4 && force != 4) KS4 = dec2_part_ks<MB>(N, K, 4, false);  // no cheap exact split: >= 192 workgroups
     if (KS4) {
       if (launch)
         dec2_launch<MB, 4, EPI_NONE, true, true, PSW>(A, W, nullptr, nullptr, nullptr, M, N, K, N, st, KS4, ws);

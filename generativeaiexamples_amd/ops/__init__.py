@@ -470,7 +470,10 @@ class DecodeWorkspace:
         768-key splits (2048 WGs = 2.67 waves, a 1/3-empty last wave) 5.04 TB/s; 256-key splits
         4.5 TB/s (per-workgroup prologue / combine not amortised)."""
         if target_wgs is None:
-            target_wgs = _DECODE_TARGET_WGS
+            # few (sequence, kv head) pairs - a TP shard with one kv head per rank - take one resident wave (2
+            # workgroups per CU): Llama-3-70B TP = 8 rank, B = 64, ctx 2500: 10.63 -> 10.27 ms per decode step
+            # (profiles/r5/tp8_rank); Llama-3-8B at B = 64 (512 pairs) keeps 1024
+            target_wgs = _DECODE_TARGET_WGS if batch * hkv > 64 or hkv > 2 or _DECODE_TARGET_ENV else 512
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128
@@ -485,6 +488,7 @@ class DecodeWorkspace:
 # With the non-temporal K / V loads (attention.hip) two splits per (sequence, kv head) beat three at B = 64:
 # ctx 2535 graph replay 7.68 -> 7.47 ms per step at 1024 target workgroups (768 the same, 2048 7.71;
 # profiles/r4/decode/decode_nt_split_ab.txt). GAI_DECODE_TARGET_WGS overrides (sweeps).
+_DECODE_TARGET_ENV = "GAI_DECODE_TARGET_WGS" in os.environ
 _DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1024"))
 _DECODE_MAX_SPLIT = int(os.environ.get("GAI_DECODE_MAX_SPLIT", "2048"))  # keys per split, upper bound (sweeps)
 _DECODE_ADAPTIVE = os.environ.get("GAI_DECODE_ADAPTIVE", "1") == "1"

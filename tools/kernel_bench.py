@@ -259,6 +259,12 @@ def main():
                    (M, 28672, 4096, "swiglu", bf, f"gate_up+swiglu b{M}"), (M, 4096, 14336, None, bf, f"down b{M}"),
                    (M, 128256, 4096, None, f32, f"lm_head b{M}")]
         bench_dec_hbm(rows, sh)
+    if "dec_hbm_tp8" in only:  # one rank of Llama-3-70B at TP = 8, batch 64
+        bf, f32 = torch.bfloat16, torch.float32
+        bench_dec_hbm(rows, [(64, 1280, 8192, None, bf, "70b/tp8 qkv b64"), (64, 8192, 1024, None, bf, "70b/tp8 o b64"),
+                             (64, 7168, 8192, "swiglu", bf, "70b/tp8 gate_up+swiglu b64"),
+                             (64, 8192, 3584, None, bf, "70b/tp8 down b64"),
+                             (64, 16032, 8192, None, f32, "70b/tp8 lm_head b64")], rounds=3)
     if "fp8" in only:
         bench_fp8(rows, [(4096, 6144, 4096, "qkv prefill"), (4096, 28672, 4096, "gate_up prefill"),
                          (4096, 4096, 14336, "down prefill"), (8192, 8192, 8192, "square 8k"),
