@@ -582,7 +582,8 @@ void gemv_rope_kv(const Tensor& x, const optional<Tensor>& gamma, double eps, co
 
 void custom_all_to_all(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
                        const std::vector<int64_t>& sig_ptrs, Tensor& counters, Tensor& err, int64_t rank,
-                       int64_t slot_bytes) {
+                       int64_t slot_bytes, const optional<Tensor>& send_rows, const optional<Tensor>& recv_rows,
+                       int64_t row_bytes) {
   check_dev(inp, "inp");
   check_dev(out, "out");
   TORCH_CHECK(inp.is_contiguous() && out.is_contiguous(), "custom_all_to_all: contiguous tensors");
@@ -600,9 +601,22 @@ void custom_all_to_all(const Tensor& inp, Tensor& out, const std::vector<int64_t
     d[q] = reinterpret_cast<void*>(data_ptrs[q]);
     s[q] = reinterpret_cast<uint32_t*>(sig_ptrs[q]);
   }
+  const int* sr = nullptr;
+  const int* rr = nullptr;
+  if (send_rows || recv_rows) {
+    TORCH_CHECK(send_rows && recv_rows, "custom_all_to_all: send_rows and recv_rows go together");
+    check_i32(*send_rows, "send_rows");
+    check_i32(*recv_rows, "recv_rows");
+    TORCH_CHECK(send_rows->numel() == world && recv_rows->numel() == world && send_rows->is_contiguous() &&
+                    recv_rows->is_contiguous(), "custom_all_to_all: row counts [world]");
+    TORCH_CHECK(row_bytes > 0 && row_bytes % 16 == 0 && (bytes / world) % row_bytes == 0,
+                "custom_all_to_all: segments must hold whole rows of a multiple of 16 bytes");
+    sr = send_rows->data_ptr<int>();
+    rr = recv_rows->data_ptr<int>();
+  }
   gai_custom_all_to_all(inp.data_ptr(), out.data_ptr(), bytes / world, d, s,
                         reinterpret_cast<uint32_t*>(counters.data_ptr()), (int)rank, world, slot_bytes,
-                        err.data_ptr<int>(), cur_stream());
+                        err.data_ptr<int>(), cur_stream(), sr, rr, row_bytes);
 }
 
 void ep_pack(const Tensor& x, const Tensor& ids, const Tensor& offs, const Tensor& a_pairs, int64_t W, int64_t C,

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "gai_common.h"
@@ -86,6 +87,18 @@ __device__ __forceinline__ void wait_epoch(uint32_t* f, uint32_t e, uint32_t lim
       break;
     }
   }
+}
+
+// Workgroups of one all-to-all launch (they loop over the chunks). Every workgroup spin-waits for its peers', so all
+// ranks' workgroups must be resident at once: one GPU per rank holds 512 easily, but W ranks sharing ONE GPU (the
+// one-GPU rehearsals: 8 workgroups of 256 threads per CU = 2048 on 256 CUs) need GAI_AR_MAX_GRID <= 2048 / W.
+static int ar_max_grid() {
+  static const int v = [] {
+    const char* e = getenv("GAI_AR_MAX_GRID");
+    const int g = e ? atoi(e) : GAI_AR_MAX_BLOCKS;
+    return g < 1 ? 1 : g > GAI_AR_MAX_BLOCKS ? GAI_AR_MAX_BLOCKS : g;
+  }();
+  return v;
 }
 
 template <int W, bool F32>
@@ -303,29 +316,39 @@ __global__ __launch_bounds__(kArThreads) void ar_twoshot_kernel(const uint4* in,
 
 
 // One-shot all-to-all on the same buffers (expert-parallel token exchange, parallel/ep.py): the input is W
-// equal segments, segment q bound for rank q. Block b owns chunk b of every segment: it pushes chunk b of
-// segment q into slot `rank` of peer q's data area (direct xGMI writes, all peers at once), signals every
-// peer with the block's epoch, waits for all of them, then copies chunk b of every local slot q into output
-// segment q. Epochs, parities and the bounded wait are the one-shot all-reduce's (shared counters and
-// signals: every rank issues the same sequence of collectives), so it replays from a HIP graph too.
+// equal segments, segment q bound for rank q. Block b owns chunks b, b + G, ... of every segment: it pushes them
+// into slot `rank` of peer q's data area (direct xGMI writes, all peers at once), signals every peer with the
+// block's epoch, waits for all of them, then copies the same chunks of every local slot q into output segment q.
+// Epochs, parities and the bounded wait are the one-shot all-reduce's (shared counters and signals: every rank
+// issues the same sequence of collectives), so it replays from a HIP graph too.
+// Variable segments (send_rows / recv_rows, device int32 [W], optional): only the first send_rows[q] rows
+// (row16 16-B vectors each) of segment q are pushed and only the first recv_rows[q] rows of slot q are copied out
+// - a capacity-sized slab of which only the valid rows cross xGMI, with the counts known on the device only (the
+// expert-parallel prefill exchange needs no host round trip). Rows past a count are left untouched in `out`.
 template <int W>
 __global__ __launch_bounds__(kArThreads) void a2a_oneshot_kernel(const uint4* in, uint4* out, ArPtrs p,
                                                                  uint32_t* __restrict__ counters, int rank,
-                                                                 int64_t seg16, int64_t slot_bytes, int* err) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+                                                                 int64_t seg16, int64_t slot_bytes, int* err,
+                                                                 const int* __restrict__ send_rows,
+                                                                 const int* __restrict__ recv_rows, int64_t row16,
+                                                                 int nchunks) {
+  const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
   __shared__ uint32_t e_sh;
   if (tid == 0) e_sh = counters[b] + 1u;
   __syncthreads();
   const uint32_t e = e_sh;
   const int par = (int)(e & 1u);
   constexpr int64_t kVec = GAI_AR_CHUNK / 16;
-  const int64_t v0 = (int64_t)b * kVec, v1 = min(v0 + kVec, seg16);
   const int64_t my_off = ((int64_t)par * W + rank) * slot_bytes;
 #pragma unroll
   for (int q = 0; q < W; ++q) {
     uint4* dst = reinterpret_cast<uint4*>(p.data[q] + my_off);
     const uint4* src = in + (int64_t)q * seg16;
-    for (int64_t v = v0 + tid; v < v1; v += kArThreads) dst[v] = src[v];
+    const int64_t lim = send_rows ? min(seg16, (int64_t)send_rows[q] * row16) : seg16;
+    for (int c = b; c < nchunks; c += G) {
+      const int64_t v1 = min((int64_t)(c + 1) * kVec, lim);
+      for (int64_t v = (int64_t)c * kVec + tid; v < v1; v += kArThreads) dst[v] = src[v];
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
@@ -341,7 +364,11 @@ __global__ __launch_bounds__(kArThreads) void a2a_oneshot_kernel(const uint4* in
   for (int q = 0; q < W; ++q) {
     const uint4* src = reinterpret_cast<const uint4*>(base + q * slot_bytes);
     uint4* dst = out + (int64_t)q * seg16;
-    for (int64_t v = v0 + tid; v < v1; v += kArThreads) dst[v] = src[v];
+    const int64_t lim = recv_rows ? min(seg16, (int64_t)recv_rows[q] * row16) : seg16;
+    for (int c = b; c < nchunks; c += G) {
+      const int64_t v1 = min((int64_t)(c + 1) * kVec, lim);
+      for (int64_t v = (int64_t)c * kVec + tid; v < v1; v += kArThreads) dst[v] = src[v];
+    }
   }
   if (tid == 0) counters[b] = e;
 }
@@ -350,11 +377,14 @@ __global__ __launch_bounds__(kArThreads) void a2a_oneshot_kernel(const uint4* in
 
 void gai_custom_all_to_all(const void* in, void* out, int64_t seg_bytes, void* const* peer_data,
                            uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
-                           int* err, hipStream_t st) {
+                           int* err, hipStream_t st, const int* send_rows, const int* recv_rows, int64_t row_bytes) {
   if (seg_bytes == 0) return;
   if (seg_bytes % 16 || seg_bytes > slot_bytes) gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: segment size");
-  const int64_t nblk = (seg_bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
-  if (nblk > GAI_AR_MAX_BLOCKS) gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: segment too large");
+  if ((send_rows || recv_rows) && (row_bytes <= 0 || row_bytes % 16))
+    gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: row_bytes must be a positive multiple of 16");
+  const int64_t nchunks = (seg_bytes + GAI_AR_CHUNK - 1) / GAI_AR_CHUNK;
+  if (nchunks > (int64_t)1 << 30) gai_launch_error(__FILE__, __LINE__, "custom_all_to_all: segment too large");
+  const int nblk = (int)std::min<int64_t>(nchunks, ar_max_grid());  // blocks loop over the chunks
   ArPtrs p{};
   p.spin_limit = ar_spin_limit();
   for (int q = 0; q < world; ++q) {
@@ -363,8 +393,9 @@ void gai_custom_all_to_all(const void* in, void* out, int64_t seg_bytes, void* c
   }
 #define GAI_A2A(WW)                                                                                             \
   if (world == WW) {                                                                                            \
-    a2a_oneshot_kernel<WW><<<(int)nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p, counters, rank,  \
-                                                             seg_bytes / 16, slot_bytes, err);                  \
+    a2a_oneshot_kernel<WW><<<nblk, kArThreads, 0, st>>>((const uint4*)in, (uint4*)out, p, counters, rank,       \
+                                                        seg_bytes / 16, slot_bytes, err, send_rows, recv_rows,  \
+                                                        row_bytes / 16, (int)nchunks);                         \
     GAI_LAUNCH_CHECK();                                                                                         \
     return;                                                                                                     \
   }

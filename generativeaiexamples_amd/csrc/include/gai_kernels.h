@@ -143,7 +143,8 @@ void gai_custom_allreduce(const void* in, void* out, int64_t bytes, int f32, voi
 // one-shot all-to-all of W equal segments over the one-shot all-reduce's buffers / signals
 void gai_custom_all_to_all(const void* in, void* out, int64_t seg_bytes, void* const* peer_data,
                            uint32_t* const* peer_sig, uint32_t* counters, int rank, int world, int64_t slot_bytes,
-                           int* err, hipStream_t st);
+                           int* err, hipStream_t st, const int* send_rows = nullptr, const int* recv_rows = nullptr,
+                           int64_t row_bytes = 0);
 void gai_custom_allreduce_twoshot(const void* in, void* out, int64_t bytes, int f32, void* const* peer_data,
                                   uint32_t* const* peer_sig, uint32_t* counters, int rank, int world,
                                   int64_t region_bytes, int* err, hipStream_t st);

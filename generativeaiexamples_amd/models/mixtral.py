@@ -13,9 +13,9 @@ Expert parallelism, two modes:
   outputs - no extra collective.
 * EP mode (``ep_group``): data-parallel attention (every rank holds attention / embeddings and serves
   its own requests) + experts sharded over the EP group, tokens exchanged with all-to-all
-  (:mod:`..parallel.ep`): decode-sized steps use the fixed-capacity, sync-free padded exchange (capacity =
-  the step's largest per-rank token count, agreed by the engine's EP lockstep, ``LLMEngine``), prefill
-  steps the exact-count exchange. Ranks step in lockstep; a rank without work runs a one-token dummy
+  (:mod:`..parallel.ep`): every step uses the fixed-capacity, sync-free padded exchange (capacity = the
+  step's largest per-rank token count, agreed by the engine's EP lockstep, ``LLMEngine``); prefill steps
+  exchange the per-peer counts on the device and move only the valid rows. Ranks step in lockstep; a rank without work runs a one-token dummy
   forward so every all-to-all has all its peers.
 """
 from __future__ import annotations
@@ -83,7 +83,9 @@ class MixtralModel(LlamaModel):
         if (ep_group is not None and self.ep_size > 1 and self.device.type == "cuda"
                 and os.environ.get("GAI_EP_A2A", "peer") != "rccl"):
             from ..parallel.custom_ar import CustomAllReduce
-            self.ep_xchg = CustomAllReduce(group=ep_group, device=self.device)
+            # slots for the prefill slabs too (GAI_EP_A2A_MAX_MB per peer segment; larger slabs go to RCCL)
+            a2a_mb = int(os.environ.get("GAI_EP_A2A_MAX_MB", "64"))
+            self.ep_xchg = CustomAllReduce(group=ep_group, device=self.device, a2a_max_bytes=a2a_mb << 20)
 
     def _alloc(self):
         c = self.cfg
@@ -177,19 +179,14 @@ class MixtralModel(LlamaModel):
         from ..parallel import ep
 
         c = self.cfg
-        if self.ep_exact:  # prefill-sized step somewhere in the group: exact counts (one host sync)
-            rows, eid, plan = ep.dispatch(x, ids, wts, c.num_experts, group=self.ep_group)
-            y = ep.local_experts(rows, eid, w13, w2)
-            out = ep.combine(y, wts, plan, group=self.ep_group)
-        else:  # decode: fixed capacity agreed for this step, no host sync (graph-capturable)
-            cap = max(self.ep_capacity_tokens, x.shape[0]) * c.top_k
-            rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group,
-                                                 xchg=self.ep_xchg)
-            y = ep.local_experts_padded(rows, eid, w13, w2)
-            return ep.combine_padded(y, wts, plan, group=self.ep_group, xchg=self.ep_xchg, residual=residual)
-        if residual is not None:
-            out = out + residual
-        return out
+        # capacity: the step's largest per-rank token count (EP lockstep) x top-k - never drops a pair. Prefill-sized
+        # steps (ep_exact) exchange the per-peer counts on the device and move only the valid rows; decode steps
+        # move whole slabs (graph-capturable). Neither synchronises the host.
+        cap = max(self.ep_capacity_tokens, x.shape[0]) * c.top_k
+        rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group,
+                                             xchg=self.ep_xchg, exact_counts=self.ep_exact)
+        y = ep.local_experts_padded(rows, eid, w13, w2)
+        return ep.combine_padded(y, wts, plan, group=self.ep_group, xchg=self.ep_xchg, residual=residual)
 
     def _moe_down_ep(self, h1, w2, offs, rows):
         y = ops.moe_gemm(h1, None, w2, offs, rows, swiglu=False)

@@ -47,7 +47,13 @@ def _native():
 class CustomAllReduce:
     """Peer-memory all-reduce over one process group. All ranks must construct it together."""
 
-    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 8 << 20):
+    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 8 << 20,
+                 a2a_max_bytes: int = 0):
+        """max_bytes: largest all-reduce (<= AR_CHUNK x AR_MAX_BLOCKS = 8 MiB); a2a_max_bytes: largest all-to-all
+        segment (the expert-parallel prefill slabs; the all-to-all kernel's blocks loop over chunks). Every
+        collective uses one slot size, the larger of the two: the collectives share the epoch counters, and a
+        peer may write call e + 1 while this rank still reads call e, so the parity regions of consecutive calls
+        must not overlap."""
         C = _native()
         self.group = group
         self.world = dist.get_world_size(group)
@@ -56,9 +62,11 @@ class CustomAllReduce:
             raise ValueError("CustomAllReduce supports 2..8 ranks")
         max_bytes = min(int(max_bytes), C.AR_CHUNK * C.AR_MAX_BLOCKS)
         self.max_bytes = max_bytes - max_bytes % C.AR_CHUNK
+        a2a = -(-max(int(a2a_max_bytes), self.max_bytes) // C.AR_CHUNK) * C.AR_CHUNK
+        self.slot_bytes = a2a
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         with torch.cuda.device(self.device):
-            self._data = C.ipc_malloc(2 * self.world * self.max_bytes)
+            self._data = C.ipc_malloc(2 * self.world * self.slot_bytes)
             self._sig = C.ipc_malloc(C.AR_MAX_BLOCKS * 8 * 4)
             handles = (C.ipc_get_handle(self._data), C.ipc_get_handle(self._sig))
             allh: List = [None] * self.world
@@ -124,21 +132,26 @@ class CustomAllReduce:
                                                self.rank, self.region_bytes)
         else:
             _native().custom_allreduce(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
-                                       self.max_bytes)
+                                       self.slot_bytes)
         return out
 
     def eligible_a2a(self, t: torch.Tensor) -> bool:
         """Equal-split all-to-all of ``t`` (dim 0 split into world segments) fits the one-shot buffers."""
         nbytes = t.numel() * t.element_size()
         return (not self._closed and t.is_cuda and t.is_contiguous() and nbytes % (16 * self.world) == 0
-                and 0 < nbytes // self.world <= self.max_bytes)
+                and 0 < nbytes // self.world <= self.slot_bytes)
 
-    def all_to_all(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def all_to_all(self, t: torch.Tensor, out: Optional[torch.Tensor] = None, send_rows: Optional[torch.Tensor] = None,
+                   recv_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Segment q of ``t`` (dim 0 in world equal parts) goes to rank q; segment q of the result came from rank
-        q. Direct peer writes, one hop, graph-capturable (csrc/comm/custom_ar.hip a2a_oneshot_kernel)."""
+        q. Direct peer writes, one hop, graph-capturable (csrc/comm/custom_ar.hip a2a_oneshot_kernel).
+        send_rows / recv_rows (device int32 [world], together): only the first send_rows[q] rows (dim-0 rows of
+        ``t``) of segment q cross to rank q, and only the first recv_rows[q] rows of the result's segment q are
+        written (the rest keep ``out``'s previous contents); the counts never leave the device."""
         out = torch.empty_like(t) if out is None else out
+        row_bytes = t[0].numel() * t.element_size() if send_rows is not None else 0
         _native().custom_all_to_all(t, out, self.data_ptrs, self.sig_ptrs, self.counters, self.err, self.rank,
-                                    self.max_bytes)
+                                    self.slot_bytes, send_rows, recv_rows, row_bytes)
         return out
 
     def eligible_rmsnorm(self, t: torch.Tensor) -> bool:
@@ -150,7 +163,7 @@ class CustomAllReduce:
         """residual += all_reduce(t); return rmsnorm(residual) * w - one kernel (see custom_ar.hip)."""
         out = torch.empty_like(t) if out is None else out
         _native().custom_allreduce_rmsnorm(t, out, residual, w, eps, self.data_ptrs, self.sig_ptrs, self.counters,
-                                           self.err, self.rank, self.max_bytes)
+                                           self.err, self.rank, self.slot_bytes)
         return out
 
     def check(self) -> None:
