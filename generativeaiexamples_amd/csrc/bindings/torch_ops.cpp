@@ -193,7 +193,9 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                  const Tensor& ctx_lens, Tensor& out, Tensor& ws_o, Tensor& ws_ml, double scale, int64_t split_keys,
-                 int64_t max_splits, double k_scale, double v_scale, const c10::optional<Tensor>& split_cnt) {
+                 int64_t max_splits, double k_scale, double v_scale, const c10::optional<Tensor>& split_cnt,
+                 const c10::optional<Tensor>& qkv_part, int64_t part_ks, const c10::optional<Tensor>& positions,
+                 const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& slots) {
   check_bf16(q, "q");
   const int f8 = kv_cache_fp8(k_cache, v_cache);
   check_i32(block_tables, "block_tables");
@@ -211,10 +213,46 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
     TORCH_CHECK(split_cnt->numel() >= (int64_t)B * Hkv, "attn_decode: split_cnt too small");
     cnt = split_cnt->data_ptr<int>();
   }
+  GaiQkvFold fold;
+  const GaiQkvFold* fp = nullptr;
+  if (qkv_part.has_value() && qkv_part->defined()) {
+    // decode QKV tail folded into this launch: q comes from the split-K partial slabs [part_ks, B, (Hq + 2 Hkv) D]
+    check_f32(*qkv_part, "qkv_part");
+    TORCH_CHECK(positions && cos_sin && slots, "attn_decode: the folded QKV tail needs positions, cos_sin, slots");
+    check_i32(*positions, "positions");
+    check_i32(*slots, "slots");
+    check_f32(*cos_sin, "cos_sin");
+    const int64_t n = (int64_t)(Hq + 2 * Hkv) * D;
+    TORCH_CHECK(f8 == 0 && D == 128, "attn_decode: the folded QKV tail needs head_dim 128 and a bf16 cache");
+    TORCH_CHECK(part_ks >= 1 && part_ks <= 8 && qkv_part->numel() >= part_ks * B * n && qkv_part->is_contiguous(),
+                "attn_decode: qkv_part must hold part_ks x B x (Hq + 2 Hkv) x D floats");
+    TORCH_CHECK(positions->numel() >= B && slots->numel() >= B && cos_sin->size(-1) == D,
+                "attn_decode: positions / slots [B], cos_sin [max_pos, D]");
+    TORCH_CHECK(cnt != nullptr && max_splits > 1, "attn_decode: the folded QKV tail runs in the fused-merge kernel");
+    fold.part = qkv_part->data_ptr<float>();
+    fold.ks = (int)part_ks;
+    fold.n = (int)n;
+    fold.pos = positions->data_ptr<int>();
+    fold.cos_sin = cos_sin->data_ptr<float>();
+    fold.slots = slots->data_ptr<int>();
+    fp = &fold;
+  }
   gai_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                   block_tables.size(1), ctx_lens.data_ptr<int>(), out.data_ptr(), ws_o.data_ptr<float>(),
                   ws_ml.data_ptr<float>(), B, Hq, Hkv, D, (float)scale, split_keys, max_splits, f8, (float)k_scale,
-                  (float)v_scale, cur_stream(), cnt);
+                  (float)v_scale, cur_stream(), cnt, fp);
+}
+
+int64_t gemm_qkv_partials(const Tensor& A, const Tensor& W, Tensor& ws, bool psw) {
+  check_bf16(A, "A");
+  check_bf16(W, "W");
+  check_f32(ws, "ws");
+  TORCH_CHECK(A.dim() == 2 && A.is_contiguous(), "gemm_qkv_partials: A [M, K] contiguous");
+  const int M = A.size(0), K = A.size(1);
+  const int N = W.size(0);  // the fragment-shuffled copy keeps the [N, K] shape
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == K && W.is_contiguous(), "gemm_qkv_partials: W [N, K]");
+  TORCH_CHECK(ws.numel() >= (int64_t)gai_gemm_splitk_ws_bytes(M, N, K) / 4, "gemm_qkv_partials: workspace");
+  return gai_gemm_qkv_partials(A.data_ptr(), W.data_ptr(), M, N, K, ws.data_ptr<float>(), psw ? 1 : 0, cur_stream());
 }
 
 void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_p, const Tensor& top_k,
@@ -825,6 +863,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ep_pack", &ep_pack);
   m.def("ep_combine", &ep_combine);
   m.def("custom_all_to_all", &custom_all_to_all);
+  m.def("gemm_qkv_partials", &gemm_qkv_partials);
   m.def("gemv", &gemv);
   m.def("gemv_rope_kv", &gemv_rope_kv);
   m.def("embedding", &embedding);

@@ -66,10 +66,24 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
                       int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
                       float v_scale, hipStream_t st);
 int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
+// Decode QKV tail folded into the decode-attention launch: the split-K QKV partial slabs part[ks][B][n] (n = (Hq +
+// 2 Hkv) D, no bias) are summed, rounded to bf16, rotated (RoPE at pos[seq]) inside attn_decode; the split holding
+// the newest key also writes that key / value into the paged caches at slots[seq].
+struct GaiQkvFold {
+  const float* part = nullptr;
+  int ks = 0;
+  int n = 0;
+  const int* pos = nullptr;
+  const float* cos_sin = nullptr;
+  const int* slots = nullptr;
+};
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
                      int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
-                     float v_scale, hipStream_t st, int* split_cnt = nullptr);
+                     float v_scale, hipStream_t st, int* split_cnt = nullptr,
+                     const GaiQkvFold* fold = nullptr);
+// QKV partial slabs only (for GaiQkvFold): KS (2..8) when launched, 0 when the shape runs elsewhere.
+int gai_gemm_qkv_partials(const void* A, const void* B, int M, int N, int K, float* ws, int psw, hipStream_t st);
 
 // sampling.hip
 size_t gai_sample_ws_bytes(int B, int V);

@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "gai_common.h"
+#include "gai_rope.h"
 #include "gai_kernels.h"
 
 using namespace gai;
@@ -379,16 +380,23 @@ __device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_
 // Occupancy: unconstrained, the compiler takes 138 VGPRs + 32 AGPRs (2 workgroups per CU, 512 resident), and two
 // splits per (sequence, kv head) at B = 64 are exactly two rounds. Held to 3 per CU (no spill) with three splits it
 // measured 7.424 vs 7.332 ms per step (profiles/r4/decode/decode_nt_split_ab.txt): kept at 2.
-template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false, bool NTL = false>
+// QP (QkvFold): q is not read from memory - the prologue sums the split-K QKV partial slabs of this workgroup's
+// GQA group, rounds to bf16 (the rounding of the unfused GEMM output), applies RoPE (the rounding of rope_kv) and
+// stages the group's q rows in LDS; the split that holds the newest key also rotates / stores that key and value
+// into the paged caches before its own key loop reads them (the only split that reads that page). This replaces
+// the separate split-K RoPE / KV-write tail launch of the decode QKV projection.
+template <int D, bool PIPE, int H, bool V16, typename KV, bool FUSE = false, bool NTL = false, bool QP = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int Hq, int Hkv, float scale, int split_keys,
-    int max_splits, float k_scale, float v_scale, int* __restrict__ cnt) {
+    int max_splits, float k_scale, float v_scale, int* __restrict__ cnt, GaiQkvFold fold = GaiQkvFold{}) {
   static_assert(sizeof(KV) == 2 || V16, "fp8 KV decode uses the 16-key V^T loads");
+  static_assert(!QP || sizeof(KV) == 2, "the folded QKV tail writes bf16 caches");
   __shared__ __attribute__((aligned(16))) float red_o[4][D][16];
   __shared__ float red_m[4][16], red_l[4][16];
   __shared__ int s_last;
+  __shared__ __attribute__((aligned(16))) bf16 q_lds[QP ? 16 : 1][QP ? D : 8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, gq = lane >> 4;
   const int split = blockIdx.x, g = blockIdx.y, seq = blockIdx.z;
   const int ratio = Hq / Hkv;
@@ -402,7 +410,67 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int qi = lane & 15;  // GQA head index inside the group (MFMA column)
 
   bf16x8 qf[D / 32];
-  {
+  // QP prologue (called after this wave's first K / V chunk is in flight, so its latency hides under the stream):
+  // quarter-row items (4 + 4 rotation partners of one head) of the group's ratio q heads, plus its k and v head in
+  // the split that holds key ctx - 1
+  auto qp_prologue = [&]() {
+    constexpr int LPH = D / 8;
+    const int nh = ratio + (split == nsplit - 1 ? 2 : 0);
+    const size_t slab = (size_t)B * fold.n;
+    for (int it = tid; it < nh * LPH; it += 256) {
+      const int hh = it / LPH, i0 = (it % LPH) * 4;
+      const int habs = hh < ratio ? g * ratio + hh : hh == ratio ? Hq + g : Hq + Hkv + g;
+      const float* p1 = fold.part + (size_t)seq * fold.n + habs * D + i0;
+      float x[4] = {0.f, 0.f, 0.f, 0.f}, y[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < fold.ks; s0 += 4) {  // 4 slabs in flight; slab order from 0 (the split-K tails' rounding)
+        float4 a[4], b[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (s0 + s < fold.ks) {
+            a[s] = *reinterpret_cast<const float4*>(p1 + (s0 + s) * slab);
+            b[s] = *reinterpret_cast<const float4*>(p1 + (s0 + s) * slab + D / 2);
+          }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (s0 + s < fold.ks) {
+            x[0] += a[s].x; x[1] += a[s].y; x[2] += a[s].z; x[3] += a[s].w;
+            y[0] += b[s].x; y[1] += b[s].y; y[2] += b[s].z; y[3] += b[s].w;
+          }
+      }
+      bf16x4 x1, x2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x1[j] = (bf16)x[j];
+        x2[j] = (bf16)y[j];
+      }
+      if (hh < ratio) {
+        const int pp = fold.pos[seq];
+        const float4 c = *reinterpret_cast<const float4*>(fold.cos_sin + (size_t)pp * D + i0);
+        const float4 sn = *reinterpret_cast<const float4*>(fold.cos_sin + (size_t)pp * D + D / 2 + i0);
+        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float u = (float)x1[j], w = (float)x2[j];
+          x1[j] = (bf16)(u * cc[j] - w * ss[j]);
+          x2[j] = (bf16)(w * cc[j] + u * ss[j]);
+        }
+        *reinterpret_cast<bf16x4*>(&q_lds[hh][i0]) = x1;
+        *reinterpret_cast<bf16x4*>(&q_lds[hh][i0 + D / 2]) = x2;
+      } else {
+        rope_kv_store<D, bf16>(x1, x2, seq, habs, i0, fold.pos, fold.cos_sin, fold.slots, nullptr,
+                               const_cast<bf16*>(reinterpret_cast<const bf16*>(kc)),
+                               const_cast<bf16*>(reinterpret_cast<const bf16*>(vc)), Hq, Hkv, 1, 1.f, 1.f);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new key / value have landed before any wave reads them
+    __syncthreads();
+    const bool qv = qi < ratio;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+      qf[t] = qv ? *reinterpret_cast<const bf16x8*>(&q_lds[qi][32 * t + 8 * gq]) : bf16x8{};
+  };
+  static_assert(!QP || !PIPE, "the folded QKV prologue runs in the non-pipelined loop");
+  if constexpr (!QP) {
     const bool qv = qi < ratio;
     const bf16* qp = q + ((size_t)seq * Hq + g * ratio + (qv ? qi : 0)) * D + 8 * gq;
 #pragma unroll
@@ -564,15 +632,33 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         if (kb >= kend) break;
       }
     }
-  } else if (kb < kend) {
+  } else if (!QP) {
+    if (kb < kend) {
+      Blk nb;
+      lookup(kb, nb);
+      for (; kb < kend; kb += kStep) {
+        Chunk c;
+        load_chunk_blk(kb, nb, c);  // blocks looked up one chunk earlier
+        // the next chunk's blocks, issued after this chunk's K/V loads (SMEM returns out of order, so a wait for the
+        // blocks in use would also wait for these) and landing under this chunk's compute; pages past the split
+        // clamp to its last page (looked up, never loaded)
+        lookup(kb + kStep, nb);
+        compute_chunk(kb, c);
+      }
+    }
+  } else {
+    // first chunk in flight before the prologue, unless it holds the newest key, whose value the prologue writes
     Blk nb;
-    lookup(kb, nb);
-    for (; kb < kend; kb += kStep) {
+    Chunk c0;
+    const bool live = kb < kend;
+    const bool pre = live && !(split == nsplit - 1 && kb <= ctx - 1 && ctx - 1 < kb + 32 * H);
+    if (live) lookup(kb, nb);
+    if (pre) load_chunk_blk(kb, nb, c0);
+    qp_prologue();  // every wave (barrier inside)
+    for (bool first = true; kb < kend; kb += kStep, first = false) {
       Chunk c;
-      load_chunk_blk(kb, nb, c);  // blocks looked up one chunk earlier
-      // the next chunk's blocks, issued after this chunk's K/V loads (SMEM returns out of order, so a wait for the
-      // blocks in use would also wait for these) and landing under this chunk's compute; pages past the split
-      // clamp to its last page (looked up, never loaded)
+      if (first && pre) c = c0;
+      else load_chunk_blk(kb, nb, c);
       lookup(kb + kStep, nb);
       compute_chunk(kb, c);
     }
@@ -718,7 +804,7 @@ int gai_attn_prefill_rows_per_tile(int Hq, int Hkv) {
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      int max_blocks, const int* ctx_lens, void* out, float* ws_o, float* ws_ml, int B, int Hq,
                      int Hkv, int D, float scale, int split_keys, int max_splits, int kv_fp8, float k_scale,
-                     float v_scale, hipStream_t st, int* split_cnt) {
+                     float v_scale, hipStream_t st, int* split_cnt, const GaiQkvFold* fold) {
   if (B == 0) return;
   if (Hq / Hkv > 16) gai_launch_error(__FILE__, __LINE__, "attn_decode: GQA ratio > 16 unsupported");
   if (split_keys < 0 || split_keys % 128)
@@ -732,6 +818,15 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   // non-temporal K / V loads in the fused bf16 kernel (GAI_DECODE_NT=0: plain loads). Llama-3-8B B = 64, ctx 2535
   // graph replay 7.84 -> 7.68 ms per step (profiles/r4/decode/decode_nt_split_ab.txt)
   static const bool ntl = !(getenv("GAI_DECODE_NT") && atoi(getenv("GAI_DECODE_NT")) == 0);
+  if (fold != nullptr && !(fuse && ntl && !kv_fp8 && D == 128 && fold->ks >= 1 && fold->ks <= 8))
+    gai_launch_error(__FILE__, __LINE__, "attn_decode: the folded QKV tail needs the fused non-temporal bf16 kernel");
+  if (fold != nullptr) {
+    attn_decode_kernel<128, false, 1, true, bf16, true, true, true><<<grid, 256, 0, st>>>(
+        (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, max_blocks, ctx_lens, (bf16*)out,
+        ws_o, ws_ml, B, Hq, Hkv, scale, split_keys, max_splits, k_scale, v_scale, split_cnt, *fold);
+    GAI_LAUNCH_CHECK();
+    return;
+  }
 #define GAI_DEC(DD)                                                                                             \
   if (D == DD && fuse && ntl && !kv_fp8) {                                                                      \
     attn_decode_kernel<DD, false, 1, true, bf16, true, true><<<grid, 256, 0, st>>>(                             \
@@ -759,7 +854,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                                  : attn_decode_kernel<DD, false, 1, true, fp8>;                                 \
       kern<<<grid, 256, 0, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache, block_tables,        \
                                  max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
-                                 max_splits, k_scale, v_scale, nullptr);                                         \
+                                 max_splits, k_scale, v_scale, nullptr, GaiQkvFold{});                           \
     } else {                                                                                                    \
       auto kern = variant == 0   ? attn_decode_kernel<DD, false, 1, false, bf16>                                \
                   : variant == 2 ? attn_decode_kernel<DD, false, 2, true, bf16>                                 \
@@ -767,7 +862,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
                                  : attn_decode_kernel<DD, false, 1, true, bf16>;                                \
       kern<<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, block_tables,      \
                                  max_blocks, ctx_lens, (bf16*)out, ws_o, ws_ml, B, Hq, Hkv, scale, split_keys,   \
-                                 max_splits, k_scale, v_scale, nullptr);                                         \
+                                 max_splits, k_scale, v_scale, nullptr, GaiQkvFold{});                           \
     }                                                                                                           \
     GAI_LAUNCH_CHECK();                                                                                         \
     if (max_splits > 1) {                                                                                       \

@@ -907,6 +907,19 @@ int gai_gemm_splitk_rope_kv(const void* A, const void* B, const void* bias, cons
   return 0;
 }
 
+int gai_gemm_qkv_partials(const void* A, const void* B, int M, int N, int K, float* ws, int psw, hipStream_t st) {
+  if (M < 1 || M > 64 || N % 16) return 0;
+  if (gai_gemm_dec2_ok(M, N, K, EPI_NONE)) return 0;  // single-pass kernel owns it
+  const int ks2 = gai_gemm_dec2_partials_ks(M, N, K);
+  const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
+  if (KS < 2 || KS > 8) return 0;
+  if (ks2)
+    gai_gemm_dec2_partials(A, B, M, N, K, ws, st, psw);
+  else
+    launch_partials(A, B, M, N, K, KS, ws, psw, st);
+  return KS;
+}
+
 void gai_gemm_splitk(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
                      int ldc, int epi, int out_f32, float* ws, int psw, hipStream_t st) {
   if (psw && N % 16) gai_launch_error(__FILE__, __LINE__, "gemm_splitk: pre-shuffled weights need N % 16 == 0");

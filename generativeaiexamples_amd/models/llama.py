@@ -599,7 +599,12 @@ class LlamaModel:
                 x = self._norm(res, p + "attn_norm") if h is None else self._norm(h, p + "attn_norm", residual=res)
             kc, vc = kv.layer(i)
             ks, vs = kv.scales(i)
-            if fuse_qkv:
+            # pure decode: the QKV RoPE / KV-write tail runs inside the decode-attention launch (ops.qkv_fold_partials)
+            fold = (ops.qkv_fold_partials(x, w[p + "qkv"], w.get(p + "qkv_b"), kc, hd, decode_ws, ks, vs)
+                    if fuse_qkv and P == 0 and T <= 64 else None)
+            if fold is not None:
+                fold = (fold[0], fold[1], fb.positions, self.cos_sin, fb.slots)
+            elif fuse_qkv:
                 ops.linear_rope_kv(x, w[p + "qkv"], w.get(p + "qkv_b"), fb.positions, self.cos_sin, fb.slots, q, kc,
                                    vc, self.hq, self.hkv, hd, ks, vs)
             else:
@@ -614,7 +619,7 @@ class LlamaModel:
                                       v_scale=vs)
             if T > P:
                 ops.attention_decode(q[P:], kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
-                                     max_ctx=fb.max_decode_ctx, out=attn[P:], k_scale=ks, v_scale=vs)
+                                     max_ctx=fb.max_decode_ctx, out=attn[P:], k_scale=ks, v_scale=vs, qkv_fold=fold)
             a2 = attn.view(T, -1)
             if fuse:
                 x = ops.linear_add_rmsnorm(a2, w[p + "o"], res, w[p + "mlp_norm"], c.rms_eps, bias=w.get(p + "o_b"))

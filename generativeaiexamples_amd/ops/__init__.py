@@ -495,7 +495,10 @@ _DECODE_ADAPTIVE = os.environ.get("GAI_DECODE_ADAPTIVE", "1") == "1"
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: DecodeWorkspace | None = None,
-                     max_ctx: int | None = None, out=None, k_scale=1.0, v_scale=1.0):
+                     max_ctx: int | None = None, out=None, k_scale=1.0, v_scale=1.0, qkv_fold=None):
+    """qkv_fold = (slabs, ks, positions, cos_sin, slots) from :func:`qkv_fold_partials`: q is computed inside the
+    launch from the QKV split-K partials (sum, bf16, RoPE) and the new key / value are written to the caches there;
+    ``q`` is then only read for its shape."""
     if not q.is_cuda:
         return _into(out, ref.attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, k_scale, v_scale))
     B, Hq, D = q.shape
@@ -504,14 +507,44 @@ def attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, ws: Dec
         ws = DecodeWorkspace(B, Hq, D, mc, q.device)
     split = ws.split_for(B, k_cache.shape[1], mc)
     nsplit = (mc + split - 1) // split
+    if qkv_fold is not None:
+        nsplit = max(nsplit, 2)  # the fold runs in the fused-merge kernel; surplus splits exit at once
     assert nsplit <= ws.max_splits, "decode workspace too small for this context"
     out = torch.empty_like(q) if out is None else out
     # adaptive (split_keys 0): the kernel cuts each sequence's ACTUAL context into nsplit equal parts, so graphs
     # captured for max_ctx balance their splits at every replay (GAI_DECODE_ADAPTIVE=0: fixed split_keys)
+    f = qkv_fold if qkv_fold is not None else (None, 0, None, None, None)
     native().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, scale,
                          0 if (_DECODE_ADAPTIVE and ws.fixed_split is None) else split, nsplit, k_scale, v_scale,
-                         ws.cnt if _ATTN_FUSE else None)
+                         ws.cnt if _ATTN_FUSE else None, f[0], f[1], f[2], f[3], f[4])
     return out
+
+
+# Decode QKV tail folded into the decode-attention launch (attention.hip QP): the QKV projection writes only its split-K
+# partial slabs, and attention_decode sums them, applies RoPE and writes the new key / value itself - one launch per
+# layer fewer than the split-K RoPE / KV-write tail (GAI_QKV_FOLD=0: the tail kernel). Needs the default fused,
+# non-temporal bf16 decode kernel.
+_QKV_FOLD = (os.environ.get("GAI_QKV_FOLD", "1") == "1" and os.environ.get("GAI_DECODE_NT", "1") != "0"
+             and os.environ.get("GAI_DECODE_VARIANT", "1") == "1")
+
+
+def qkv_fold_partials(x: torch.Tensor, w, bias, k_cache, head_dim: int, ws: "DecodeWorkspace | None", k_scale=1.0,
+                      v_scale=1.0):
+    """Decode QKV projection for attention_decode(qkv_fold=...): launches the split-K partial slabs and returns
+    (slabs, ks), or None when the fold does not apply (the caller then runs linear_rope_kv)."""
+    if not (_QKV_FOLD and _ATTN_FUSE and _SPLITK and _GEMM_FORCE == 0 and x.is_cuda and bias is None
+            and head_dim == 128 and k_cache.dtype == torch.bfloat16 and k_scale == 1.0 and v_scale == 1.0
+            and ws is not None and ws.max_splits >= 2 and not isinstance(w, Fp8Weight)):
+        return None
+    K = x.shape[-1]
+    M, N = x.numel() // K, w.shape[0]
+    if not 1 <= M <= 64:
+        return None
+    nat = native()
+    psw = getattr(w, "_gai_psw", None)
+    slabs = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x.device)
+    ks = nat.gemm_qkv_partials(x.reshape(M, K).contiguous(), w if psw is None else psw, slabs, psw is not None)
+    return (slabs, int(ks)) if ks else None
 
 
 # Decode-attention splits are merged inside the attention launch by the last-arriving split (write-through sc1
