@@ -15,6 +15,8 @@
 //    one head for RoPE + q / paged K / V^T stores - no split-K, no slabs, no tail launch.
 // A Llama decode layer at batch <= 4 is then five launches: QKV(+norm, +RoPE/KV) -> attention -> O(+residual)
 // -> gate_up(+norm, +SwiGLU) -> down(+residual).
+#include <cstdlib>
+
 #include "gai_common.h"
 #include "gai_kernels.h"
 
@@ -22,7 +24,7 @@ using namespace gai;
 
 namespace {
 
-constexpr int kGvWaves = 8;
+constexpr int kGvWaves = 8;  // waves per workgroup (default); 6 where 8 leaves the grid unbalanced (gemv_waves)
 constexpr int kGvThreads = 64 * kGvWaves;
 constexpr int kPiece = 512;  // K elements of one wave load (64 lanes x 8 bf16)
 constexpr int kG = 4;        // pieces per row per pipeline group
@@ -56,18 +58,49 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
   return acc;
 }
 
-template <int MR, int EPI>
-__global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
+template <int MR, int EPI, int NW = kGvWaves>
+__global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
+  constexpr int kThr = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
-  __shared__ float red[kGvWaves][MR];
+  __shared__ float red[NW][MR];
   __shared__ float inv_s[MR];
   bf16* xs = reinterpret_cast<bf16*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int K = a.K, nch = K / 8;
 
+  // ---- this wave's row pair; its first weight group is issued BEFORE the activation staging, so the HBM
+  // latency of the weight stream overlaps the staging (and the RMSNorm reduction) instead of following it
+  const int p = blockIdx.x * NW + wid;
+  const int npairs = a.N / 2;
+  const bool live = p < npairs;
+  int r0, r1;
+  if (EPI == GV_SWIGLU) {  // rows interleaved per 16: [gate16 | up16]; output column p
+    r0 = 32 * (p >> 4) + (p & 15);
+    r1 = r0 + 16;
+  } else if (EPI == GV_ROPE) {  // head p / 64, rotate-half pair (i, i + 64)
+    r0 = 128 * (p >> 6) + (p & 63);
+    r1 = r0 + 64;
+  } else {
+    r0 = 2 * p;
+    r1 = r0 + 1;
+  }
+  const bf16* w0 = a.W + (size_t)(live ? r0 : 0) * K + 8 * lane;
+  const bf16* w1 = a.W + (size_t)(live ? r1 : 0) * K + 8 * lane;
+  const int ngroups = K / (kPiece * kG);  // host: K % 2048 == 0
+  bf16x8 cur0[kG], cur1[kG], nxt0[kG], nxt1[kG];
+  auto load_group = [&](int g, bf16x8(&b0)[kG], bf16x8(&b1)[kG]) {
+#pragma unroll
+    for (int c = 0; c < kG; ++c) {
+      const int off = (g * kG + c) * kPiece;
+      b0[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + off));
+      b1[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + off));
+    }
+  };
+  if (live) load_group(0, cur0, cur1);
+
   // ---- stage the activation rows (normalised when gamma is given); the host keeps K <= 8192 for the norm form
   if (a.gamma != nullptr) {
-    constexpr int kMaxC = 2;  // chunks per thread per row: K <= 2 * 8 * 512
+    constexpr int kMaxC = (8192 + 8 * kThr - 1) / (8 * kThr);  // chunks per thread per row: K <= 8192
     bf16x8 v[MR][kMaxC];
     float ss[MR];
 #pragma unroll
@@ -75,7 +108,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       ss[m] = 0.f;
 #pragma unroll
       for (int c = 0; c < kMaxC; ++c) {
-        const int ch = c * kGvThreads + tid;
+        const int ch = c * kThr + tid;
         if (ch < nch) {
           v[m][c] = load8(a.x + (size_t)m * K + 8 * ch);
 #pragma unroll
@@ -89,7 +122,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
     if (tid < MR) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < kGvWaves; ++w) t += red[w][tid];
+      for (int w = 0; w < NW; ++w) t += red[w][tid];
       inv_s[tid] = rsqrtf(t / K + a.eps);
     }
     __syncthreads();
@@ -98,7 +131,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       const float inv = inv_s[m];
 #pragma unroll
       for (int c = 0; c < kMaxC; ++c) {
-        const int ch = c * kGvThreads + tid;
+        const int ch = c * kThr + tid;
         if (ch < nch) {
           const bf16x8 g = load8(a.gamma + 8 * ch);
           bf16x8 o;
@@ -109,44 +142,17 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       }
     }
   } else {
-    for (int ch = tid; ch < MR * nch; ch += kGvThreads) {
+    for (int ch = tid; ch < MR * nch; ch += kThr) {
       const int m = ch / nch, c = ch % nch;
       *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * c) = load8(a.x + (size_t)m * K + 8 * c);
     }
   }
   __syncthreads();
-
-  // ---- this wave's row pair
-  const int p = blockIdx.x * kGvWaves + wid;
-  const int npairs = a.N / 2;
-  if (p >= npairs) return;  // no barrier below
-  int r0, r1;
-  if (EPI == GV_SWIGLU) {  // rows interleaved per 16: [gate16 | up16]; output column p
-    r0 = 32 * (p >> 4) + (p & 15);
-    r1 = r0 + 16;
-  } else if (EPI == GV_ROPE) {  // head p / 64, rotate-half pair (i, i + 64)
-    r0 = 128 * (p >> 6) + (p & 63);
-    r1 = r0 + 64;
-  } else {
-    r0 = 2 * p;
-    r1 = r0 + 1;
-  }
-  const bf16* w0 = a.W + (size_t)r0 * K + 8 * lane;
-  const bf16* w1 = a.W + (size_t)r1 * K + 8 * lane;
-  const int ngroups = K / (kPiece * kG);  // host: K % 2048 == 0
+  if (!live) return;  // no barrier below
 
   float acc[MR][2];
 #pragma unroll
   for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = 0.f;
-  bf16x8 cur0[kG], cur1[kG], nxt0[kG], nxt1[kG];
-  auto load_group = [&](int g, bf16x8(&b0)[kG], bf16x8(&b1)[kG]) {
-#pragma unroll
-    for (int c = 0; c < kG; ++c) {
-      const int off = (g * kG + c) * kPiece;
-      b0[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + off));
-      b1[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + off));
-    }
-  };
   auto compute_group = [&](int g, const bf16x8(&b0)[kG], const bf16x8(&b1)[kG]) {
 #pragma unroll
     for (int c = 0; c < kG; ++c) {
@@ -159,8 +165,7 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
       }
     }
   };
-  load_group(0, cur0, cur1);
-  int g = 0;
+  int g = 0;  // group 0 is in flight since the kernel start
   for (; g + 2 <= ngroups; g += 2) {
     load_group(g + 1, nxt0, nxt1);
     compute_group(g, cur0, cur1);
@@ -231,19 +236,27 @@ __global__ __launch_bounds__(kGvThreads) void gemv_kernel(GemvArgs a) {
   }
 }
 
-template <int EPI>
-void gemv_launch(const GemvArgs& a, hipStream_t st) {
+// Waves per workgroup: 8. GAI_GEMV_WAVES=6 (sweeps): 6-wave workgroups, which balance the Llama-3-8B QKV grid
+// (N 6144: 512 workgroups = 2 per CU instead of 384 = 1.5) but stage the normalised activations in 1/3 more
+// workgroups - measured slower (13.2 vs 11.4 us, profiles/r5/gemv_b1), so not the default.
+int gemv_waves(int) {
+  static const int force = getenv("GAI_GEMV_WAVES") ? atoi(getenv("GAI_GEMV_WAVES")) : 0;
+  return force == 6 ? 6 : 8;
+}
+
+template <int EPI, int NW>
+void gemv_launch_nw(const GemvArgs& a, hipStream_t st) {
   const size_t lds = (size_t)a.M * a.K * sizeof(bf16);
-  const int grid = (a.N / 2 + kGvWaves - 1) / kGvWaves;
+  const int grid = (a.N / 2 + NW - 1) / NW;
 #define GAI_GV(MRV)                                                                                           \
   if (a.M == MRV) {                                                                                           \
     static bool once = false;                                                                                 \
     if (!once) {                                                                                              \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_kernel<MRV, EPI>),                              \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_kernel<MRV, EPI, NW>),                          \
                           hipFuncAttributeMaxDynamicSharedMemorySize, kGvMaxDyn);                             \
       once = true;                                                                                            \
     }                                                                                                         \
-    gemv_kernel<MRV, EPI><<<grid, kGvThreads, lds, st>>>(a);                                                  \
+    gemv_kernel<MRV, EPI, NW><<<grid, 64 * NW, lds, st>>>(a);                                                 \
     GAI_LAUNCH_CHECK();                                                                                       \
     return;                                                                                                   \
   }
@@ -253,6 +266,12 @@ void gemv_launch(const GemvArgs& a, hipStream_t st) {
   GAI_GV(4)
 #undef GAI_GV
   gai_launch_error(__FILE__, __LINE__, "gemv: 1 <= M <= 4");
+}
+
+template <int EPI>
+void gemv_launch(const GemvArgs& a, hipStream_t st) {
+  if (gemv_waves(a.N) == 6) return gemv_launch_nw<EPI, 6>(a, st);
+  gemv_launch_nw<EPI, 8>(a, st);
 }
 
 }  // namespace
