@@ -395,6 +395,14 @@ def main():
         log(f"step {s}: {dt:.3f}s  p50 TTFT {statistics.median(ttft):.3f}s  retrieval {rt * 1000:.1f} ms")
 
     stats1, phase1 = dict(engine.stats), dict(engine.phase_ms)  # the timed steps only (before the probes)
+    if engine.host_timeline:  # GAI_HOST_TIMELINE=1: host gaps of the pipelined decode, last timed step
+        tl = engine.host_timeline
+        ch = sorted(e - s for n, s, e in tl if n == "chain")
+        co = sorted(e - s for n, s, e in tl if n == "complete")
+        gaps = sorted(tl[i + 1][1] - tl[i][2] for i in range(len(tl) - 1))
+        log(f"host timeline: {len(ch)} chained launches median {1e3 * ch[len(ch) // 2]:.2f} ms max "
+            f"{1e3 * ch[-1]:.2f}; complete median {1e3 * co[len(co) // 2]:.2f} ms; between calls median "
+            f"{1e3 * gaps[len(gaps) // 2]:.3f} ms max {1e3 * gaps[-1]:.3f}; nochain {sum(n == 'nochain' for n, _, _ in tl)}")
     # ---------------- untimed TTFT probes on the rank-local shard (no collectives: ranks run them freely)
     probes = {}
     if not args.no_probes:

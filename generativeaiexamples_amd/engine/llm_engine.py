@@ -199,6 +199,9 @@ class LLMEngine:
         self._pipeline = os.environ.get("GAI_PIPELINE", "1") == "1"  # chained multi-step runs (A/B switch)
         self._masks = None  # guided-decoding mask builder (lazy)
         self._timing = os.environ.get("GAI_STEP_TIMING") == "1"
+        # GAI_HOST_TIMELINE=1: (event, t_start, t_end) host timestamps of the pipelined decode (chain / complete /
+        # non-chained launches), no synchronisation added - for finding host gaps between graph runs
+        self.host_timeline: Optional[list] = [] if os.environ.get("GAI_HOST_TIMELINE") == "1" else None
         self.phase_ms: Dict[str, float] = {}
         self._t_mark = 0.0
         self.requests: Dict[int, Request] = {}
@@ -887,6 +890,14 @@ class LLMEngine:
             p = self._pending
             if isinstance(p, _Run):
                 # pipelined decode: enqueue run r+1, then process run r while r+1 executes
+                if self.host_timeline is not None:
+                    t0 = time.perf_counter()
+                    self._pending = self._chain(p)
+                    t1 = time.perf_counter()
+                    outs = self._complete(p)
+                    self.host_timeline += [("chain" if self._pending is not None else "nochain", t0, t1),
+                                           ("complete", t1, time.perf_counter())]
+                    return outs
                 self._pending = self._chain(p)
                 return self._complete(p)
             if isinstance(p, _Single):

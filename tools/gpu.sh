@@ -9,6 +9,7 @@
 #   testsl <name> <pytest args...>  the same with an 1100 s step limit (the whole suite)
 #   bench <name> <bench.py args...> bench.py ... --json-out <name>.json
 #   prof  <name> <bench.py args...> rocprofv3 --kernel-trace --stats around bench.py, reduced to <name>_kernels.csv
+#   proftrace <name> <bench.py args...> the same, plus the raw kernel trace as <name>_trace.csv.gz
 #   py    <name> <script args...>   python <script> <args>
 #   pyprof <name> <script args...>  rocprofv3 --kernel-trace --stats around python3 <script> <args>
 #   smoke                           __graft_entry__.smoke()
@@ -57,6 +58,12 @@ for spec in "$@"; do
              > /dev/null || exit $?
            python tools/trace_gaps.py "/tmp/prof_$n/**/*kernel_trace.csv" --from-frac 0.6 --top 40 \
              -o "$O/${n}_gaps.json" > /dev/null || exit $? ;;
+    proftrace) rm -rf "/tmp/prof_$n"  # prof + the raw kernel trace (gzipped) for gap analysis
+           step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
+             python3 "$PWD/bench.py" "${rest[@]}" --json-out "$O/$n.json" || exit $?
+           python tools/rocprof_summary.py "/tmp/prof_$n/**/*kernel_stats.csv" -o "$O/${n}_kernels.csv" --top 60 \
+             > /dev/null || exit $?
+           f=$(find "/tmp/prof_$n" -name "*kernel_trace.csv" | head -1); gzip -c "$f" > "$O/${n}_trace.csv.gz" || exit $? ;;
     py)    step 600 "$O/$n.log" python "${rest[@]}" || exit $? ;;
     pyprof) rm -rf "/tmp/prof_$n"
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
