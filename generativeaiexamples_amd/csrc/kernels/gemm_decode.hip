@@ -364,14 +364,18 @@ bool dec2_run(const void* A, const void* W, void* C, const void* bias, const voi
 
 }  // namespace
 
-// Wide projections only (gate_up, LM head, TP-shard O / down: N >= 8192 by default): there the activation re-staging is
+// Wide projections only (gate_up, LM head: N >= 16384 by default; TP-shard O / down: N >= 8192 at K <= 4096): there the activation re-staging is
 // <= 1/2 of the weight bytes and this kernel beats the split-K kernels (gate_up+SwiGLU 54.9 vs 80.9 us,
 // LM head 233 vs 327 us at M = 64). On the narrow ones (QKV, O, down) every column tile needs the whole
 // activation K range, 2-4x the weight bytes, and the split-K kernels stay ahead.
 int gai_gemm_dec2_ok(int M, int N, int K, int epi) {
-  // N >= 8192 since round 5 (TP shards: O and down of Llama-3-70B at TP = 8, N 8192, run faster here than split-K)
-  static const int min_n = getenv("GAI_DEC2_MINN") ? atoi(getenv("GAI_DEC2_MINN")) : 8192;
-  if (M < 1 || M > 64 || N % 16 || N < min_n || (epi == EPI_SWIGLU && N % 32)) return 0;
+  // Also 8192 <= N < 16384 at shallow K (<= 4096) since round 5: the O and down projections of a Llama-3-70B TP = 8
+  // shard (K 1024 / 3584) run faster here than split-K (profiles/r5/tp8_rank). At deep K the full-K tile leaves half
+  // the CUs idle on a long stream: Llama-3-70B on one GPU (QKV / O, K 8192) config 3 1.57 -> 1.49 q/s when they ran
+  // here (profiles/r5/config3_dec2_ab) - those keep the split-K kernels.
+  static const int min_n = getenv("GAI_DEC2_MINN") ? atoi(getenv("GAI_DEC2_MINN")) : 16384;
+  const bool shallow_shard = N >= 8192 && K <= 4096 && !getenv("GAI_DEC2_MINN");
+  if (M < 1 || M > 64 || N % 16 || (N < min_n && !shallow_shard) || (epi == EPI_SWIGLU && N % 32)) return 0;
   static const bool off = getenv("GAI_DEC2") && atoi(getenv("GAI_DEC2")) == 0;
   if (off) return 0;
   const bool sw = epi == EPI_SWIGLU;
