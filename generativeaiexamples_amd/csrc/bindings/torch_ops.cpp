@@ -845,7 +845,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_rows_fp8", &quant_rows_fp8);
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv) { return gai_attn_prefill_rows_per_tile(hq, hkv); });
-  m.def("attn_decode", &attn_decode);
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("scale"), py::arg("split_keys"),
+        py::arg("max_splits"), py::arg("k_scale"), py::arg("v_scale"), py::arg("split_cnt") = py::none(),
+        py::arg("qkv_part") = py::none(), py::arg("part_ks") = 0, py::arg("positions") = py::none(),
+        py::arg("cos_sin") = py::none(), py::arg("slots") = py::none());
   m.def("sample", &sample, py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"),
         py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("ws") = py::none());
   m.def("sample_ws_bytes", &sample_ws_bytes);

@@ -547,14 +547,23 @@ constexpr int kDblHalf = 256 * 64 * 2;
 // VAR (microbench ablations only; 0 in the framework): bit 0 = the 16 loads issued in a burst over the
 // odd phase's first 32 MFMAs (measured 3-9 % slower than 1 per 4 MFMAs: an LDS-DMA issue stalls the
 // wave), bit 1 = no vmcnt wait at even phase ends (timing only)
-template <int EPI, bool OUTF32, int VAR = 0>
+//
+// MI = 16-row A fragments per wave: 8 = the 256x256 tile; 6 = a 192x256 tile (each wave 96x128, 192 AGPRs,
+// 48 MFMAs and 6 + 8 loads / fragment reads per phase). The launcher takes the tile height whose grid of tiles
+// quantises best onto the CUs: a 2406-token prefill has 160 O / down tiles of 256 rows (one 62 %-full wave) but
+// 208 of 192 rows (81 %, each 3/4 of the work).
+template <int EPI, bool OUTF32, int VAR = 0, int MI = 8>
 __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
                                                           int K, int ldc, RopeKvArgs rk) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 slots x [A 32K | B 32K]
+  static_assert(MI == 8 || MI == 6, "tile heights 256 / 192");
+  constexpr int BM = 32 * MI;       // tile rows
+  constexpr int NT = 8 * MI;        // MFMAs per phase
+  constexpr int NL = MI + 8;        // loads (odd phase) and fragment reads per phase
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 slots x [A 32K | B 32K] (A: BM rows used)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_m = (M + LBM - 1) / LBM, tiles_n = (N + LBN - 1) / LBN;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + LBN - 1) / LBN;
   const int tiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int n_my = (tiles - (int)blockIdx.x + G - 1) / G;
@@ -565,27 +574,33 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
     const int first_m = group * GM;
     const int gsz = min(tiles_m - first_m, GM);
     const int pin = wg % (GM * tiles_n);
-    m0 = (first_m + pin % gsz) * LBM;
+    m0 = (first_m + pin % gsz) * BM;
     n0 = (pin / gsz) * LBN;
   };
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
-  // load j (0..7) of wave w, per operand: rows (8w + j) * 8 + lane / 8, 16-B chunk (lane & 7) of the LDS
-  // row <- global chunk (lane & 7) ^ f(row); byte offsets (rows clamped to the matrix: partial tiles)
+  // load j of wave w: A rows (MI w + j) * 8 + lane / 8 (j < MI), B rows (8w + j) * 8 + lane / 8 (j < 8), 16-B
+  // chunk (lane & 7) of the LDS row <- global chunk (lane & 7) ^ f(row); byte offsets (rows clamped to the
+  // matrix: partial tiles)
   auto offsets = [&](int m0, int n0, int* oa, int* ob) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = (wid * 8 + j) * 8 + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
-      oa[j] = min(m0 + row, M - 1) * K * 2 + gc * 16;
       ob[j] = min(n0 + row, N - 1) * K * 2 + gc * 16;
+    }
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+      const int row = (wid * MI + j) * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ ((row >> 1) & 7);
+      oa[j] = min(m0 + row, M - 1) * K * 2 + gc * 16;
     }
   };
   const int wm = wid >> 1, wn = wid & 1;
-  // fragment reads: row wm*128 + 16i + (lane & 15) (f depends on lane & 15 only), chunk 4h + lane / 16
+  // fragment reads: row wm*BM/2 + 16i + (lane & 15) (f depends on lane & 15 only), chunk 4h + lane / 16
   const int fr = (lane & 15) >> 1;
-  const int a_rd0 = (wm * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
-  const int a_rd1 = (wm * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  const int a_rd0 = (wm * 16 * MI + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int a_rd1 = (wm * 16 * MI + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
   const int b_rd0 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
   const int b_rd1 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
   auto barrier = [&]() {
@@ -593,17 +608,18 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // one k32 phase: 64 MFMAs on (af, bfr); the 16 ds_reads of the next unit (half 1 of slot `rslot` in
-  // an even phase, half 0 in an odd one) interleaved in the first 32 MFMAs and, in an odd phase, the 16
-  // loads of k-double `kd` from (oa, ob) into slot `wslot` spread over all 64
+  // one k32 phase: NT MFMAs on (af, bfr); the NL ds_reads of the next unit (half 1 of slot `rslot` in
+  // an even phase, half 0 in an odd one) interleaved in the first 2 NL MFMAs and, in an odd phase, the NL
+  // loads of k-double `kd` from (oa, ob) into slot `wslot` spread over all NT
   auto phase = [&](auto odd_c, const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int rslot,
                    int wslot, const int* oa, const int* ob, int kd) {
     constexpr bool ODD = decltype(odd_c)::value;
     const char* sr = smem + rslot * kDblBytes;
-    char* d = smem + wslot * kDblBytes + wid * 8192;
+    char* da = smem + wslot * kDblBytes + wid * MI * 1024;
+    char* db = smem + wslot * kDblBytes + kDblHalf + wid * 8192;
     const int ar = ODD ? a_rd0 : a_rd1, br = ODD ? b_rd0 : b_rd1;
     const int soff = kd * 128;
-    for_each_const<64>([&](auto tc) {
+    for_each_const<NT>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       constexpr int i = t >> 3, j = t & 7;
       asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
@@ -611,16 +627,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
                    : "i"(4 * t), "i"(4 * t + 3), "v"(bfr[j]), "v"(af[i])
                    : GAI_AGPR_CLOBBERS);
       constexpr int g = t >> 1;
-      constexpr bool LD = (VAR & 1) ? (t % 2 == 1 && t < 32) : (t % 4 == 1);  // load issue slots
-      constexpr int gl = (VAR & 1) ? g : (t >> 2);                               // load number 0..15
-      if constexpr (ODD && LD && gl < 8)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(d + gl * 1024), 16, oa[gl], soff, 0, 0);
+      // load issue slots: 1 per 4 MFMAs at MI = 8 (the tuned schedule); NL spread evenly over NT otherwise
+      constexpr bool LD = (VAR & 1) ? (t % 2 == 1 && t < 32)
+                                    : (MI == 8 ? (t % 4 == 1) : ((t + 1) * NL / NT > t * NL / NT));
+      constexpr int gl = (VAR & 1) ? g : (MI == 8 ? (t >> 2) : (t * NL / NT));  // load number 0..NL-1
+      // (a load slot and a fragment-read slot may coincide at MI = 6: both issue)
+      if constexpr (ODD && LD && gl < MI)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(da + gl * 1024), 16, oa[gl], soff, 0, 0);
       else if constexpr (ODD && LD)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(d + kDblHalf + (gl - 8) * 1024), 16, ob[gl - 8], soff, 0, 0);
-      else if constexpr (t % 2 == 0 && t < 32 && g < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(db + (gl - MI) * 1024), 16, ob[gl - MI], soff, 0, 0);
+      if constexpr (t % 2 == 0 && g < NL && g < MI)
         naf[g] = *reinterpret_cast<const bf16x8*>(sr + ar + g * 2048);
-      else if constexpr (t % 2 == 0 && t < 32)
-        nbf[g - 8] = *reinterpret_cast<const bf16x8*>(sr + br + (g - 8) * 2048);
+      else if constexpr (t % 2 == 0 && g < NL)
+        nbf[g - MI] = *reinterpret_cast<const bf16x8*>(sr + br + (g - MI) * 2048);
       __builtin_amdgcn_sched_barrier(0);
     });
     __builtin_amdgcn_sched_barrier(0);
@@ -636,23 +655,27 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
   const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2
   int m0, n0;
   coords(0, m0, n0);
-  int ca[8], cb[8], xa[8], xb[8];
+  int ca[8], cb[8], xa[8], xb[8];  // A uses MI entries (an MI-sized local array here drops the host launch stub)
   offsets(m0, n0, ca, cb);
   asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
 #pragma unroll
   for (int dd = 0; dd < 2; ++dd) {
-    char* dst = smem + dd * kDblBytes + wid * 8192;
+    char* dst = smem + dd * kDblBytes;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(dst + j * 1024), 16, ca[j], dd * 128, 0, 0);
+    for (int j = 0; j < MI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(dst + (wid * MI + j) * 1024), 16, ca[j], dd * 128, 0, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(dst + kDblHalf + j * 1024), 16, cb[j], dd * 128, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(dst + kDblHalf + (wid * 8 + j) * 1024), 16, cb[j], dd * 128, 0, 0);
   }
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
+  if constexpr (MI == 8)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
+  else
+    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   barrier();
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  bf16x8 a0[MI], b0[8], a1[MI], b1[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + a_rd0 + i * 2048);
+  for (int i = 0; i < MI; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(smem + a_rd0 + i * 2048);
 #pragma unroll
   for (int j = 0; j < 8; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(smem + b_rd0 + j * 2048);
   __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -677,14 +700,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
     }
     // (a0, b0) hold the next tile's unit-0 fragments; this tile's accumulators are complete
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
-    for_each_const<8>([&](auto ic) {
+    for_each_const<MI>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       f32x4 row[8];
       read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
       if constexpr (EPI == EPI_ROPE_KV) {
         // the wave's 128 columns are one head h of [Hq | Hkv | Hkv]; lane (m, q) holds dims 16j + 4q + r
         // (tile j) and, in tile j + 4, their rotate-half partners 64 further on
-        const int m = m0 + wm * 128 + 16 * i + (lane & 15), nb = n0 + wn * 128, q = lane >> 4;
+        const int m = m0 + wm * 16 * MI + 16 * i + (lane & 15), nb = n0 + wn * 128, q = lane >> 4;
         if (m < M && nb < N) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
@@ -700,7 +723,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
           }
         }
       } else {
-        epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 128 + 16 * i, n0 + wn * 128, lane);
+        epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 16 * MI + 16 * i, n0 + wn * 128, lane);
       }
     });
     asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
@@ -1134,10 +1157,23 @@ void launch_w4p(const void* A, const void* B, void* C, const void* bias, const v
   GAI_LAUNCH_CHECK();
 }
 
+// Tile height of the w4d walk: 192 rows when its tiles quantise onto the CUs' waves enough better to pay for the
+// smaller tile's lower rate (15 % per FLOP: M = 16384 QKV / O / gate_up 645 / 406 / 3096 us vs 559 / 358 / 2634 on
+// 256-row tiles): cost = waves x rows. M = 2406, N = 4096 (O / down): 10 x 16 = 160 tiles of 256 rows (1 wave x 256)
+// vs 13 x 16 = 208 of 192 (1 x 192): O 77.9 -> 66.7 us, down 255.1 -> 225.8 us (profiles/r5/gemm/w4d192.jsonl).
+// QKV (N 6144: 240 tiles vs 312 = 2 waves) and gate_up (1120 vs 1456 tiles: 5 x 256 vs 6 x 192) keep 256 rows;
+// M = 16384 keeps 256. GAI_GEMM_BM = 192 / 256 forces one.
+int w4d_rows(int M, int N, int ncu) {
+  static const int env = getenv("GAI_GEMM_BM") ? atoi(getenv("GAI_GEMM_BM")) : 0;
+  if (env == 192 || env == 256) return env;
+  const int G = ncu & ~7, tn = (N + LBN - 1) / LBN;
+  auto cost = [&](int bm) { return (double)((((M + bm - 1) / bm) * tn + G - 1) / G) * bm; };
+  return cost(192) * 1.15 < cost(256) ? 192 : 256;
+}
+
 template <int EPI, bool OUTF32>
 void launch_w4d(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st, RopeKvArgs rk = {}) {
-  const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
+                hipStream_t st, RopeKvArgs rk = {}, int rows = 0) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1145,10 +1181,18 @@ void launch_w4d(const void* A, const void* B, void* C, const void* bias, const v
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
       gai_launch_error(__FILE__, __LINE__, "gemm_w4d: cannot query the CU count");
     set_max_lds(gemm_w4d_kernel<EPI, OUTF32>);
+    set_max_lds(gemm_w4d_kernel<EPI, OUTF32, 0, 6>);
   }
+  const int bm = rows ? rows : w4d_rows(M, N, ncu);
+  const int tiles = ((M + bm - 1) / bm) * ((N + LBN - 1) / LBN);
   const int grid = tiles <= ncu ? tiles : (ncu & ~7);
-  gemm_w4d_kernel<EPI, OUTF32><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                 (const bf16*)bias, (const bf16*)R, M, N, K, ldc, rk);
+  if (bm == 192)
+    gemm_w4d_kernel<EPI, OUTF32, 0, 6><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                        (const bf16*)bias, (const bf16*)R, M, N, K,
+                                                                        ldc, rk);
+  else
+    gemm_w4d_kernel<EPI, OUTF32><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
+                                                                   (const bf16*)bias, (const bf16*)R, M, N, K, ldc, rk);
   GAI_LAUNCH_CHECK();
 }
 
@@ -1326,12 +1370,16 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
       return;
     if (force == 12 && launch_w4x<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, std::max(2, split_parts(M, N, K))))
       return;
-    // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up): the
-    // part ring's longer A-operand latency cover wins (+7 % / +1-5 %); otherwise the double-slot kernel
-    // (+2-4 % on O / e5), profiles/r2/gemm_w4r.jsonl, gemm_rule.jsonl, gemm_w4p_ab.jsonl
-    if (force == 10 || (force == 0 && (K >= 8192 || N >= 16384)))
+    // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up) at large M:
+    // the part ring's longer A-operand latency cover wins (+7 % / +1-5 %, M = 16384); otherwise the double-slot
+    // kernel (+2-4 % on O / e5), profiles/r2/gemm_w4r.jsonl, gemm_rule.jsonl, gemm_w4p_ab.jsonl. Below M = 8192 the
+    // double-slot walk is the faster one there too (M = 2406 down 237.7 vs 252.3 us, gate_up 437.2 vs 444.4,
+    // M = 1024 gate_up 186.6 vs 189.9: profiles/r5/gemm/native_vs_hipblaslt_midM.jsonl).
+    if (force == 10 || (force == 0 && M >= 8192 && (K >= 8192 || N >= 16384)))
       return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    // force 9 / 13: the double-slot walk with 256- / 192-row tiles (tests, A/B); auto: w4d_rows
+    return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, RopeKvArgs{},
+                                   force == 9 ? 256 : force == 13 ? 192 : 0);
   }
   launch_tiled<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
 }

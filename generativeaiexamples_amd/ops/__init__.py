@@ -56,7 +56,7 @@ def native_available() -> bool:
 
 
 EPI = {None: 0, "bias": 1, "gelu": 2, "residual": 3, "swiglu": 4, "bias_residual": 5, "relu": 6, "quick_gelu": 7}
-_GEMM_KERNELS = {"auto": 0, "skinny": 1, "tiled": 2, "w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12,
+_GEMM_KERNELS = {"auto": 0, "skinny": 1, "tiled": 2, "w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12, "w4d192": 13,
                  # names of round-3 kernels that the persistent 256x256 kernels replaced
                  "large": 9, "ring": 10}
 

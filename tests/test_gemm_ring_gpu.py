@@ -14,10 +14,12 @@ pytestmark = pytest.mark.gpu
 # force codes in gai_gemm: persistent 4-wave ring (tile walk per CU), persistent full-line double-unit kernel, and
 # its 5-part LDS ring variant (the default for M >= 1024), and that ring on the stream-K walk (K % 128 == 0; forced
 # onto shapes with K % 128 != 0 it takes the tile walk)
-KERNELS = {"w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12}  # w4x: the split walk (k-parts per tile)
+KERNELS = {"w4p": 8, "w4d": 9, "w4r": 10, "w4s": 11, "w4x": 12,  # w4x: the split walk (k-parts per tile)
+           "w4d192": 13}  # the double-slot walk on 192-row tiles (6 A fragments per wave)
 
 SHAPES = [(1024, 256, 192), (1280, 1040, 256), (2048, 2304, 1024), (1100, 4096, 4096), (4096, 6144, 320),
-          (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256)]  # last two: > 256 tiles, multi-tile walks
+          (1536, 512, 14336), (4608, 4096, 192), (8192, 8448, 256),  # last two: > 256 tiles, multi-tile walks
+          (2406, 4096, 1024)]  # the 2406-token O / down row count: 192-row tiles by the auto policy
 
 
 def _run(x, w, bias, res, act, out_dtype=torch.bfloat16, force=4):
@@ -122,8 +124,9 @@ def test_stream_k_split_tiles(cuda, M, N, K, act, walk):
         assert torch.equal(_run(x, w, None, res, act, out_dtype, force=KERNELS[walk]), y)
 
 
-@pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(1024, 512, 4, 2, False), (1300, 4096, 32, 8, False),
-                                                  (2048, 256, 8, 2, True)])
+# 192-row tiles (8192 x 1024: 172 tiles vs 128 of 256 rows; 1300 x 6144) and 256-row tiles (2406 x 6144, with bias)
+@pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(8192, 512, 4, 2, False), (1300, 4096, 32, 8, False),
+                                                  (2406, 1024, 32, 8, True)])
 def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
     """Prefill QKV GEMM with RoPE + paged K / V^T write in its epilogue == gemm + rope_kv_write (same
     accumulators, same bf16 roundings); skipped slots (-1) leave the caches untouched."""
@@ -159,3 +162,28 @@ def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
         assert (a != b).sum().item() <= max(2, a.numel() // 10000)
     assert not torch.isnan(outs[0][0]).any()
     assert outs[0][1].float().abs().sum() > 0 and outs[0][2].float().abs().sum() > 0  # caches written
+
+
+def test_prefill_qkv_rope_kv_narrow_declines(cuda):
+    """A QKV projection whose 256x256 tiles fill less than half the CUs (1024 x 1024: 16 tiles) is not fused: the
+    call returns False and ops.linear_rope_kv takes the plain GEMM + rope_kv path, with the same results."""
+    torch.manual_seed(2)
+    M, K, Hq, Hkv, D = 1024, 512, 4, 2, 128
+    N, nblk = (Hq + 2 * Hkv) * D, 1024 // 16 + 4
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    pos = torch.arange(M, device=cuda, dtype=torch.int32)
+    slots = torch.arange(M, device=cuda, dtype=torch.int32)
+    cs = ops.rope_cos_sin(4096, D, 500000.0, device=cuda)
+    q = torch.empty(M, Hq, D, device=cuda, dtype=torch.bfloat16)
+    kc = torch.zeros(nblk, Hkv, 16, D, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros(nblk, Hkv, D, 16, device=cuda, dtype=torch.bfloat16)
+    assert not ops.native().gemm_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D, 1.0, 1.0,
+                                         torch.empty(0, device=cuda), False, None)
+    ops.linear_rope_kv(x, w, None, pos, cs, slots, q, kc, vc, Hq, Hkv, D)
+    qkv = ref.linear(x.cpu(), w.cpu())
+    q2, k2, v2 = torch.empty(M, Hq, D), kc.cpu().float().zero_(), vc.cpu().float().zero_()
+    ref.rope_kv_write(qkv, pos.cpu(), cs.cpu(), slots.cpu(), q2, k2, v2, Hq, Hkv, D)
+    assert (q.float().cpu() - q2).abs().max().item() < 5e-2
+    assert (kc.float().cpu() - k2).abs().max().item() < 5e-2
+    assert (vc.float().cpu() - v2).abs().max().item() < 5e-2

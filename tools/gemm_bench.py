@@ -53,6 +53,7 @@ def main():
                 "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
                 "w4s": lambda: nat.gemm(x, w, out, None, None, 0, 11),
                 "w4x": lambda: nat.gemm(x, w, out, None, None, 0, 12),
+                "w4d192": lambda: nat.gemm(x, w, out, None, None, 0, 13),
                 "tiled": lambda: nat.gemm(x, w, out, None, None, 0, 2),
                 "hipblaslt": lambda: torch.mm(x, w.t())}
         ts = {k: [] for k in arms}
@@ -70,6 +71,8 @@ def main():
         r["w4r_vs_blas"] = round(r["hipblaslt_ms"] / r["w4r_ms"], 3)
         r["w4s_vs_blas"] = round(r["hipblaslt_ms"] / r["w4s_ms"], 3)
         r["w4x_vs_blas"] = round(r["hipblaslt_ms"] / r["w4x_ms"], 3)
+        r["w4d192_vs_blas"] = round(r["hipblaslt_ms"] / r["w4d192_ms"], 3)
+        r["auto_vs_blas"] = round(r["hipblaslt_ms"] / r["auto_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
     if enable_tuned_blas():
