@@ -89,7 +89,8 @@ def dispatch_padded(x: torch.Tensor, ids: torch.Tensor, num_experts: int, capaci
     C = T * k if capacity is None else capacity
     offs, pos, a_pairs = ops.ep_dispatch_plan(ids, world, e_local)
     send_n = recv_n = None
-    if xchg is not None:  # one exchange: the expert id rides in each slab row's 16-B tail
+    if xchg is not None and x.is_cuda and x.dtype == torch.bfloat16:  # one exchange: the expert id rides in each
+        # slab row's 16-B tail (two bf16 lanes)
         D = x.shape[1]
         slab, _ = ops.ep_pack(x, ids, offs, a_pairs, world, C, e_local, ids_in_rows=True)
         if exact_counts and xchg.eligible_a2a(slab):

@@ -191,6 +191,9 @@ def test_ep_exchange_error_word_raises_and_retires(tmp_path):
             rank = 0
             check = CustomAllReduce.check
 
+            def eligible_a2a(self, t):  # no peer buffers: the exchange itself takes the gloo path
+                return False
+
         m.ep_xchg = FakeXchg()
         eng = LLMEngine(m, small_byte_tokenizer(512), EngineConfig(num_blocks=32, max_model_len=64, use_graphs=False))
         eng.add_request([5, 6, 7], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
