@@ -612,8 +612,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
   // an even phase, half 0 in an odd one) interleaved in the first 2 NL MFMAs and, in an odd phase, the NL
   // loads of k-double `kd` from (oa, ob) into slot `wslot` spread over all NT
   auto phase = [&](auto odd_c, const bf16x8* af, const bf16x8* bfr, bf16x8* naf, bf16x8* nbf, int rslot,
-                   int wslot, const int* oa, const int* ob, int kd) {
+                   int wslot, const int* oa, const int* ob, int kd, auto rd_c) {
     constexpr bool ODD = decltype(odd_c)::value;
+    constexpr bool RD = decltype(rd_c)::value;  // read the next unit's fragments (false: the caller reads them later)
     const char* sr = smem + rslot * kDblBytes;
     char* da = smem + wslot * kDblBytes + wid * MI * 1024;
     char* db = smem + wslot * kDblBytes + kDblHalf + wid * 8192;
@@ -636,9 +637,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(da + gl * 1024), 16, oa[gl], soff, 0, 0);
       else if constexpr (ODD && LD)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(db + (gl - MI) * 1024), 16, ob[gl - MI], soff, 0, 0);
-      if constexpr (t % 2 == 0 && g < NL && g < MI)
+      if constexpr (RD && t % 2 == 0 && g < NL && g < MI)
         naf[g] = *reinterpret_cast<const bf16x8*>(sr + ar + g * 2048);
-      else if constexpr (t % 2 == 0 && g < NL)
+      else if constexpr (RD && t % 2 == 0 && g < NL)
         nbf[g - MI] = *reinterpret_cast<const bf16x8*>(sr + br + (g - MI) * 2048);
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -651,6 +652,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
   };
   using EvenT = std::integral_constant<bool, false>;
   using OddT = std::integral_constant<bool, true>;
+  using RdT = std::integral_constant<bool, true>;
+  // the RoPE / KV-write epilogue needs the registers of the next tile's first fragments: those are read after it
+  using LastRdT = std::integral_constant<bool, EPI != EPI_ROPE_KV>;
 
   const int nd = K / 64;  // host guarantees K % 64 == 0, nd >= 2
   int m0, n0;
@@ -689,43 +693,145 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
     int D = 0;
     for (; D < nd - 2; ++D) {
       const int s = (gd + D) & 1;
-      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0);
-      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, ca, cb, D + 2);
+      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0, RdT{});
+      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, ca, cb, D + 2, RdT{});
     }
-#pragma unroll
-    for (int e = 0; e < 2; ++e, ++D) {
+    int last_rslot = 0;
+    {
       const int s = (gd + D) & 1;
-      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0);
-      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, xa, xb, e);
+      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0, RdT{});
+      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, xa, xb, 0, RdT{});
+      ++D;
+    }
+    {
+      const int s = (gd + D) & 1;
+      phase(EvenT{}, a0, b0, a1, b1, s, 0, ca, cb, 0, RdT{});
+      phase(OddT{}, a1, b1, a0, b0, s ^ 1, s, xa, xb, 1, LastRdT{});
+      last_rslot = s ^ 1;
+      ++D;
     }
     // (a0, b0) hold the next tile's unit-0 fragments; this tile's accumulators are complete
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs retire
+    // RoPE / KV-write epilogue: the wave's 128 columns are one head h of [Hq | Hkv | Hkv]; lane (m, q) holds dims
+    // 16j + 4q + r (tile j) and, in tile j + 4, their rotate-half partners 64 further on. Every load is issued ahead
+    // of the stores that would otherwise serialise it: each row group's position, slot and 8 cos / sin vectors are
+    // loaded one or two groups early, before the earlier group's stores (vmcnt is in order and counts stores: a
+    // load issued after a store waits for the store too). Per-call loads cost a load + store round trip per 4 columns:
+    // QKV at M = 2406 112.8 vs 90.9 us for the plain GEMM (profiles/r5/c1_prefill_kernels_before_epi.csv). The
+    // registers come from the next tile's first fragments, which this epilogue reads after it (LastRdT).
+    // the lane id passes an opaque asm: nothing lane-dependent of this epilogue (64-bit store bases, offsets) is
+    // hoisted out of the tile walk into registers the main loop needs (it spilled them, and the scratch reloads queued
+    // behind the stores)
+    int rk_lane = lane;
+    asm volatile("" : "+v"(rk_lane));
+    const int rk_nb = n0 + wn * 128, rk_h = rk_nb / 128, rk_q = rk_lane >> 4;
+    const bool rk_rot = rk_h < rk.Hq + rk.Hkv;  // q and k heads are rotated, v heads only written
+    const __amdgpu_buffer_rsrc_t rk_rq = __builtin_amdgcn_make_buffer_rsrc(rk.q_out, (short)0, 0x7fffffff, 0x00020000);
+    int rk_pos[8], rk_slot[8];
+    float4 rk_cs[2][8];
+    auto rk_row = [&](int i) { return min(m0 + wm * 16 * MI + 16 * i + (rk_lane & 15), M - 1); };  // row of group i
+    // buffer loads (uniform resource + 32-bit lane offset): no per-lane 64-bit bases for the compiler to hoist out
+    // of the tile walk (they spilled at the kernel's 256-VGPR budget)
+    const __amdgpu_buffer_rsrc_t rk_rcs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rk.cos_sin), (short)0,
+                                                                             0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk_rpos = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(rk.pos), (short)0,
+                                                                              0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk_rslot = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(rk.slots), (short)0,
+                                                                               0x7fffffff, 0x00020000);
+    auto rk_load_cs = [&](int i, float4* dst) {
+      const int base = (rk_pos[i] * 128 + 4 * rk_q) * 4;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        dst[jj] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rk_rcs, base + 64 * jj, 0, 0));
+        dst[4 + jj] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rk_rcs, base + 256 + 64 * jj, 0, 0));
+      }
+    };
+    auto rk_ld_pos = [&](int i) { return (int)__builtin_amdgcn_raw_buffer_load_b32(rk_rpos, rk_row(i) * 4, 0, 0); };
+    auto rk_ld_slot = [&](int i) { return (int)__builtin_amdgcn_raw_buffer_load_b32(rk_rslot, rk_row(i) * 4, 0, 0); };
+    // positions two row groups ahead, slots one ahead (short live ranges: the epilogue holds 2 x 8 cos / sin vectors
+    // and the kernel sits at its 256-VGPR budget)
+    if constexpr (EPI == EPI_ROPE_KV) {
+      rk_pos[0] = rk_ld_pos(0);
+      if (MI > 1) rk_pos[1] = rk_ld_pos(1);
+      rk_slot[0] = rk_ld_slot(0);
+      if (rk_rot) rk_load_cs(0, rk_cs[0]);
+    }
     for_each_const<MI>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
+      if constexpr (EPI == EPI_ROPE_KV) {  // issued before this group's stores
+        if constexpr (i + 2 < MI) rk_pos[i + 2] = rk_ld_pos(i + 2);
+        if constexpr (i + 1 < MI) {
+          rk_slot[i + 1] = rk_ld_slot(i + 1);
+          if (rk_rot) rk_load_cs(i + 1, rk_cs[(i + 1) & 1]);
+        }
+      }
       f32x4 row[8];
       read_acc_row<i>(row, std::make_integer_sequence<int, 8>{});
       if constexpr (EPI == EPI_ROPE_KV) {
-        // the wave's 128 columns are one head h of [Hq | Hkv | Hkv]; lane (m, q) holds dims 16j + 4q + r
-        // (tile j) and, in tile j + 4, their rotate-half partners 64 further on
-        const int m = m0 + wm * 16 * MI + 16 * i + (lane & 15), nb = n0 + wn * 128, q = lane >> 4;
-        if (m < M && nb < N) {
+        const int m = m0 + wm * 16 * MI + 16 * i + (rk_lane & 15);
+        if (m < M && rk_nb < N) {
+          const float4* cs = rk_cs[i & 1];
+          const int slot = rk_slot[i];
+          const int blk = slot / kKvBlock, off = slot % kKvBlock;
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
+            const int i0 = 16 * jj + 4 * rk_q;
             bf16x4 x1, x2;
+            if (bias) {  // Qwen-style QKV bias (uniform branch)
+              const bf16x4 b1 = *reinterpret_cast<const bf16x4*>(bias + rk_nb + i0);
+              const bf16x4 b2 = *reinterpret_cast<const bf16x4*>(bias + rk_nb + i0 + 64);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int n = nb + 16 * jj + 4 * q + r;
-              x1[r] = (bf16)(row[jj][r] + (bias ? (float)bias[n] : 0.f));
-              x2[r] = (bf16)(row[jj + 4][r] + (bias ? (float)bias[n + 64] : 0.f));
+              for (int r = 0; r < 4; ++r) {
+                x1[r] = (bf16)(row[jj][r] + (float)b1[r]);
+                x2[r] = (bf16)(row[jj + 4][r] + (float)b2[r]);
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                x1[r] = (bf16)row[jj][r];
+                x2[r] = (bf16)row[jj + 4][r];
+              }
             }
-            rope_kv_store<128, bf16>(x1, x2, m, nb / 128, 16 * jj + 4 * q, rk.pos, rk.cos_sin, rk.slots, rk.q_out,
-                                     rk.k_cache, rk.v_cache, rk.Hq, rk.Hkv, 1, 1.f, 1.f);
+            if (rk_rot) {  // the rounding of rope_kv_store: bf16 inputs, fp32 rotation, bf16 result
+              const float cc[4] = {cs[jj].x, cs[jj].y, cs[jj].z, cs[jj].w};
+              const float ss[4] = {cs[4 + jj].x, cs[4 + jj].y, cs[4 + jj].z, cs[4 + jj].w};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float a = (float)x1[r], b = (float)x2[r];
+                x1[r] = (bf16)(a * cc[r] - b * ss[r]);
+                x2[r] = (bf16)(b * cc[r] + a * ss[r]);
+              }
+            }
+            if (rk_h < rk.Hq) {  // q_out [M, Hq, 128] (< 2 GiB: 32-bit buffer offsets)
+              const int qo = ((m * rk.Hq + rk_h) * 128 + i0) * 2;
+              using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x1), rk_rq, qo, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x2), rk_rq, qo + 128, 0, 0);
+            } else if (slot >= 0 && rk_rot) {
+              bf16* dst = rk.k_cache + (((size_t)blk * rk.Hkv + (rk_h - rk.Hq)) * kKvBlock + off) * 128;
+              *reinterpret_cast<bf16x4*>(dst + i0) = x1;
+              *reinterpret_cast<bf16x4*>(dst + i0 + 64) = x2;
+            } else if (slot >= 0) {
+              bf16* dst = rk.v_cache + ((size_t)blk * rk.Hkv + (rk_h - rk.Hq - rk.Hkv)) * 128 * kKvBlock + off;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                dst[(size_t)(i0 + r) * kKvBlock] = x1[r];
+                dst[(size_t)(i0 + 64 + r) * kKvBlock] = x2[r];
+              }
+            }
           }
         }
       } else {
         epilogue_rows<EPI, OUTF32, 8>(row, C, bias, R, M, N, ldc, m0 + wm * 16 * MI + 16 * i, n0 + wn * 128, lane);
       }
     });
+    if constexpr (EPI == EPI_ROPE_KV) {  // the next tile's unit-0 fragments (the last phase skipped them)
+      const char* sr = smem + last_rslot * kDblBytes;
+#pragma unroll
+      for (int g = 0; g < MI; ++g) a0[g] = *reinterpret_cast<const bf16x8*>(sr + a_rd0 + g * 2048);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) b0[g] = *reinterpret_cast<const bf16x8*>(sr + b_rd0 + g * 2048);
+    }
     asm volatile(GAI_AGPR_ZERO "s_nop 7\n\ts_nop 7\n" ::: GAI_AGPR_CLOBBERS);
     m0 = nm0;
     n0 = nn0;
