@@ -1266,11 +1266,14 @@ void launch_w4p(const void* A, const void* B, void* C, const void* bias, const v
 // Tile height of the w4d walk: 192 rows when its tiles quantise onto the CUs' waves enough better to pay for the
 // smaller tile's lower rate (15 % per FLOP: M = 16384 QKV / O / gate_up 645 / 406 / 3096 us vs 559 / 358 / 2634 on
 // 256-row tiles): cost = waves x rows. M = 2406, N = 4096 (O / down): 10 x 16 = 160 tiles of 256 rows (1 wave x 256)
-// vs 13 x 16 = 208 of 192 (1 x 192): O 77.9 -> 66.7 us, down 255.1 -> 225.8 us (profiles/r5/gemm/w4d192.jsonl).
-// QKV (N 6144: 240 tiles vs 312 = 2 waves) and gate_up (1120 vs 1456 tiles: 5 x 256 vs 6 x 192) keep 256 rows;
-// M = 16384 keeps 256. GAI_GEMM_BM = 192 / 256 forces one.
+// vs 13 x 16 = 208 of 192 (1 x 192): O 77.9 -> 66.7 us, down 255.1 -> 225.8 us with cache-resident operands
+// (profiles/r5/gemm/w4d192.jsonl). QKV (N 6144: 240 tiles vs 312 = 2 waves) and gate_up (1120 vs 1456 tiles: 5 x 256
+// vs 6 x 192) keep 256 rows; M = 16384 keeps 256. GAI_GEMM_BM = 192 / 256 forces one.
 int w4d_rows(int M, int N, int ncu) {
-  static const int env = getenv("GAI_GEMM_BM") ? atoi(getenv("GAI_GEMM_BM")) : 0;
+  // opt-in (GAI_GEMM_BM=0 selects by the model below): with HBM-streamed operands the 192-row tile's shorter latency
+  // cover (3 phases of 48 MFMAs) loses more than the better wave quantisation gains (cold M = 2406 down 291.4 us vs
+  // 293.3 on 256 rows and 251.8 on the part ring, profiles/r5/gemm/cold_m2406_16384.jsonl)
+  static const int env = getenv("GAI_GEMM_BM") ? atoi(getenv("GAI_GEMM_BM")) : 256;
   if (env == 192 || env == 256) return env;
   const int G = ncu & ~7, tn = (N + LBN - 1) / LBN;
   auto cost = [&](int bm) { return (double)((((M + bm - 1) / bm) * tn + G - 1) / G) * bm; };
@@ -1476,12 +1479,15 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
       return;
     if (force == 12 && launch_w4x<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, std::max(2, split_parts(M, N, K))))
       return;
-    // deep K (activations streamed from HBM, e.g. the MLP down projection) and very wide N (gate_up) at large M:
-    // the part ring's longer A-operand latency cover wins (+7 % / +1-5 %, M = 16384); otherwise the double-slot
-    // kernel (+2-4 % on O / e5), profiles/r2/gemm_w4r.jsonl, gemm_rule.jsonl, gemm_w4p_ab.jsonl. Below M = 8192 the
-    // double-slot walk is the faster one there too (M = 2406 down 237.7 vs 252.3 us, gate_up 437.2 vs 444.4,
-    // M = 1024 gate_up 186.6 vs 189.9: profiles/r5/gemm/native_vs_hipblaslt_midM.jsonl).
-    if (force == 10 || (force == 0 && M >= 8192 && (K >= 8192 || N >= 16384)))
+    // the part ring (its operands get 2-3 phases of latency cover) with the operands streamed from HBM as in the
+    // model - every layer's weights are read once per forward, past the 256 MB Infinity Cache: it is the fastest
+    // or tied walk on every Llama-3-8B projection at M = 2406 and 16384 (O 78.9 vs 91.0 us double-slot / 88.6 on
+    // 192-row tiles, down 251.8 vs 293.3 / 291.4; profiles/r5/gemm/cold_m2406_16384.jsonl, tools/gemm_bench.py
+    // --cold). Back-to-back runs on one operand pair (cache-resident) favour the double-slot kernel by 2-15 % and
+    // misled the round-4 / early round-5 rules. Exception, measured in the model (profiles/r5/c1_prefill_kernels*.csv):
+    // the wide gate_up (N >= 16384, 1120 tiles) of a single 2406-token prompt runs 430.6 us per layer on the double-slot
+    // walk vs 445.4 on the part ring.
+    if (force == 10 || (force == 0 && !(M < 8192 && N >= 16384)))
       return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
     // force 9 / 13: the double-slot walk with 256- / 192-row tiles (tests, A/B); auto: w4d_rows
     return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, RopeKvArgs{},

@@ -39,29 +39,40 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cold", action="store_true",
+                    help="cycle operand copies (> 512 MB in all) so weights / activations stream from HBM as in the "
+                         "model, not from the 256 MB Infinity Cache")
     a = ap.parse_args()
     nat = ops.native()
     rows = []
     for M, name in [(int(m), n) for m in str(a.m).split(",") for n in a.shapes.split(",")]:
         N, K = SHAPES[name]
-        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+        ncopy = max(1, -(-(512 << 20) // ((M + N) * K * 2))) if a.cold else 1
+        xs = [torch.randn(M, K, device="cuda", dtype=torch.bfloat16) for _ in range(ncopy)]
+        ws = [(torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16) for _ in range(ncopy)]
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        arms = {"auto": lambda: nat.gemm(x, w, out, None, None, 0, 0),
-                "w4p": lambda: nat.gemm(x, w, out, None, None, 0, 8),
-                "w4d": lambda: nat.gemm(x, w, out, None, None, 0, 9),
-                "w4r": lambda: nat.gemm(x, w, out, None, None, 0, 10),
-                "w4s": lambda: nat.gemm(x, w, out, None, None, 0, 11),
-                "w4x": lambda: nat.gemm(x, w, out, None, None, 0, 12),
-                "w4d192": lambda: nat.gemm(x, w, out, None, None, 0, 13),
-                "tiled": lambda: nat.gemm(x, w, out, None, None, 0, 2),
-                "hipblaslt": lambda: torch.mm(x, w.t())}
+        it = [0]
+
+        def op():  # the next operand pair (one pair unless --cold)
+            it[0] = (it[0] + 1) % ncopy
+            return xs[it[0]], ws[it[0]]
+
+        def g(force):
+            x, w = op()
+            nat.gemm(x, w, out, None, None, 0, force)
+
+        def blas():
+            x, w = op()
+            torch.mm(x, w.t())
+        arms = {"auto": lambda: g(0), "w4p": lambda: g(8), "w4d": lambda: g(9), "w4r": lambda: g(10),
+                "w4s": lambda: g(11), "w4x": lambda: g(12), "w4d192": lambda: g(13), "tiled": lambda: g(2),
+                "hipblaslt": blas}
         ts = {k: [] for k in arms}
         for _ in range(a.rounds):
             for k, f in arms.items():
                 ts[k].append(timeit(f))
         fl = 2 * M * N * K
-        r = {"gemm": name, "M": M, "N": N, "K": K}
+        r = {"gemm": name, "M": M, "N": N, "K": K, "cold": bool(a.cold)}
         for k, v in ts.items():
             v.sort()
             r[f"{k}_ms"] = round(v[len(v) // 2], 4)
@@ -75,7 +86,7 @@ def main():
         r["auto_vs_blas"] = round(r["hipblaslt_ms"] / r["auto_ms"], 3)
         print(json.dumps(r), flush=True)
         rows.append(r)
-    if enable_tuned_blas():
+    if not a.cold and enable_tuned_blas():
         for r in rows:
             M, N, K = r["M"], r["N"], r["K"]
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
