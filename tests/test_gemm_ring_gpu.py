@@ -124,9 +124,10 @@ def test_stream_k_split_tiles(cuda, M, N, K, act, walk):
         assert torch.equal(_run(x, w, None, res, act, out_dtype, force=KERNELS[walk]), y)
 
 
-# 192-row tiles (8192 x 1024: 172 tiles vs 128 of 256 rows; 1300 x 6144) and 256-row tiles (2406 x 6144, with bias)
+# one tile per workgroup (8192 x 1024: 128 tiles; 1300 x 6144; 2406 x 6144 with bias) and a multi-tile walk
+# (8192 x 6144: 768 tiles, 3 per workgroup - the epilogue reads the next tile's first fragments after its stores)
 @pytest.mark.parametrize("M,K,Hq,Hkv,with_bias", [(8192, 512, 4, 2, False), (1300, 4096, 32, 8, False),
-                                                  (2406, 1024, 32, 8, True)])
+                                                  (2406, 1024, 32, 8, True), (8192, 256, 32, 8, False)])
 def test_prefill_qkv_rope_kv_fused(cuda, M, K, Hq, Hkv, with_bias):
     """Prefill QKV GEMM with RoPE + paged K / V^T write in its epilogue == gemm + rope_kv_write (same
     accumulators, same bf16 roundings); skipped slots (-1) leave the caches untouched."""
