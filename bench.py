@@ -141,7 +141,7 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
         return build_requests(qs, rows.cpu().tolist(), new_phase())
 
     # concurrency 1: each query runs its full max_tokens (TTFT and per-token latency of a lone stream)
-    c1, tpot = [], []
+    c1, tpot, c1_ret = [], [], []
     base = 900_000 + 1000 * rank
     for i in range(args.probe_c1):
         qid = base + i
@@ -149,6 +149,7 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
         _sync()
         t0 = time.perf_counter()
         req = retrieve([qid])[0]
+        c1_ret.append(time.perf_counter() - t0)  # embed + scan + prompt + add_request (host clock, not synced)
         while engine.has_work():
             engine.step()
         c1.append(req.first_token_time - t0)
@@ -187,6 +188,7 @@ def run_probes(args, embedder, index, engine, build_requests, plant, unplant, ne
     tt = sorted(r.first_token_time - t0 - a for a, r in reqs)
     tp = statistics.median(tpot) if tpot else float("nan")
     return {"p50_ttft_c1_s": round(statistics.median(c1), 4), "ttft_c1_s": [round(x, 4) for x in c1],
+            "ttft_c1_retrieve_ms": round(1000 * statistics.median(c1_ret), 2),
             "tpot_c1_ms": round(1000 * tp, 3), "decode_tok_s_c1": round(1.0 / tp, 1) if tpot else None,
             "poisson": {"rate_qps_per_gpu": round(rate, 3), "queries": n, "achieved_qps_per_gpu": round(n / span, 3),
                         "p50_ttft_s": round(tt[len(tt) // 2], 4),

@@ -844,7 +844,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vit_embed", &vit_embed);
   m.def("quant_rows_fp8", &quant_rows_fp8);
   m.def("attn_prefill", &attn_prefill);
-  m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv) { return gai_attn_prefill_rows_per_tile(hq, hkv); });
+  m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv, int64_t d) { return gai_attn_prefill_rows_per_tile(hq, hkv, d); },
+        py::arg("hq"), py::arg("hkv"), py::arg("d") = 128);
+  m.def("attn_prefill_set_hl", [](int64_t hl) { gai_attn_prefill_set_hl((int)hl); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("scale"), py::arg("split_keys"),
         py::arg("max_splits"), py::arg("k_scale"), py::arg("v_scale"), py::arg("split_cnt") = py::none(),

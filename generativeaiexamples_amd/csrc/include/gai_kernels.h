@@ -65,7 +65,8 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
                       int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
                       float v_scale, hipStream_t st);
-int gai_attn_prefill_rows_per_tile(int Hq, int Hkv);
+int gai_attn_prefill_rows_per_tile(int Hq, int Hkv, int D = 128);
+void gai_attn_prefill_set_hl(int hl);
 // Decode QKV tail folded into the decode-attention launch: the split-K QKV partial slabs part[ks][B][n] (n = (Hq +
 // 2 Hkv) D, no bias) are summed, rounded to bf16, rotated (RoPE at pos[seq]) inside attn_decode; the split holding
 // the newest key also writes that key / value into the paged caches at slots[seq].

@@ -87,14 +87,19 @@ __device__ __forceinline__ bf16x8 kv_to_bf16(bf16x8 v, float) { return v; }
 __device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to_bf16(v, s); }
 
 // KV = bf16 or fp8 (OCP e4m3fn cache, dequantised by the per-layer scale when the tile is written to LDS)
-template <int D, int HPW, typename KV>
-__global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
+// HL = q heads per wave (1 or 2, same 32 query rows): with 2, every K / V^T fragment a wave reads from LDS feeds two
+// MFMAs, halving the LDS read traffic per FLOP (with one head per wave the fragment reads + tile writes, ~2.5K LDS
+// cycles per CU per 64-key tile, exceed the ~2K MFMA cycles per SIMD); twice the registers, so one wave per SIMD.
+template <int D, int HPW, typename KV, int HL = 1>
+__global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
     float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale, int xcd) {
   using Cfg = PrefillCfg<D>;
-  constexpr int RPW = 4 / HPW;  // row groups per workgroup
+  static_assert(HL == 1 || HPW % HL == 0, "a wave's heads come from one workgroup head group");
+  constexpr int WPR = HPW / HL;  // waves per row group
+  constexpr int RPW = 4 / WPR;   // row groups per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   // xcd: head group = linear workgroup id mod gridDim.y. Workgroups go to the 8 XCDs round-robin by linear id, so
@@ -111,9 +116,9 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
   const int seq = tiles[2 * bx], qs = tiles[2 * bx + 1];
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int ctx = ctx_lens[seq];
-  const int head = by * HPW + (wid % HPW);
+  const int head = by * HPW + HL * (wid % WPR);  // first of this wave's HL heads
   const int g = (by * HPW) / (Hq / Hkv);
-  const int r0 = qs + 32 * (wid / HPW);  // first q row (within the sequence) of this wave
+  const int r0 = qs + 32 * (wid / WPR);  // first q row (within the sequence) of this wave
   const int qrow = r0 + (lane & 31);
   const int qpos = ctx - qlen + qrow;  // absolute position of this lane's query
   const int* bt = block_tables + (size_t)seq * max_blocks;
@@ -124,11 +129,20 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
   const int ntiles = (kmax + Cfg::KT - 1) / Cfg::KT;
 
   // Q fragments (B operand of S^T = K.Q^T): lane (q = lane&31, h) holds Q[q][16t + 8h .. +7]
-  bf16x8 qf[D / 16];
-  {
-    const bf16* qp = q + ((size_t)(qbeg + min(qrow, qlen - 1)) * Hq + head) * D + 8 * h;
+  // HL == 1: the Q fragments live in registers. HL == 2: in this wave's LDS region (padded rows like the K image),
+  // read once per tile per (head, k-step) - two heads' fragments in registers spill.
+  constexpr int QL = HL == 1 ? 1 : 0;  // heads whose fragments stay in registers
+  bf16x8 qf[QL ? HL : 1][D / 16];
+  char* sq = smem + 2 * Cfg::BUF + wid * (HL * 32 * Cfg::KRS);
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) qf[t] = load8(qp + 16 * t);
+  for (int j = 0; j < HL; ++j) {
+    const bf16* qp = q + ((size_t)(qbeg + min(qrow, qlen - 1)) * Hq + head + j) * D + 8 * h;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+      const bf16x8 v = load8(qp + 16 * t);
+      if constexpr (QL) qf[j][t] = v;
+      else *reinterpret_cast<bf16x8*>(sq + (j * 32 + (lane & 31)) * Cfg::KRS + ((2 * t + h) << 4)) = v;
+    }
   }
 
   // One set of staging registers (raw cache bytes: the fp8 conversion happens at the LDS write), used
@@ -186,10 +200,15 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     }
   };
 
-  f32x16 acc_o[D / 32];
+  f32x16 acc_o[HL][D / 32];
+  float m_run[HL], l_run[HL];
 #pragma unroll
-  for (int i = 0; i < D / 32; ++i) acc_o[i] = f32x16{};
-  float m_run = kNeg, l_run = 0.f;
+  for (int j = 0; j < HL; ++j) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) acc_o[j][i] = f32x16{};
+    m_run[j] = kNeg;
+    l_run[j] = 0.f;
+  }
   const float sl2 = scale * kLog2e;
 
   if (ntiles > 0) {
@@ -212,16 +231,33 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     const char* sk = smem + cur * Cfg::BUF;
     const char* sv = sk + Cfg::KBYTES;
 
-    // S^T[key][q] for two 32-key halves
-    f32x16 s[2];
+    // S^T[key][q] for two 32-key halves (each K fragment feeds the wave's HL heads)
+    f32x16 s[HL][2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      s[sub] = f32x16{};
-      const int key = 32 * sub + (lane & 31);
+#pragma unroll
+      for (int j = 0; j < HL; ++j) s[j][sub] = f32x16{};
+      if constexpr (QL) {
+        const int key = 32 * sub + (lane & 31);
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
+#pragma unroll
+          for (int j = 0; j < HL; ++j) s[j][sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][t], s[j][sub], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (!QL) {  // k-step outer: each K fragment (both halves) and each Q fragment read once per tile
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
-        s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], s[sub], 0, 0, 0);
+        const bf16x8 kf0 = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(lane & 31, 2 * t + h));
+        const bf16x8 kf1 = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(32 + (lane & 31), 2 * t + h));
+#pragma unroll
+        for (int j = 0; j < HL; ++j) {
+          const bf16x8 qv = *reinterpret_cast<const bf16x8*>(sq + (j * 32 + (lane & 31)) * Cfg::KRS + ((2 * t + h) << 4));
+          s[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf0, qv, s[j][0], 0, 0, 0);
+          s[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf1, qv, s[j][1], 0, 0, 0);
+        }
       }
     }
     if (more) {  // buffer cur ^ 1 was released by the previous barrier
@@ -232,13 +268,17 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
     // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves.
     // Interior tiles (every key < ctx and, causal, <= the wave's first query position) skip the
     // per-element mask: wave-uniform test, so only the diagonal / tail tiles pay for it.
-    float mt = kNeg;
+    float mt[HL];
+#pragma unroll
+    for (int j = 0; j < HL; ++j) mt[j] = kNeg;
     const int kend = kt * 64 + 63;
     if (kend < ctx && (!causal || kend <= ctx - qlen + r0)) {
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int j = 0; j < HL; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[sub][r]);
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mt[j] = fmaxf(mt[j], s[j][sub][r]);
     } else {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -246,66 +286,86 @@ __global__ __launch_bounds__(256, D > 128 ? 1 : 2) void attn_prefill_kernel(
         for (int r = 0; r < 16; ++r) {
           const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
           const bool ok = key < ctx && (!causal || key <= qpos);
-          const float x = ok ? s[sub][r] : kNeg;
-          s[sub][r] = x;
-          mt = fmaxf(mt, x);
+#pragma unroll
+          for (int j = 0; j < HL; ++j) {
+            const float x = ok ? s[j][sub][r] : kNeg;
+            s[j][sub][r] = x;
+            mt[j] = fmaxf(mt[j], x);
+          }
         }
     }
     // scores stay unscaled; the scale folds into the max (scale > 0) and into one fma per exp
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
-    const float m_new = fmaxf(m_run, mt);
-    const float alpha = fexp2(m_run - m_new);
-    // lazy rescale: once the running maxima settle (most tiles after the first few) alpha == 1 in
-    // every lane and the D/32 x 16 accumulator multiplies are skipped (bit-identical result)
-    if (__any(alpha != 1.f)) {
+    float m_new[HL], alpha[HL];
 #pragma unroll
-      for (int i = 0; i < D / 32; ++i) acc_o[i] *= alpha;
+    for (int j = 0; j < HL; ++j) {
+      mt[j] = fmaxf(mt[j], __shfl_xor(mt[j], 32, 64)) * sl2;
+      m_new[j] = fmaxf(m_run[j], mt[j]);
+      alpha[j] = fexp2(m_run[j] - m_new[j]);
+      // lazy rescale: once the running maxima settle (most tiles after the first few) alpha == 1 in
+      // every lane and the D/32 x 16 accumulator multiplies are skipped (bit-identical result)
+      if (__any(alpha[j] != 1.f)) {
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) acc_o[j][i] *= alpha[j];
+      }
+      m_run[j] = m_new[j];
     }
-    m_run = m_new;
 
     // O^T[d][q] += V^T[d][key] . P^T[key][q]. The 8 probabilities of each 8-key step are exponentiated
     // right before that step's MFMAs, so step st's MFMAs run in the matrix pipe while step st+1's
-    // v_exp / cvt issue (the row sum is only needed after the tile).
-    float rs = 0.f;
+    // v_exp / cvt issue (the row sum is only needed after the tile). Each V^T fragment feeds the HL heads.
+    float rs[HL];
+#pragma unroll
+    for (int j = 0; j < HL; ++j) rs[j] = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int sub = st >> 1, sp = st & 1;
-      bf16x8 pf;
+      bf16x8 pf[HL];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = fexp2(fmaf(s[sub][8 * sp + j], sl2, -m_new));
-        rs += p;
-        pf[j] = (bf16)p;
-      }
+      for (int j = 0; j < HL; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float p = fexp2(fmaf(s[j][sub][8 * sp + e], sl2, -m_new[j]));
+          rs[j] += p;
+          pf[j][e] = (bf16)p;
+        }
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
         // units 4st + h (lo) and 4st + 2 + h (hi) of row d: one 16-B pair in the image
         const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off<D>(32 * dt + (lane & 31), 4 * st + h));
-        acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[dt], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < HL; ++j)
+          acc_o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], acc_o[j][dt], 0, 0, 0);
       }
     }
-    rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
+#pragma unroll
+    for (int j = 0; j < HL; ++j) {
+      rs[j] += __shfl_xor(rs[j], 32, 64);
+      l_run[j] = l_run[j] * alpha[j] + rs[j];
+    }
     if (more) write_v(cur ^ 1);
     __syncthreads();
   }
 
   if (qrow < qlen) {
-    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-    bf16* op = out + ((size_t)(qbeg + qrow) * Hq + head) * D;
 #pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
+    for (int j = 0; j < HL; ++j) {
+      const float inv = l_run[j] > 0.f ? 1.f / l_run[j] : 0.f;
+      bf16* op = out + ((size_t)(qbeg + qrow) * Hq + head + j) * D;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-        bf16x4_t o;
+      for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc_o[dt][4 * c + r] * inv);
-        *reinterpret_cast<bf16x4_t*>(op + 32 * dt + 8 * c + 4 * h) = o;
-      }
-    // natural-log softmax normaliser per (row, head): merges partial results (ring attention)
-    if (lse != nullptr && h == 0)
-      lse[(size_t)(qbeg + qrow) * Hq + head] = l_run > 0.f ? (m_run + __log2f(l_run)) * 0.69314718055994531f : kNeg;
+        for (int c = 0; c < 4; ++c) {
+          typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc_o[j][dt][4 * c + r] * inv);
+          *reinterpret_cast<bf16x4_t*>(op + 32 * dt + 8 * c + 4 * h) = o;
+        }
+      // natural-log softmax normaliser per (row, head): merges partial results (ring attention)
+      if (lse != nullptr && h == 0)
+        lse[(size_t)(qbeg + qrow) * Hq + head + j] =
+            l_run[j] > 0.f ? (m_run[j] + __log2f(l_run[j])) * 0.69314718055994531f : kNeg;
+    }
   }
 }
 
@@ -745,7 +805,18 @@ void set_max_lds(F* f, int bytes) {
   }
 }
 
+// Heads per wave of the prefill kernel (attn_prefill_kernel HL): 2 for head_dim 128 with >= 4 q heads per kv head when
+// enabled (GAI_ATTN_HL=2 or gai_attn_prefill_set_hl), else 1. The tile list's rows per tile follow it
+// (gai_attn_prefill_rows_per_tile), so it is read once per process unless set explicitly.
+int g_prefill_hl = -1;
+int prefill_hl(int D, int ratio) {
+  if (g_prefill_hl < 0) g_prefill_hl = getenv("GAI_ATTN_HL") ? atoi(getenv("GAI_ATTN_HL")) : 1;
+  return g_prefill_hl == 2 && D == 128 && ratio >= 4 ? 2 : 1;
+}
+
 }  // namespace
+
+void gai_attn_prefill_set_hl(int hl) { g_prefill_hl = hl == 2 ? 2 : 1; }
 
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
@@ -760,6 +831,25 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   // GAI_ATTN_XCD=0 / 2: off / on everywhere.
   static const int xcd_env = getenv("GAI_ATTN_XCD") ? atoi(getenv("GAI_ATTN_XCD")) : 1;
   const int xcd = xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal);
+  const int hl = prefill_hl(D, ratio);
+  if (hl == 2) {  // D == 128, hpw == 4: 64 rows per tile; + the 4 waves' Q images (2 heads x 32 rows each)
+    const int lds = 2 * PrefillCfg<128>::BUF + 4 * 2 * 32 * PrefillCfg<128>::KRS;
+    if (kv_fp8) {
+      auto kern = attn_prefill_kernel<128, 4, fp8, 2>;
+      set_max_lds(kern, lds);
+      kern<<<dim3(ntiles, Hq / 4), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,
+                                                   block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
+                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd);
+    } else {
+      auto kern = attn_prefill_kernel<128, 4, bf16, 2>;
+      set_max_lds(kern, lds);
+      kern<<<dim3(ntiles, Hq / 4), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,
+                                                   block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
+                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd);
+    }
+    GAI_LAUNCH_CHECK();
+    return;
+  }
 #define GAI_PF(DD, HP)                                                                                         \
   if (D == DD && hpw == HP) {                                                                                  \
     const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
@@ -795,10 +885,10 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   gai_launch_error(__FILE__, __LINE__, "attn_prefill: unsupported head_dim");
 }
 
-int gai_attn_prefill_rows_per_tile(int Hq, int Hkv) {
+int gai_attn_prefill_rows_per_tile(int Hq, int Hkv, int D) {
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
-  return 32 * (4 / hpw);
+  return 32 * (4 / (hpw / prefill_hl(D, ratio)));
 }
 
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,

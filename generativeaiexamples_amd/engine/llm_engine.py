@@ -389,7 +389,7 @@ class LLMEngine:
         arrs = [b.token_ids, b.positions, b.slots, cu, b.prefill_ctx, b.prefill_block_tables, b.decode_ctx,
                 b.decode_block_tables, np.asarray(rows, dtype=np.int32)]
         if P > 0:
-            rpt = ops.prefill_rows_per_tile(self.model.hq, self.model.hkv)
+            rpt = ops.prefill_rows_per_tile(self.model.hq, self.model.hkv, self.model.cfg.head_dim)
             arrs.append(ops.prefill_tile_list(b.prefill_qlen, rpt, b.prefill_ctx))
         plan = dict(op="eager", P=int(P), arr=arrs, qlen=[int(x) for x in b.prefill_qlen],
                     pctx=[int(x) for x in b.prefill_ctx], max_dctx=int(b.decode_ctx.max()) if nd else 0,

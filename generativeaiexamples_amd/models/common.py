@@ -125,7 +125,8 @@ class PackedAttention:
         self.slots = kv_slots.to(dev, non_blocking=True)
         self.cu_q = torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True)
         self.ctx = torch.tensor(kv_lens, dtype=torch.int32).to(dev, non_blocking=True)
-        self.tiles = ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev) if dev.type == "cuda" else None
+        self.tiles = (ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev, head_dim=head_dim) if dev.type == "cuda"
+                      else None)
         self.k_cache = torch.zeros(offs[-1] + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
         self.v_cache = torch.zeros(offs[-1] + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)
         self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)

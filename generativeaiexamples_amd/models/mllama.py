@@ -170,7 +170,8 @@ class _TileMaskAttention(PackedAttention):
             cu.append(cu[-1] + n)
         self.cu_q = torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=True)
         self.ctx = torch.tensor(ctx, dtype=torch.int32).to(dev, non_blocking=True)
-        self.tiles = ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev) if dev.type == "cuda" else None
+        self.tiles = (ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev, head_dim=head_dim) if dev.type == "cuda"
+                      else None)
         nblk = len(nvalid) * nb
         self.k_cache = torch.zeros(nblk + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
         self.v_cache = torch.zeros(nblk + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)

@@ -393,10 +393,20 @@ def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, H
                            v_scale)
 
 
-def prefill_rows_per_tile(Hq: int, Hkv: int) -> int:
+def prefill_rows_per_tile(Hq: int, Hkv: int, head_dim: int = 128) -> int:
+    """Query rows per attention_prefill tile; the kernel launcher owns the choice (it follows the heads per wave of
+    the prefill kernel, attention.hip prefill_hl), so GPU builds ask it."""
+    if torch.cuda.is_available():
+        return int(native().attn_prefill_rows_per_tile(Hq, Hkv, head_dim))
     r = Hq // Hkv
     hpw = 4 if r >= 4 else 2 if r >= 2 else 1
     return 32 * (4 // hpw)
+
+
+def set_prefill_heads_per_wave(hl: int) -> None:
+    """Prefill attention heads per wave (1 or 2; 2 applies to head_dim 128 with >= 4 q heads per kv head). Tile lists
+    built before a change keep the old rows per tile: build them after setting it."""
+    native().attn_prefill_set_hl(int(hl))
 
 
 def prefill_tile_list(q_lens: Sequence[int], rows: int, ctx_lens: Sequence[int] | None = None) -> np.ndarray:
@@ -413,9 +423,9 @@ def prefill_tile_list(q_lens: Sequence[int], rows: int, ctx_lens: Sequence[int] 
 
 
 def build_prefill_tiles(q_lens: Sequence[int], Hq: int, Hkv: int, device,
-                        ctx_lens: Sequence[int] | None = None) -> torch.Tensor:
+                        ctx_lens: Sequence[int] | None = None, head_dim: int = 128) -> torch.Tensor:
     """Host-side varlen tile list [(seq, q_start), ...] for attention_prefill (longest tile first)."""
-    t = prefill_tile_list(q_lens, prefill_rows_per_tile(Hq, Hkv), ctx_lens)
+    t = prefill_tile_list(q_lens, prefill_rows_per_tile(Hq, Hkv, head_dim), ctx_lens)
     return torch.from_numpy(t).reshape(-1).to(device, non_blocking=True)
 
 
@@ -434,7 +444,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
         if q_lens is None:
             cu = cu_q.tolist()
             q_lens = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
-        tiles = build_prefill_tiles(q_lens, Hq, Hkv, q.device)
+        tiles = build_prefill_tiles(q_lens, Hq, Hkv, q.device, head_dim=q.shape[2])
     out = torch.empty_like(q) if out is None else out
     native().attn_prefill(q, k_cache, v_cache, block_tables, tiles, cu_q, ctx_lens, out, Hq, Hkv, scale, causal, lse,
                           k_scale, v_scale)

@@ -160,6 +160,35 @@ def test_attention_prefill_long(cuda, L, D, Hq, Hkv):
             _close(o[int(cu[s]):int(cu[s]) + n, h], ref_o, 2e-2, 2e-2, f"prefill L={n} h={h}")
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_prefill_two_heads_per_wave(cuda, Hq, Hkv, causal):
+    """The head_dim-128 prefill kernel with two q heads per wave (64 query rows per tile, Q fragments staged in LDS)
+    against the fp32 reference and against the one-head kernel: varlen, chunked prefill over a cached prefix, and a
+    long sequence (multi-tile walks, diagonal and interior key tiles)."""
+    torch.manual_seed(11)
+    D = 128
+    ctx = [1, 77, 130, 300, 1500]
+    qlen = [1, 77, 33, 300, 1500] if causal else ctx
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, cuda, seed=3)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(int(cu[-1]), Hq, D, device=cuda, dtype=torch.bfloat16)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    outs = []
+    try:
+        for hl in (2, 1):
+            ops.set_prefill_heads_per_wave(hl)
+            assert ops.prefill_rows_per_tile(Hq, Hkv, D) == (64 if hl == 2 else 32 * 4 // min(4, Hq // Hkv))
+            outs.append(ops.attention_prefill(q, kc, vc, bt, cu.to(cuda), ctx_t.to(cuda), scale, causal, q_lens=qlen))
+    finally:
+        ops.set_prefill_heads_per_wave(1)
+    o_ref = ref.attention_prefill(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu, ctx_t, scale, causal)
+    _close(outs[0], o_ref, 2e-2, 2e-2, "prefill, two heads per wave")
+    # same math per head (the k-step loop order of QK^T differs: fp32 sums in another order)
+    assert (outs[0].float() - outs[1].float()).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 64, 8), (64, 8, 8), (128, 4, 4)])
 def test_attention_decode(cuda, D, Hq, Hkv):
     torch.manual_seed(6)

@@ -172,7 +172,7 @@ def bench_prefill(rows, B, S, Hq, Hkv, D):
     q = torch.randn(B * S, Hq, D, device="cuda", dtype=torch.bfloat16)
     cu = torch.arange(0, B * S + 1, S, device="cuda", dtype=torch.int32)
     ctx = torch.full((B,), S, device="cuda", dtype=torch.int32)
-    tiles = ops.build_prefill_tiles([S] * B, Hq, Hkv, "cuda")
+    tiles = ops.build_prefill_tiles([S] * B, Hq, Hkv, "cuda", head_dim=D)
     t = timeit(lambda: ops.attention_prefill(q, kc, vc, bt, cu, ctx, 1 / math.sqrt(D), True, tiles=tiles))
     qs = q.view(B, S, Hq, D).transpose(1, 2)
     ks = torch.randn(B, Hkv, S, D, device="cuda", dtype=torch.bfloat16).repeat_interleave(Hq // Hkv, 1)

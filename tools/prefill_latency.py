@@ -32,7 +32,7 @@ def main():
                       slots=slots, num_prefill_tokens=T,
                       cu_q=torch.tensor([0, T], device="cuda", dtype=torch.int32),
                       prefill_ctx=torch.tensor([T], device="cuda", dtype=torch.int32), prefill_block_tables=bt,
-                      prefill_tiles=ops.build_prefill_tiles([T], m.hq, m.hkv, "cuda"), prefill_qlen=[T],
+                      prefill_tiles=ops.build_prefill_tiles([T], m.hq, m.hkv, "cuda", head_dim=c.head_dim), prefill_qlen=[T],
                       prefill_ctx_host=[T], sample_rows=torch.tensor([T - 1], device="cuda", dtype=torch.int64))
     with torch.inference_mode():
         for _ in range(3):

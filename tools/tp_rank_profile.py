@@ -91,7 +91,7 @@ def prefill_batch(m, T):
                       slots=(bt[0, pos.long() // ops.BLOCK] * ops.BLOCK + pos % ops.BLOCK).int(), num_prefill_tokens=T,
                       cu_q=torch.tensor([0, T], device="cuda", dtype=torch.int32),
                       prefill_ctx=torch.tensor([T], device="cuda", dtype=torch.int32), prefill_block_tables=bt,
-                      prefill_tiles=ops.build_prefill_tiles([T], m.hq, m.hkv, "cuda"), prefill_qlen=[T],
+                      prefill_tiles=ops.build_prefill_tiles([T], m.hq, m.hkv, "cuda", head_dim=c.head_dim), prefill_qlen=[T],
                       prefill_ctx_host=[T], sample_rows=torch.tensor([T - 1], device="cuda", dtype=torch.int64))
     return fb, kv
 
