@@ -487,7 +487,11 @@ class DecodeWorkspace:
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128
-        return int(min(max(s, 128), _DECODE_MAX_SPLIT))
+        # a few (sequence, kv head) pairs (batch 1-2 at 8 kv heads): the kernel is latency-bound, and 256-key splits
+        # beat 128-key ones: batch 1 10.6-11.0 vs 11.7-12.2 us per layer (profiles/r5/gemv_b1/attn_b1_split_sweep.log),
+        # decode step 3.00-3.03 -> 2.97-2.99 ms, batch 2 3.565 -> 3.512 ms (decode_small_batch.txt)
+        lo = 256 if batch * hkv <= 16 and not _DECODE_TARGET_ENV else 128
+        return int(min(max(s, lo), _DECODE_MAX_SPLIT))
 
     def split_for(self, batch: int, hkv: int, max_ctx: int) -> int:
         if self.fixed_split:
