@@ -224,7 +224,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
     check_f32(*cos_sin, "cos_sin");
     const int64_t n = (int64_t)(Hq + 2 * Hkv) * D;
     TORCH_CHECK(f8 == 0 && D == 128, "attn_decode: the folded QKV tail needs head_dim 128 and a bf16 cache");
-    TORCH_CHECK(part_ks >= 1 && part_ks <= 8 && qkv_part->numel() >= part_ks * B * n && qkv_part->is_contiguous(),
+    TORCH_CHECK(part_ks >= 1 && part_ks <= 16 && qkv_part->numel() >= part_ks * B * n && qkv_part->is_contiguous(),
                 "attn_decode: qkv_part must hold part_ks x B x (Hq + 2 Hkv) x D floats");
     TORCH_CHECK(positions->numel() >= B && slots->numel() >= B && cos_sin->size(-1) == D,
                 "attn_decode: positions / slots [B], cos_sin [max_pos, D]");

@@ -912,7 +912,10 @@ int gai_gemm_qkv_partials(const void* A, const void* B, int M, int N, int K, flo
   if (gai_gemm_dec2_ok(M, N, K, EPI_NONE)) return 0;  // single-pass kernel owns it
   const int ks2 = gai_gemm_dec2_partials_ks(M, N, K);
   const int KS = ks2 ? ks2 : gai_gemm_splitk_ks(M, N, K);
-  if (KS < 2 || KS > 8) return 0;
+  // up to 16 slabs: the TP = 8 shard of Llama-3-70B (N 1280, K 8192) takes 16 K-slices to reach 192 workgroups;
+  // GAI_QKV_FOLD_MAXKS = 8 restores the round-5 limit (A/B)
+  static const int max_ks = getenv("GAI_QKV_FOLD_MAXKS") ? atoi(getenv("GAI_QKV_FOLD_MAXKS")) : 16;
+  if (KS < 2 || KS > max_ks) return 0;
   if (ks2)
     gai_gemm_dec2_partials(A, B, M, N, K, ws, st, psw);
   else
