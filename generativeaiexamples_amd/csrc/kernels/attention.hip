@@ -908,7 +908,7 @@ void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, co
   // non-temporal K / V loads in the fused bf16 kernel (GAI_DECODE_NT=0: plain loads). Llama-3-8B B = 64, ctx 2535
   // graph replay 7.84 -> 7.68 ms per step (profiles/r4/decode/decode_nt_split_ab.txt)
   static const bool ntl = !(getenv("GAI_DECODE_NT") && atoi(getenv("GAI_DECODE_NT")) == 0);
-  if (fold != nullptr && !(fuse && ntl && !kv_fp8 && D == 128 && fold->ks >= 1 && fold->ks <= 8))
+  if (fold != nullptr && !(fuse && ntl && !kv_fp8 && D == 128 && fold->ks >= 1 && fold->ks <= 16))
     gai_launch_error(__FILE__, __LINE__, "attn_decode: the folded QKV tail needs the fused non-temporal bf16 kernel");
   if (fold != nullptr) {
     attn_decode_kernel<128, false, 1, true, bf16, true, true, true><<<grid, 256, 0, st>>>(
