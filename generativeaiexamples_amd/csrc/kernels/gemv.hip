@@ -24,7 +24,7 @@ using namespace gai;
 
 namespace {
 
-constexpr int kGvWaves = 8;  // waves per workgroup (default); 6 where 8 leaves the grid unbalanced (gemv_waves)
+constexpr int kGvWaves = 8;  // waves per workgroup (default); 12 where 8 leaves the grid unbalanced (gemv_waves)
 constexpr int kGvThreads = 64 * kGvWaves;
 constexpr int kPiece = 512;  // K elements of one wave load (64 lanes x 8 bf16)
 constexpr int kG = 4;        // pieces per row per pipeline group
@@ -236,12 +236,27 @@ __global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
   }
 }
 
-// Waves per workgroup: 8. GAI_GEMV_WAVES=6 (sweeps): 6-wave workgroups, which balance the Llama-3-8B QKV grid
-// (N 6144: 512 workgroups = 2 per CU instead of 384 = 1.5) but stage the normalised activations in 1/3 more
-// workgroups - measured slower (13.2 vs 11.4 us, profiles/r5/gemv_b1), so not the default.
-int gemv_waves(int) {
+// Waves per workgroup: 8, or 12 where that quantises the row pairs onto the CUs better (Llama-3-8B QKV, N 6144: 3072
+// pairs = 384 eight-wave workgroups, 1.5 per CU, vs 256 twelve-wave ones). 6-wave workgroups also balance that grid
+// (512 = 2 per CU) but stage the normalised activations in 1/3 more workgroups - measured slower (13.2 vs 11.4 us,
+// profiles/r5/gemv_b1). Batch 1 only: QKV 11.42 -> 10.53 us, decode step 3.007 -> 2.97 ms; at batch 4 the step
+// went 4.466 -> 4.530 ms (profiles/r5/gemv_b1/gemv_12waves_ab.txt). GAI_GEMV_WAVES = 6 / 8 / 12 forces one (sweeps).
+int gemv_waves(int N, int M) {
   static const int force = getenv("GAI_GEMV_WAVES") ? atoi(getenv("GAI_GEMV_WAVES")) : 0;
-  return force == 6 ? 6 : 8;
+  if (force == 6 || force == 8 || force == 12) return force;
+  if (M != 1) return 8;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      ncu = 256;
+  }
+  auto fill = [&](int nw) {  // fraction of the workgroup slots (one per CU per round) the grid's rounds use
+    const int grid = (N / 2 + nw - 1) / nw;
+    return (double)grid / ((double)((grid + ncu - 1) / ncu) * ncu);
+  };
+  return fill(12) > fill(8) + 0.1 ? 12 : 8;
 }
 
 template <int EPI, int NW>
@@ -270,7 +285,9 @@ void gemv_launch_nw(const GemvArgs& a, hipStream_t st) {
 
 template <int EPI>
 void gemv_launch(const GemvArgs& a, hipStream_t st) {
-  if (gemv_waves(a.N) == 6) return gemv_launch_nw<EPI, 6>(a, st);
+  const int nw = gemv_waves(a.N, a.M);
+  if (nw == 6) return gemv_launch_nw<EPI, 6>(a, st);
+  if (nw == 12) return gemv_launch_nw<EPI, 12>(a, st);
   gemv_launch_nw<EPI, 8>(a, st);
 }
 
