@@ -107,6 +107,9 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   // on it re-read that head's K/V prefixes from the XCD's own L2 instead of all heads' prefixes streaming through
   // every XCD. MI355X (profiles/r3/attn_prefill_xcd): B 4 x S 2048 GQA 32/8 D 128 604 -> 660 TF/s, the headline
   // chunk (7 x 2406) 703 -> 728, Gemma D 256 315 -> 473; 64 x 512 MHA D 64 413 -> 394. GAI_ATTN_XCD=0: off.
+  // xcd bits 1-2: wave priority around the MFMA phases (A/B, GAI_ATTN_PRIO): 1 = QK^T at priority 1, 2 = QK^T and P.V
+  const int prio = xcd >> 1;
+  xcd &= 1;
   int bx = blockIdx.x, by = blockIdx.y;
   if (xcd) {
     const int L = blockIdx.y * gridDim.x + blockIdx.x;
@@ -232,6 +235,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     const char* sv = sk + Cfg::KBYTES;
 
     // S^T[key][q] for two 32-key halves (each K fragment feeds the wave's HL heads)
+    if (prio) __builtin_amdgcn_s_setprio(1);
     f32x16 s[HL][2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
         }
       }
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
     if (more) {  // buffer cur ^ 1 was released by the previous barrier
       write_k(cur ^ 1);
       load_half(vc);
@@ -316,6 +321,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     float rs[HL];
 #pragma unroll
     for (int j = 0; j < HL; ++j) rs[j] = 0.f;
+    if (prio == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int sub = st >> 1, sp = st & 1;
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
           acc_o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], acc_o[j][dt], 0, 0, 0);
       }
     }
+    if (prio == 2) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int j = 0; j < HL; ++j) {
       rs[j] += __shfl_xor(rs[j], 32, 64);
@@ -830,7 +837,10 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   // cross-attention over the vision tokens) ran 6.69 -> 6.52 q/s with it (profiles/r3/attn_prefill_xcd).
   // GAI_ATTN_XCD=0 / 2: off / on everywhere.
   static const int xcd_env = getenv("GAI_ATTN_XCD") ? atoi(getenv("GAI_ATTN_XCD")) : 1;
-  const int xcd = xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal);
+  // wave priority 1 while a wave issues its QK^T / P.V MFMAs (0 in the softmax): +1-2 % on every head_dim-64/128 shape
+  // (headline chunk 707-714 -> 721 TF/s, profiles/r5/attn_prefill/prio_ab.txt); GAI_ATTN_PRIO = 0 / 1 for A/B
+  static const int prio_env = getenv("GAI_ATTN_PRIO") ? atoi(getenv("GAI_ATTN_PRIO")) : 2;
+  const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1);
   const int hl = prefill_hl(D, ratio);
   if (hl == 2) {  // D == 128, hpw == 4: 64 rows per tile; + the 4 waves' Q images (2 heads x 32 rows each)
     const int lds = 2 * PrefillCfg<128>::BUF + 4 * 2 * 32 * PrefillCfg<128>::KRS;
