@@ -591,6 +591,11 @@ class LlamaModel:
                    and T >= 2 * int(os.environ.get("GAI_TP_OVERLAP_CHUNK_ROWS", "1024")))
         # TP: the all-reduce of each row-parallel projection carries the residual add and the next RMSNorm
         tp_norm = (ctx.tp_size > 1 and c.norm != "layernorm" and os.environ.get("GAI_FUSE_NORM", "1") == "1")
+        # TP = 1 prefill: the O / down GEMMs' residual epilogue writes bf16(bf16(h) + residual) into the residual
+        # stream in place - the rounding the residual-adding norm kernel applies - and the norms then only read it:
+        # one fewer [T, d] read and write per norm (a 16K-token chunk: 134 MB each)
+        res_epi = (res.is_cuda and ctx.tp_size == 1 and not fuse and not self.lora_names
+                   and os.environ.get("GAI_RES_EPI", "1") == "1")
         for i in range(c.num_layers):
             p = f"l{i}."
             if xn is not None:
@@ -626,6 +631,9 @@ class LlamaModel:
             elif overlap:  # TP prefill: each row chunk's all-reduce overlaps the next chunk's GEMM
                 h = ctx.tp_linear_all_reduce(a2, w[p + "o"], self._row_bias(p + "o_b"))
                 x = self._norm(h, p + "mlp_norm", residual=res)
+            elif res_epi:
+                ops.linear(a2, w[p + "o"], bias=w.get(p + "o_b"), residual=res, out=res)
+                x = self._norm(res, p + "mlp_norm")
             else:
                 h = self._lora(ops.linear(a2, w[p + "o"], bias=self._row_bias(p + "o_b")), a2, i, "o", fb)
                 if tp_norm:  # all-reduce + residual add + RMSNorm in one peer-memory kernel
@@ -644,6 +652,9 @@ class LlamaModel:
                 h = None
             elif overlap:
                 h = ctx.tp_linear_all_reduce(g, w[p + "down"], self._row_bias(p + "down_b"))
+            elif res_epi:  # the next layer's norm (or the final one) reads the updated residual stream
+                ops.linear(g, w[p + "down"], bias=w.get(p + "down_b"), residual=res, out=res)
+                h = None
             else:
                 h = ops.linear(g, w[p + "down"], bias=self._row_bias(p + "down_b"))
                 if tp_norm and not (last and fb.sample_rows is not None):
@@ -658,9 +669,9 @@ class LlamaModel:
                 return logits
             return ctx.tp_all_gather_last(logits)[:, : c.vocab_size]
         if fb.sample_rows is not None:
-            h = h.index_select(0, fb.sample_rows)
+            h = h.index_select(0, fb.sample_rows) if h is not None else None
             res = res.index_select(0, fb.sample_rows)
-        x = self._norm(h, "norm", residual=res)
+        x = self._norm(res, "norm") if h is None else self._norm(h, "norm", residual=res)
         logits = ops.linear(x, w["lm_head"], out_dtype=torch.float32)
         if fb.tp_local_logits and ctx.tp_size > 1:
             return logits
