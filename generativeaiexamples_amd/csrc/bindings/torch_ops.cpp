@@ -118,7 +118,8 @@ bool gemm_rope_kv(const Tensor& A, const Tensor& B, const optional<Tensor>& bias
   if (M > 64)  // prefill: RoPE + KV write in the 256x256 GEMM's epilogue (ws unused)
     return gai_gemm_prefill_rope_kv(A.data_ptr(), B.data_ptr(), opt_ptr(bias), pos.data_ptr<int>(),
                                     cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
-                                    k_cache.data_ptr(), v_cache.data_ptr(), M, K, Hq, Hkv, D, f8, cur_stream()) != 0;
+                                    k_cache.data_ptr(), v_cache.data_ptr(), M, K, Hq, Hkv, D, f8, cur_stream(),
+                                    psw ? 1 : 0) != 0;
   TORCH_CHECK(ws.scalar_type() == at::kFloat && (size_t)ws.numel() * 4 >= gai_gemm_splitk_ws_bytes(M, N, K),
               "gemm_rope_kv: workspace too small");
   int* cnt = nullptr;
@@ -145,7 +146,7 @@ static void check_epi_operands(int64_t epi, const optional<Tensor>& bias, const 
 }
 
 void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& bias, const optional<Tensor>& R,
-          int64_t epi, int64_t force) {
+          int64_t epi, int64_t force, bool bfrag) {
   check_bf16(A, "A");
   check_bf16(B, "B");
   check_dev(C, "C");
@@ -164,7 +165,7 @@ void gemm(const Tensor& A, const Tensor& B, Tensor& C, const optional<Tensor>& b
     TORCH_CHECK(R->numel() == (int64_t)M * N, "gemm: residual has wrong size");
   }
   gai_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr(bias), opt_ptr(R), M, N, K, ldc, (int)epi, f32 ? 1 : 0,
-           (int)force, cur_stream());
+           (int)force, cur_stream(), bfrag ? 1 : 0);
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -570,7 +571,7 @@ void geglu_interleaved(const Tensor& x, Tensor& y) {
 }
 
 void gemv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, int64_t epi,
-          const optional<Tensor>& out, const optional<Tensor>& res) {
+          const optional<Tensor>& out, const optional<Tensor>& res, bool frag) {
   check_bf16(x, "x");
   check_bf16(W, "W");
   TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1) && x.is_contiguous() && W.is_contiguous(),
@@ -595,12 +596,12 @@ void gemv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tens
     o = out->data_ptr();
   }
   gai_gemv(x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), M, N, K, (int)epi, o, r,
-           cur_stream());
+           cur_stream(), frag ? 1 : 0);
 }
 
 void gemv_rope_kv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, const Tensor& pos,
                   const Tensor& cos_sin, const Tensor& slots, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
-                  int64_t Hq, int64_t Hkv) {
+                  int64_t Hq, int64_t Hkv, bool frag) {
   check_bf16(x, "x");
   check_bf16(W, "W");
   check_i32(pos, "pos");
@@ -615,7 +616,7 @@ void gemv_rope_kv(const Tensor& x, const optional<Tensor>& gamma, double eps, co
   if (gamma) check_bf16(*gamma, "gamma");
   gai_gemv_rope_kv(x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), x.size(0), x.size(1),
                    pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(),
-                   k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv, cur_stream());
+                   k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv, cur_stream(), frag ? 1 : 0);
 }
 
 void custom_all_to_all(const Tensor& inp, Tensor& out, const std::vector<int64_t>& data_ptrs,
@@ -829,7 +830,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
+        pybind11::arg("R"), pybind11::arg("epi"), pybind11::arg("force"), pybind11::arg("bfrag") = false);
   m.def("gemm_fp8", &gemm_fp8);
   m.def("gemm_splitk", &gemm_splitk, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("R"), pybind11::arg("epi"), pybind11::arg("ws"), pybind11::arg("psw") = false);
@@ -870,8 +872,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ep_combine", &ep_combine);
   m.def("custom_all_to_all", &custom_all_to_all);
   m.def("gemm_qkv_partials", &gemm_qkv_partials);
-  m.def("gemv", &gemv);
-  m.def("gemv_rope_kv", &gemv_rope_kv);
+  m.def("gemv", &gemv, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("eps"), pybind11::arg("W"),
+        pybind11::arg("epi"), pybind11::arg("out"), pybind11::arg("res"), pybind11::arg("frag") = false);
+  m.def("gemv_rope_kv", &gemv_rope_kv, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("eps"),
+        pybind11::arg("W"), pybind11::arg("pos"), pybind11::arg("cos_sin"), pybind11::arg("slots"),
+        pybind11::arg("q_out"), pybind11::arg("k_cache"), pybind11::arg("v_cache"), pybind11::arg("Hq"),
+        pybind11::arg("Hkv"), pybind11::arg("frag") = false);
   m.def("embedding", &embedding);
   m.def("decode_advance", &decode_advance);
   m.def("pool", &pool);

@@ -19,15 +19,16 @@ void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, co
                        float k_scale, float v_scale, hipStream_t st);
 
 // gemm.hip  (epi: 0 none, 1 bias, 2 bias+gelu, 3 residual, 4 swiglu, 5 bias+residual, 6 bias+relu, 7 bias+quick-gelu;
-//            force: 0 auto, 1 skinny, 2 tiled 128x128, 3 large 256x256)
+//            force: 0 auto, 1 skinny, 2 tiled 128x128, 3 large 256x256; bfrag: B stored in MFMA fragment order,
+//            ops.shuffle_fragments - the one layout of the decode projection weights)
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-              int epi, int out_f32, int force, hipStream_t st);
+              int epi, int out_f32, int force, hipStream_t st, int bfrag = 0);
 
 // gemm.hip prefill QKV projection (M >= 1024, D = 128, bf16 KV) with (+ bias) -> RoPE -> q_out / paged K, V^T
 // caches fused into the GEMM epilogue (as gai_gemm + gai_rope_kv_write); returns 0 (nothing launched) otherwise
 int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
                              const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq,
-                             int Hkv, int D, int kv_fp8, hipStream_t st);
+                             int Hkv, int D, int kv_fp8, hipStream_t st, int bfrag = 0);
 
 // gemm_fp8.hip (force: 0 auto, 2 tiled 128x128, 3 large 256x256; OCP e4m3fn operands, per-row sa[M] x per-channel sb[N] scales; epi as gai_gemm + 7 bias+quick-gelu)
 void gai_gemm_fp8(const void* A, const void* B, const float* sa, const float* sb, void* C, const void* bias,
@@ -111,11 +112,12 @@ void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* off
                       int div = 1, int* a_pairs = nullptr);
 // gemv.hip: decode GEMV for 1..4 token rows with the RMSNorm staged in and the epilogue fused
 int gai_gemv_ok(int M, int N, int K, int normed);
+// wfrag: W stored in MFMA fragment order (ops.shuffle_fragments; N % 16 == 0, 32 for SwiGLU)
 void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
-              void* res, hipStream_t st);
+              void* res, hipStream_t st, int wfrag = 0);
 void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W, int M, int K, const int* pos,
                       const float* cos_sin, const int* slots, void* q_out, void* k_cache, void* v_cache, int Hq,
-                      int Hkv, hipStream_t st);
+                      int Hkv, hipStream_t st, int wfrag = 0);
 // expert parallelism (moe.hip): fixed-capacity send slabs and the weighted combine of the returned slabs
 void gai_ep_pack(const void* x, const int* ids, const int* offs, const int* a_pairs, int W, int C, int k, int D,
                  int ld, int e_local, void* send, int* send_eid, hipStream_t st);

@@ -34,20 +34,20 @@ bool gai_sk_workspace(hipStream_t st, size_t ws_bytes, size_t cnt_n, float** ws_
 }
 
 void gai_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-              int epi, int out_f32, int force, hipStream_t st) {
+              int epi, int out_f32, int force, hipStream_t st, int bfrag) {
   if (M == 0 || N == 0) return;
   static_assert(EPI_NONE == 0 && EPI_BIAS == 1 && EPI_BIAS_GELU == 2 && EPI_RESIDUAL == 3 && EPI_SWIGLU == 4 &&
                     EPI_BIAS_RESIDUAL == 5 && EPI_BIAS_RELU == 6 && EPI_BIAS_QUICKGELU == 7,
                 "gai_gemm_run<E> numbering");
   switch (epi) {
-    case 0: return gai_gemm_run0(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 1: return gai_gemm_run1(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 2: return gai_gemm_run2(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 3: return gai_gemm_run3(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 4: return gai_gemm_run4(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 5: return gai_gemm_run5(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 6: return gai_gemm_run6(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
-    case 7: return gai_gemm_run7(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st);
+    case 0: return gai_gemm_run0(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 1: return gai_gemm_run1(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 2: return gai_gemm_run2(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 3: return gai_gemm_run3(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 4: return gai_gemm_run4(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 5: return gai_gemm_run5(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 6: return gai_gemm_run6(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
+    case 7: return gai_gemm_run7(A, B, C, bias, R, M, N, K, ldc, out_f32, force, st, bfrag);
     default:
       gai_launch_error(__FILE__, __LINE__, "gemm: unknown epilogue");
   }
@@ -55,7 +55,7 @@ void gai_gemm(const void* A, const void* B, void* C, const void* bias, const voi
 
 int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, const int* pos, const float* cos_sin,
                              const int* slots, void* q_out, void* k_cache, void* v_cache, int M, int K, int Hq,
-                             int Hkv, int D, int kv_fp8, hipStream_t st) {
+                             int Hkv, int D, int kv_fp8, hipStream_t st, int bfrag) {
   const int N = (Hq + 2 * Hkv) * D;
   if (D != 128 || kv_fp8 || M < 1024 || K % 64 || K < 192 || (size_t)M * K * 2 >= (1ull << 31) ||
       (size_t)N * K * 2 >= (1ull << 31))
@@ -73,7 +73,7 @@ int gai_gemm_prefill_rope_kv(const void* A, const void* B, const void* bias, con
   rk.v_cache = (bf16*)v_cache;
   rk.Hq = Hq;
   rk.Hkv = Hkv;
-  launch_w4d<EPI_ROPE_KV, false>(A, B, nullptr, bias, nullptr, M, N, K, N, st, rk);
+  launch_w4d<EPI_ROPE_KV, false>(A, B, nullptr, bias, nullptr, M, N, K, N, st, rk, 0, bfrag);
   return 1;
 }
 #endif  // GAI_GEMM_KERNELS_ONLY

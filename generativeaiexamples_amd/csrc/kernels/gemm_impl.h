@@ -52,7 +52,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds) {
 template <int EPI, bool OUTF32>
 __global__ __launch_bounds__(256, 2) void gemm_tiled_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                             void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                            int K, int ldc) {
+                                                            int K, int ldc, int bfrag) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (A 16K + B 16K)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -66,15 +66,20 @@ __global__ __launch_bounds__(256, 2) void gemm_tiled_kernel(const bf16* __restri
   const int tm = first_m + pin % gsz, tn = pin / gsz;
   const int m0 = tm * TBM, n0 = tn * TBN;
 
-  // per-lane staging source offsets (4 glds per operand per wave per K tile)
+  // per-lane staging source offsets (4 glds per operand per wave per K tile). bfrag: B is stored in MFMA fragment
+  // order (ops.shuffle_fragments: [N/16][K/32][64 lanes][8]); load q of wave w is then the whole 1 KiB fragment
+  // (n-tile (4w + q) / 2, k-half q & 1) of the K tile, and the LDS image is fragment-ordered too
   size_t a_off[4], b_off[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = (wid * 4 + q) * 64 + lane;
     const int row = p >> 3, cl = p & 7, cg = cl ^ (row & 7);
     a_off[q] = (size_t)min(m0 + row, M - 1) * K + cg * 8;
-    b_off[q] = (size_t)min(n0 + row, N - 1) * K + cg * 8;
+    const int f = wid * 4 + q;
+    b_off[q] = bfrag ? ((size_t)min(n0 / 16 + (f >> 1), N / 16 - 1) * (K / 32) + (f & 1)) * 512 + lane * 8
+                     : (size_t)min(n0 + row, N - 1) * K + cg * 8;
   }
+  const size_t bk = bfrag ? 1024 : TBK;  // B elements per K tile
   auto stage = [&](int kt, int buf) {
     char* sa = smem + buf * 2 * kTileBytes;
     char* sb = sa + kTileBytes;
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tiled_kernel(const bf16* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       glds16(A + a_off[q] + k0, sa + (wid * 4 + q) * 1024);
-      glds16(B + b_off[q] + k0, sb + (wid * 4 + q) * 1024);
+      glds16(B + b_off[q] + kt * bk, sb + (wid * 4 + q) * 1024);
     }
   };
 
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tiled_kernel(const bf16* __restri
       const int ra = wm * 64 + 16 * i + (lane & 15);
       const int rb = wn * 64 + 16 * i + (lane & 15);
       a_rd[i][s] = ra * 128 + ((c ^ (ra & 7)) << 4);
-      b_rd[i][s] = rb * 128 + ((c ^ (rb & 7)) << 4);
+      b_rd[i][s] = bfrag ? ((wn * 4 + i) * 2 + s) * 1024 + lane * 16 : rb * 128 + ((c ^ (rb & 7)) << 4);
     }
 
   const int nk = K / TBK;
@@ -555,7 +560,7 @@ constexpr int kDblHalf = 256 * 64 * 2;
 template <int EPI, bool OUTF32, int VAR = 0, int MI = 8>
 __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc, RopeKvArgs rk) {
+                                                          int K, int ldc, RopeKvArgs rk, int bfrag) {
   static_assert(MI == 8 || MI == 6, "tile heights 256 / 192");
   constexpr int BM = 32 * MI;       // tile rows
   constexpr int NT = 8 * MI;        // MFMAs per phase
@@ -581,13 +586,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
   // load j of wave w: A rows (MI w + j) * 8 + lane / 8 (j < MI), B rows (8w + j) * 8 + lane / 8 (j < 8), 16-B
   // chunk (lane & 7) of the LDS row <- global chunk (lane & 7) ^ f(row); byte offsets (rows clamped to the
-  // matrix: partial tiles)
+  // matrix: partial tiles). bfrag (B in MFMA fragment order, ops.shuffle_fragments): B load j of wave w is the whole
+  // 1 KiB fragment (n-tile 4w + j / 2, k32 half j & 1) of the double, landing fragment-ordered in LDS
+  const int bks = bfrag ? 2048 : 128;  // B bytes per k-double step
   auto offsets = [&](int m0, int n0, int* oa, int* ob) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = (wid * 8 + j) * 8 + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
-      ob[j] = min(n0 + row, N - 1) * K * 2 + gc * 16;
+      ob[j] = bfrag ? (min(n0 / 16 + wid * 4 + (j >> 1), N / 16 - 1) * (K / 32) + (j & 1)) * 1024 + lane * 16
+                    : min(n0 + row, N - 1) * K * 2 + gc * 16;
     }
 #pragma unroll
     for (int j = 0; j < MI; ++j) {
@@ -601,8 +609,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
   const int fr = (lane & 15) >> 1;
   const int a_rd0 = (wm * 16 * MI + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
   const int a_rd1 = (wm * 16 * MI + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
-  const int b_rd0 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
-  const int b_rd1 = kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  const int b_rd0 = kDblHalf + (bfrag ? wn * 16384 + lane * 16 : (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4));
+  const int b_rd1 = bfrag ? b_rd0 + 1024 : kDblHalf + (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -619,7 +627,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
     char* da = smem + wslot * kDblBytes + wid * MI * 1024;
     char* db = smem + wslot * kDblBytes + kDblHalf + wid * 8192;
     const int ar = ODD ? a_rd0 : a_rd1, br = ODD ? b_rd0 : b_rd1;
-    const int soff = kd * 128;
+    const int soff = kd * 128, soffb = kd * bks;
     for_each_const<NT>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       constexpr int i = t >> 3, j = t & 7;
@@ -636,7 +644,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
       if constexpr (ODD && LD && gl < MI)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(da + gl * 1024), 16, oa[gl], soff, 0, 0);
       else if constexpr (ODD && LD)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(db + (gl - MI) * 1024), 16, ob[gl - MI], soff, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(db + (gl - MI) * 1024), 16, ob[gl - MI], soffb, 0, 0);
       if constexpr (RD && t % 2 == 0 && g < NL && g < MI)
         naf[g] = *reinterpret_cast<const bf16x8*>(sr + ar + g * 2048);
       else if constexpr (RD && t % 2 == 0 && g < NL)
@@ -670,7 +678,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4d_kernel(const bf16* __restrict
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, GAI_LDS(dst + (wid * MI + j) * 1024), 16, ca[j], dd * 128, 0, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(dst + kDblHalf + (wid * 8 + j) * 1024), 16, cb[j], dd * 128, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, GAI_LDS(dst + kDblHalf + (wid * 8 + j) * 1024), 16, cb[j], dd * bks, 0, 0);
   }
   if constexpr (MI == 8)
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double 0 landed
@@ -884,8 +892,7 @@ constexpr int kSkQuad = 128 * 128;  // fp32 of one wave's quadrant partial
 template <int EPI, bool OUTF32, int WALK = 0>
 __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc, float* ws = nullptr, int* cnt = nullptr,
-                                                          int S = 1) {
+                                                          int K, int ldc, float* ws, int* cnt, int S, int bfrag) {
   constexpr bool SK = WALK == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 5 parts x 32 KiB
   const int tid = threadIdx.x, lane = tid & 63;
@@ -932,21 +939,24 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
   };
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
+  // bfrag: B in MFMA fragment order (as gemm_w4d_kernel): B load j of wave w = fragment (n-tile 4w + j / 2, half j & 1)
+  const int bks = bfrag ? 2048 : 128;  // B bytes per k-double step
   auto offsets = [&](int m0, int n0, int* oa, int* ob) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = (wid * 8 + j) * 8 + (lane >> 3);
       const int gc = (lane & 7) ^ ((row >> 1) & 7);
       oa[j] = min(m0 + row, M - 1) * K * 2 + gc * 16;
-      ob[j] = min(n0 + row, N - 1) * K * 2 + gc * 16;
+      ob[j] = bfrag ? (min(n0 / 16 + wid * 4 + (j >> 1), N / 16 - 1) * (K / 32) + (j & 1)) * 1024 + lane * 16
+                    : min(n0 + row, N - 1) * K * 2 + gc * 16;
     }
   };
   const int wm = wid >> 1, wn = wid & 1;
   const int fr = (lane & 15) >> 1;
   const int a_rd0 = (wm * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
   const int a_rd1 = (wm * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
-  const int b_rd0 = (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
-  const int b_rd1 = (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
+  const int b_rd0 = bfrag ? wn * 16384 + lane * 16 : (wn * 128 + (lane & 15)) * 128 + (((lane >> 4) ^ fr) << 4);
+  const int b_rd1 = bfrag ? b_rd0 + 1024 : (wn * 128 + (lane & 15)) * 128 + (((4 + (lane >> 4)) ^ fr) << 4);
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -961,7 +971,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
     const char* pa = smem + sa * kPart + (ODD ? a_rd0 : a_rd1);
     const char* pb = smem + sb * kPart + (ODD ? b_rd0 : b_rd1);
     char* d = smem + sw * kPart + wid * 8192;
-    const int soff = kd * 128;
+    const int soff = kd * (ODD ? bks : 128);
     for_each_const<64>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       constexpr int i = t >> 3, j = t & 7;
@@ -1003,7 +1013,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(q & 1 ? rb : ra, GAI_LDS(dst + j * 1024), 16, q & 1 ? cb[j] : ca[j],
-                                               (kb + (q >> 1)) * 128, 0, 0);
+                                               (kb + (q >> 1)) * (q & 1 ? bks : 128), 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // double kb landed
   barrier();
@@ -1151,7 +1161,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4r_kernel(const bf16* __restrict
 template <int MT, int NF, int EPI, bool OUTF32>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                           void* C, const bf16* bias, const bf16* R, int M, int N,
-                                                          int K, int ldc) {
+                                                          int K, int ldc, int bfrag) {
   constexpr int NB = 16 * NF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* part = reinterpret_cast<float*>(smem);  // [8 waves][MT][NF][4][64 lanes]
@@ -1161,9 +1171,13 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
   const int KS = K / 8;
   const int kbeg = wid * KS, kend = kbeg + KS;
 
+  // bfrag: B in MFMA fragment order, the lane's 16 B of fragment (n-tile, k32 step) = 1 KiB per step
   const bf16* bp[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) bp[f] = B + (size_t)min(n0 + 16 * f + (lane & 15), N - 1) * K + 8 * (lane >> 4);
+  for (int f = 0; f < NF; ++f)
+    bp[f] = bfrag ? B + (size_t)min(n0 / 16 + f, N / 16 - 1) * (K / 32) * 512 + 8 * lane
+                  : B + (size_t)min(n0 + 16 * f + (lane & 15), N - 1) * K + 8 * (lane >> 4);
+  const int kmul = bfrag ? 16 : 1;
   const bf16* ap[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) ap[i] = A + (size_t)min(16 * i + (lane & 15), M - 1) * K + 8 * (lane >> 4);
@@ -1178,7 +1192,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
   for (int k = kbeg; k < kend; k += 32) {
     bf16x8 bfr[NF], af[MT];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) bfr[f] = load8(bp[f] + k);
+    for (int f = 0; f < NF; ++f) bfr[f] = load8(bp[f] + (size_t)k * kmul);
 #pragma unroll
     for (int i = 0; i < MT; ++i) af[i] = load8(ap[i] + k);
 #pragma unroll
@@ -1232,7 +1246,7 @@ void set_max_lds(F* f) {
 
 template <int EPI, bool OUTF32>
 void launch_tiled(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                  hipStream_t st) {
+                  hipStream_t st, int bfrag) {
   const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
   static bool once = false;
   if (!once) {
@@ -1240,7 +1254,7 @@ void launch_tiled(const void* A, const void* B, void* C, const void* bias, const
     once = true;
   }
   gemm_tiled_kernel<EPI, OUTF32><<<tiles, 256, 4 * kTileBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                      (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
+                                                                      (const bf16*)bias, (const bf16*)R, M, N, K, ldc, bfrag);
   GAI_LAUNCH_CHECK();
 }
 
@@ -1282,7 +1296,7 @@ int w4d_rows(int M, int N, int ncu) {
 
 template <int EPI, bool OUTF32>
 void launch_w4d(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st, RopeKvArgs rk = {}, int rows = 0) {
+                hipStream_t st, RopeKvArgs rk, int rows, int bfrag) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1298,16 +1312,17 @@ void launch_w4d(const void* A, const void* B, void* C, const void* bias, const v
   if (bm == 192)
     gemm_w4d_kernel<EPI, OUTF32, 0, 6><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
                                                                         (const bf16*)bias, (const bf16*)R, M, N, K,
-                                                                        ldc, rk);
+                                                                        ldc, rk, bfrag);
   else
     gemm_w4d_kernel<EPI, OUTF32><<<grid, 256, 2 * kDblBytes, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                   (const bf16*)bias, (const bf16*)R, M, N, K, ldc, rk);
+                                                                   (const bf16*)bias, (const bf16*)R, M, N, K, ldc, rk,
+                                                                   bfrag);
   GAI_LAUNCH_CHECK();
 }
 
 template <int EPI, bool OUTF32>
 void launch_w4r(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st) {
+                hipStream_t st, int bfrag) {
   const int tiles = ((M + LBM - 1) / LBM) * ((N + LBN - 1) / LBN);
   static int ncu = 0;
   if (!ncu) {
@@ -1319,7 +1334,7 @@ void launch_w4r(const void* A, const void* B, void* C, const void* bias, const v
   }
   const int grid = tiles <= ncu ? tiles : (ncu & ~7);
   gemm_w4r_kernel<EPI, OUTF32><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C, (const bf16*)bias,
-                                                             (const bf16*)R, M, N, K, ldc);
+                                                             (const bf16*)R, M, N, K, ldc, nullptr, nullptr, 1, bfrag);
   GAI_LAUNCH_CHECK();
 }
 
@@ -1367,7 +1382,7 @@ bool ring_auto(int M, int N, int K) { return M >= 256 && (2 * ring_tiles(M, N) >
 
 template <int EPI, bool OUTF32>
 bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st) {
+                hipStream_t st, int bfrag) {
   if (K % 128) return false;
   static bool once = false;
   if (!once) {
@@ -1383,7 +1398,7 @@ bool launch_w4s(const void* A, const void* B, void* C, const void* bias, const v
   if (!sk_workspace(st, (size_t)grid * 2 * 4 * kSkQuad * sizeof(float), (size_t)tiles * 4, w)) return false;
   gemm_w4r_kernel<EPI, OUTF32, 1><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
                                                                    (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
-                                                                   w.ws, w.cnt);
+                                                                   w.ws, w.cnt, 1, bfrag);
   GAI_LAUNCH_CHECK();
   return true;
 }
@@ -1409,7 +1424,7 @@ int split_parts(int M, int N, int K) {
 
 template <int EPI, bool OUTF32>
 bool launch_w4x(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int ldc,
-                hipStream_t st, int S) {
+                hipStream_t st, int S, int bfrag) {
   if (K % 128 || S < 2 || S > K / 128) return false;
   static bool once = false;
   if (!once) {
@@ -1425,14 +1440,14 @@ bool launch_w4x(const void* A, const void* B, void* C, const void* bias, const v
   if (!sk_workspace(st, (size_t)items * 4 * kSkQuad * sizeof(float), (size_t)tiles * 4, w)) return false;
   gemm_w4r_kernel<EPI, OUTF32, 2><<<grid, 256, 5 * kPart, st>>>((const bf16*)A, (const bf16*)B, C,
                                                                 (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
-                                                                w.ws, w.cnt, S);
+                                                                w.ws, w.cnt, S, bfrag);
   GAI_LAUNCH_CHECK();
   return true;
 }
 
 template <int MT, int NF, int EPI, bool OUTF32>
 void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                      int ldc, hipStream_t st) {
+                      int ldc, hipStream_t st, int bfrag) {
   const int nblk = (N + 16 * NF - 1) / (16 * NF);
   const size_t lds = (size_t)8 * MT * NF * 4 * 64 * sizeof(float);
   static bool once = false;
@@ -1441,43 +1456,50 @@ void launch_skinny_mt(const void* A, const void* B, void* C, const void* bias, c
     once = true;
   }
   gemm_skinny_kernel<MT, NF, EPI, OUTF32><<<nblk, 512, lds, st>>>((const bf16*)A, (const bf16*)B, C,
-                                                                  (const bf16*)bias, (const bf16*)R, M, N, K, ldc);
+                                                                  (const bf16*)bias, (const bf16*)R, M, N, K, ldc,
+                                                                  bfrag);
   GAI_LAUNCH_CHECK();
 }
 
 template <int NF, int EPI, bool OUTF32>
 void launch_skinny_nf(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                      int ldc, hipStream_t st) {
-  if (M <= 16) return launch_skinny_mt<1, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-  if (M <= 32) return launch_skinny_mt<2, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-  if (M <= 64) return launch_skinny_mt<4, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-  return launch_skinny_mt<8, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+                      int ldc, hipStream_t st, int bfrag) {
+  if (M <= 16) return launch_skinny_mt<1, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
+  if (M <= 32) return launch_skinny_mt<2, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
+  if (M <= 64) return launch_skinny_mt<4, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
+  return launch_skinny_mt<8, NF, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
 }
 
 template <int EPI, bool OUTF32>
 void launch_gemm(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K,
-                 int ldc, int force, hipStream_t st) {
+                 int ldc, int force, hipStream_t st, int bfrag) {
+  // bfrag: B [N, K] is stored in MFMA fragment order (ops.shuffle_fragments) - the one weight layout of the
+  // decode projections, read by every kernel below except the w4p fallback for >= 2 GiB operands
+  if (bfrag && (N % 16 || K % 64 || (size_t)N * K * 2 >= (1ull << 31)))
+    gai_launch_error(__FILE__, __LINE__, "gemm: a fragment-ordered B needs N%16==0, K%64==0 and < 2 GiB");
   const bool skinny_ok = (K % 256) == 0 && M <= 128;
   const bool use_skinny = force == 1 || (force == 0 && skinny_ok);
   if (use_skinny) {
     if (!skinny_ok) gai_launch_error(__FILE__, __LINE__, "gemm_skinny: needs M<=128 and K%256==0");
     // two 16-row fragments per wave when there are enough column blocks to fill the chip
     if (EPI != EPI_SWIGLU && N / 32 >= 512)
-      return launch_skinny_nf<2, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if (EPI == EPI_SWIGLU) return launch_skinny_nf<2, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    return launch_skinny_nf<1, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+      return launch_skinny_nf<2, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
+    if (EPI == EPI_SWIGLU) return launch_skinny_nf<2, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
+    return launch_skinny_nf<1, EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
   }
   if (K % TBK) gai_launch_error(__FILE__, __LINE__, "gemm_tiled: K must be a multiple of 64");
   // ring kernel: 16-B epilogue stores need N % 16 == 0; the 2-unit unrolled ring needs K % 64 == 0, K >= 160
   const bool ring_ok = N % 16 == 0 && K % 64 == 0 && K / 32 >= RNS && ldc % 8 == 0;
   if (force >= 8 || (force == 0 && N >= 256 && ring_ok && ring_auto(M, N, K))) {
     if (!ring_ok) gai_launch_error(__FILE__, __LINE__, "gemm_ring: needs N%16==0, K%64==0, K>=192, ldc%8==0");
-    if (force == 8) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31))  // 32-bit buffer offsets
-      return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
-    if ((force == 11 || (force == 0 && sk_auto(M, N, K))) && launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st))
+    const bool big = (size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31);  // 32-bit buffer offsets
+    if (!bfrag && (force == 8 || big)) return launch_w4p<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+    if (big) return launch_tiled<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);  // (64-bit addressing)
+    if ((force == 11 || (force == 0 && sk_auto(M, N, K))) &&
+        launch_w4s<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag))
       return;
-    if (force == 12 && launch_w4x<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, std::max(2, split_parts(M, N, K))))
+    if (force == 12 &&
+        launch_w4x<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, std::max(2, split_parts(M, N, K)), bfrag))
       return;
     // the part ring (its operands get 2-3 phases of latency cover) with the operands streamed from HBM as in the
     // model - every layer's weights are read once per forward, past the 256 MB Infinity Cache: it is the fastest
@@ -1488,12 +1510,12 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
     // the wide gate_up (N >= 16384, 1120 tiles) of a single 2406-token prompt runs 430.6 us per layer on the double-slot
     // walk vs 445.4 on the part ring.
     if (force == 10 || (force == 0 && !(M < 8192 && N >= 16384)))
-      return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+      return launch_w4r<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
     // force 9 / 13: the double-slot walk with 256- / 192-row tiles (tests, A/B); auto: w4d_rows
     return launch_w4d<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, RopeKvArgs{},
-                                   force == 9 ? 256 : force == 13 ? 192 : 0);
+                                   force == 9 ? 256 : force == 13 ? 192 : 0, bfrag);
   }
-  launch_tiled<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st);
+  launch_tiled<EPI, OUTF32>(A, B, C, bias, R, M, N, K, ldc, st, bfrag);
 }
 
 }  // namespace
@@ -1501,13 +1523,13 @@ void launch_gemm(const void* A, const void* B, void* C, const void* bias, const 
 // per-epilogue entry points (gemm_epi_*.hip), called by gai_gemm
 #define GAI_GEMM_RUN_ARGS                                                                                     \
   const void *A, const void *B, void *C, const void *bias, const void *R, int M, int N, int K, int ldc, int out_f32, \
-      int force, hipStream_t st
+      int force, hipStream_t st, int bfrag
 #define GAI_GEMM_RUN(E)                                                                     \
   void gai_gemm_run##E(GAI_GEMM_RUN_ARGS) {                                                 \
     if (out_f32)                                                                            \
-      launch_gemm<E, true>(A, B, C, bias, R, M, N, K, ldc, force, st);                      \
+      launch_gemm<E, true>(A, B, C, bias, R, M, N, K, ldc, force, st, bfrag);               \
     else                                                                                    \
-      launch_gemm<E, false>(A, B, C, bias, R, M, N, K, ldc, force, st);                     \
+      launch_gemm<E, false>(A, B, C, bias, R, M, N, K, ldc, force, st, bfrag);              \
   }
 void gai_gemm_run0(GAI_GEMM_RUN_ARGS);
 void gai_gemm_run1(GAI_GEMM_RUN_ARGS);

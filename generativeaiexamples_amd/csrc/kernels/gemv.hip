@@ -58,137 +58,10 @@ __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float ac
   return acc;
 }
 
-template <int MR, int EPI, int NW = kGvWaves>
-__global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
-  constexpr int kThr = 64 * NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
-  __shared__ float red[NW][MR];
-  __shared__ float inv_s[MR];
-  bf16* xs = reinterpret_cast<bf16*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int K = a.K, nch = K / 8;
-
-  // ---- this wave's row pair; its first weight group is issued BEFORE the activation staging, so the HBM
-  // latency of the weight stream overlaps the staging (and the RMSNorm reduction) instead of following it
-  const int p = blockIdx.x * NW + wid;
-  const int npairs = a.N / 2;
-  const bool live = p < npairs;
-  int r0, r1;
-  if (EPI == GV_SWIGLU) {  // rows interleaved per 16: [gate16 | up16]; output column p
-    r0 = 32 * (p >> 4) + (p & 15);
-    r1 = r0 + 16;
-  } else if (EPI == GV_ROPE) {  // head p / 64, rotate-half pair (i, i + 64)
-    r0 = 128 * (p >> 6) + (p & 63);
-    r1 = r0 + 64;
-  } else {
-    r0 = 2 * p;
-    r1 = r0 + 1;
-  }
-  const bf16* w0 = a.W + (size_t)(live ? r0 : 0) * K + 8 * lane;
-  const bf16* w1 = a.W + (size_t)(live ? r1 : 0) * K + 8 * lane;
-  const int ngroups = K / (kPiece * kG);  // host: K % 2048 == 0
-  bf16x8 cur0[kG], cur1[kG], nxt0[kG], nxt1[kG];
-  auto load_group = [&](int g, bf16x8(&b0)[kG], bf16x8(&b1)[kG]) {
-#pragma unroll
-    for (int c = 0; c < kG; ++c) {
-      const int off = (g * kG + c) * kPiece;
-      b0[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + off));
-      b1[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + off));
-    }
-  };
-  if (live) load_group(0, cur0, cur1);
-
-  // ---- stage the activation rows (normalised when gamma is given); the host keeps K <= 8192 for the norm form
-  if (a.gamma != nullptr) {
-    constexpr int kMaxC = (8192 + 8 * kThr - 1) / (8 * kThr);  // chunks per thread per row: K <= 8192
-    bf16x8 v[MR][kMaxC];
-    float ss[MR];
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      ss[m] = 0.f;
-#pragma unroll
-      for (int c = 0; c < kMaxC; ++c) {
-        const int ch = c * kThr + tid;
-        if (ch < nch) {
-          v[m][c] = load8(a.x + (size_t)m * K + 8 * ch);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ss[m] += (float)v[m][c][e] * (float)v[m][c][e];
-        }
-      }
-      ss[m] = wave_sum(ss[m]);
-      if (lane == 0) red[wid][m] = ss[m];
-    }
-    __syncthreads();
-    if (tid < MR) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) t += red[w][tid];
-      inv_s[tid] = rsqrtf(t / K + a.eps);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      const float inv = inv_s[m];
-#pragma unroll
-      for (int c = 0; c < kMaxC; ++c) {
-        const int ch = c * kThr + tid;
-        if (ch < nch) {
-          const bf16x8 g = load8(a.gamma + 8 * ch);
-          bf16x8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[m][c][e] * inv * (float)g[e]);
-          *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * ch) = o;
-        }
-      }
-    }
-  } else {
-    for (int ch = tid; ch < MR * nch; ch += kThr) {
-      const int m = ch / nch, c = ch % nch;
-      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * c) = load8(a.x + (size_t)m * K + 8 * c);
-    }
-  }
-  __syncthreads();
-  if (!live) return;  // no barrier below
-
-  float acc[MR][2];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = 0.f;
-  auto compute_group = [&](int g, const bf16x8(&b0)[kG], const bf16x8(&b1)[kG]) {
-#pragma unroll
-    for (int c = 0; c < kG; ++c) {
-      const int k0 = (g * kG + c) * kPiece + 8 * lane;
-#pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
-        acc[m][0] = dot8(xv, b0[c], acc[m][0]);
-        acc[m][1] = dot8(xv, b1[c], acc[m][1]);
-      }
-    }
-  };
-  int g = 0;  // group 0 is in flight since the kernel start
-  for (; g + 2 <= ngroups; g += 2) {
-    load_group(g + 1, nxt0, nxt1);
-    compute_group(g, cur0, cur1);
-    if (g + 2 < ngroups) load_group(g + 2, cur0, cur1);
-    compute_group(g + 1, nxt0, nxt1);
-  }
-  if (g < ngroups) compute_group(g, cur0, cur1);
-
-#pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    acc[m][0] = wave_sum(acc[m][0]);
-    acc[m][1] = wave_sum(acc[m][1]);
-  }
-  if (lane >= MR) return;
-  // lane m finishes token row m
-  float v0 = acc[0][0], v1 = acc[0][1];
-#pragma unroll
-  for (int m = 1; m < MR; ++m)
-    if (lane == m) {
-      v0 = acc[m][0];
-      v1 = acc[m][1];
-    }
-  const int m = lane;
+// The epilogue of row pair p (rows r0, r1: their fp32 dot products v0, v1) for token row m; shared by the row-pair and
+// the fragment-ordered kernels.
+template <int EPI>
+__device__ __forceinline__ void gv_epilogue(const GemvArgs& a, int m, int p, int r0, int r1, float v0, float v1) {
   const int N = a.N;
   if constexpr (EPI == GV_PLAIN) {
     bf16* o = reinterpret_cast<bf16*>(a.out) + (size_t)m * N;
@@ -233,6 +106,258 @@ __global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
       vd[(size_t)i * kBS] = (bf16)x1;
       vd[(size_t)(i + D / 2) * kBS] = (bf16)x2;
     }
+  }
+}
+
+// Stage the MR activation rows in LDS (xs, [MR][K] bf16), normalised (x_hat * gamma rounded to bf16 exactly as the norm
+// kernel does) when a.gamma is given; red [NW][MR] / inv_s [MR] are the workgroup's reduction scratch. No trailing barrier.
+template <int MR, int NW>
+__device__ __forceinline__ void gv_stage(const GemvArgs& a, bf16* xs, float* red, float* inv_s) {
+  constexpr int kThr = 64 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int K = a.K, nch = K / 8;
+  // the host keeps K <= 8192 for the norm form
+  if (a.gamma != nullptr) {
+    constexpr int kMaxC = (8192 + 8 * kThr - 1) / (8 * kThr);  // chunks per thread per row: K <= 8192
+    bf16x8 v[MR][kMaxC];
+    float ss[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      ss[m] = 0.f;
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const int ch = c * kThr + tid;
+        if (ch < nch) {
+          v[m][c] = load8(a.x + (size_t)m * K + 8 * ch);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss[m] += (float)v[m][c][e] * (float)v[m][c][e];
+        }
+      }
+      ss[m] = wave_sum(ss[m]);
+      if (lane == 0) red[wid * MR + m] = ss[m];
+    }
+    __syncthreads();
+    if (tid < MR) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[w * MR + tid];
+      inv_s[tid] = rsqrtf(t / K + a.eps);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const float inv = inv_s[m];
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const int ch = c * kThr + tid;
+        if (ch < nch) {
+          const bf16x8 g = load8(a.gamma + 8 * ch);
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[m][c][e] * inv * (float)g[e]);
+          *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * ch) = o;
+        }
+      }
+    }
+  } else {
+    for (int ch = tid; ch < MR * nch; ch += kThr) {
+      const int m = ch / nch, c = ch % nch;
+      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * c) = load8(a.x + (size_t)m * K + 8 * c);
+    }
+  }
+}
+
+template <int MR, int EPI, int NW = kGvWaves>
+__global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
+  constexpr int kThr = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
+  __shared__ float red[NW][MR];
+  __shared__ float inv_s[MR];
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int K = a.K, nch = K / 8;
+
+  // ---- this wave's row pair; its first weight group is issued BEFORE the activation staging, so the HBM
+  // latency of the weight stream overlaps the staging (and the RMSNorm reduction) instead of following it
+  const int p = blockIdx.x * NW + wid;
+  const int npairs = a.N / 2;
+  const bool live = p < npairs;
+  int r0, r1;
+  if (EPI == GV_SWIGLU) {  // rows interleaved per 16: [gate16 | up16]; output column p
+    r0 = 32 * (p >> 4) + (p & 15);
+    r1 = r0 + 16;
+  } else if (EPI == GV_ROPE) {  // head p / 64, rotate-half pair (i, i + 64)
+    r0 = 128 * (p >> 6) + (p & 63);
+    r1 = r0 + 64;
+  } else {
+    r0 = 2 * p;
+    r1 = r0 + 1;
+  }
+  const bf16* w0 = a.W + (size_t)(live ? r0 : 0) * K + 8 * lane;
+  const bf16* w1 = a.W + (size_t)(live ? r1 : 0) * K + 8 * lane;
+  const int ngroups = K / (kPiece * kG);  // host: K % 2048 == 0
+  bf16x8 cur0[kG], cur1[kG], nxt0[kG], nxt1[kG];
+  auto load_group = [&](int g, bf16x8(&b0)[kG], bf16x8(&b1)[kG]) {
+#pragma unroll
+    for (int c = 0; c < kG; ++c) {
+      const int off = (g * kG + c) * kPiece;
+      b0[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + off));
+      b1[c] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + off));
+    }
+  };
+  if (live) load_group(0, cur0, cur1);
+
+  gv_stage<MR, NW>(a, xs, &red[0][0], inv_s);
+  __syncthreads();
+  if (!live) return;  // no barrier below
+
+  float acc[MR][2];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = 0.f;
+  auto compute_group = [&](int g, const bf16x8(&b0)[kG], const bf16x8(&b1)[kG]) {
+#pragma unroll
+    for (int c = 0; c < kG; ++c) {
+      const int k0 = (g * kG + c) * kPiece + 8 * lane;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
+        acc[m][0] = dot8(xv, b0[c], acc[m][0]);
+        acc[m][1] = dot8(xv, b1[c], acc[m][1]);
+      }
+    }
+  };
+  int g = 0;  // group 0 is in flight since the kernel start
+  for (; g + 2 <= ngroups; g += 2) {
+    load_group(g + 1, nxt0, nxt1);
+    compute_group(g, cur0, cur1);
+    if (g + 2 < ngroups) load_group(g + 2, cur0, cur1);
+    compute_group(g + 1, nxt0, nxt1);
+  }
+  if (g < ngroups) compute_group(g, cur0, cur1);
+
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    acc[m][0] = wave_sum(acc[m][0]);
+    acc[m][1] = wave_sum(acc[m][1]);
+  }
+  if (lane >= MR) return;
+  // lane m finishes token row m
+  float v0 = acc[0][0], v1 = acc[0][1];
+#pragma unroll
+  for (int m = 1; m < MR; ++m)
+    if (lane == m) {
+      v0 = acc[m][0];
+      v1 = acc[m][1];
+    }
+  gv_epilogue<EPI>(a, lane, p, r0, r1, v0, v1);
+}
+
+// Fragment-ordered weights (ops.shuffle_fragments: [N/16][K/32][64 lanes][8], the one layout of the decode
+// projections): a 16-row column of W is K/32 contiguous 1 KiB MFMA fragments, lane l of fragment kt holding row l & 15,
+// k 32 kt + 8 (l >> 4) .. + 8. A workgroup owns C whole columns - one for the plain / fp32 / residual epilogues, the
+// (gate, up) pair 2b, 2b + 1 for SwiGLU, the rotate-half pair c, c + 4 of one head for RoPE - and its NW waves split K:
+// wave w streams fragments [w KF / NW, (w + 1) KF / NW) of each column, kG per column in flight ahead of the
+// arithmetic (whole 1 KiB fragments, non-temporal), dotting each lane's 8 weights with the staged activation chunk.
+// The 4 lanes of a row (l, l + 16, l + 32, l + 48) reduce by cross-lane shuffles, the NW waves through LDS, and the
+// 16 C row results per token row leave through the row-pair epilogue gv_epilogue.
+template <int EPI>
+constexpr int gv_frag_cols() { return (EPI == GV_SWIGLU || EPI == GV_ROPE) ? 2 : 1; }
+
+template <int MR, int EPI, int NW>
+__global__ __launch_bounds__(64 * NW) void gemv_frag_kernel(GemvArgs a) {
+  constexpr int C = gv_frag_cols<EPI>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
+  __shared__ float red[NW][MR];
+  __shared__ float inv_s[MR];
+  __shared__ float part[NW][MR][C][16];
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int K = a.K, KF = K / 32;
+  const int b = blockIdx.x;
+  int col[C];
+  if constexpr (EPI == GV_ROPE) {
+    col[0] = 8 * (b >> 2) + (b & 3);
+    col[C - 1] = col[0] + 4;
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) col[c] = C * b + c;
+  }
+  const int nf = KF / NW, f0 = wid * nf;  // host: KF % (NW kG) == 0
+  const bf16* wp[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) wp[c] = a.W + ((size_t)col[c] * KF + f0) * 512 + 8 * lane;
+  bf16x8 cur[C][kG], nxt[C][kG];
+  auto load_group = [&](int g, bf16x8(&bq)[C][kG]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int j = 0; j < kG; ++j)
+        bq[c][j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[c] + (size_t)(g * kG + j) * 512));
+  };
+  load_group(0, cur);  // in flight during the activation staging
+  gv_stage<MR, NW>(a, xs, &red[0][0], inv_s);
+  __syncthreads();
+
+  float acc[MR][C];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[m][c] = 0.f;
+  const int kl = 8 * (lane >> 4);  // the lane's k offset inside a fragment
+  auto compute_group = [&](int g, const bf16x8(&bq)[C][kG]) {
+#pragma unroll
+    for (int j = 0; j < kG; ++j) {
+      const int k0 = (f0 + g * kG + j) * 32 + kl;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[m][c] = dot8(xv, bq[c][j], acc[m][c]);
+      }
+    }
+  };
+  const int ngroups = nf / kG;
+  int g = 0;
+  for (; g + 2 <= ngroups; g += 2) {
+    load_group(g + 1, nxt);
+    compute_group(g, cur);
+    if (g + 2 < ngroups) load_group(g + 2, cur);
+    compute_group(g + 1, nxt);
+  }
+  if (g < ngroups) compute_group(g, cur);
+
+  // lanes l, l + 16, l + 32, l + 48 hold row l & 15's partials
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float v = acc[m][c];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) part[wid][m][c][lane] = v;
+    }
+  __syncthreads();
+  // row pairs of this workgroup: 8 per column (rows 2i, 2i + 1) or 16 (SwiGLU / RoPE: row i of each column)
+  constexpr int NP = C == 1 ? 8 : 16;
+  for (int e = tid; e < MR * NP; e += 64 * NW) {
+    const int m = e / NP, i = e % NP;
+    const int ra = C == 1 ? 2 * i : i, rb = C == 1 ? 2 * i + 1 : i;  // rows inside columns ca / cb
+    const int ca = 0, cb = C - 1;
+    float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      v0 += part[w][m][ca][ra];
+      v1 += part[w][m][cb][rb];
+    }
+    const int r0 = 16 * col[ca] + ra, r1 = 16 * col[cb] + rb;
+    int p;
+    if constexpr (EPI == GV_SWIGLU)
+      p = 16 * b + i;  // output column: gate row r0 = 32 b + i
+    else if constexpr (EPI == GV_ROPE)
+      p = 64 * (r0 >> 7) + (r0 & 63);  // head r0 / 128, dim r0 % 128 (< 64)
+    else
+      p = r0 >> 1;
+    gv_epilogue<EPI>(a, m, p, r0, r1, v0, v1);
   }
 }
 
@@ -283,8 +408,60 @@ void gemv_launch_nw(const GemvArgs& a, hipStream_t st) {
   gai_launch_error(__FILE__, __LINE__, "gemv: 1 <= M <= 4");
 }
 
+// Fragment-ordered launch: N / (16 C) workgroups; 16 waves when that grid leaves CUs without a workgroup (Llama-3-8B
+// QKV + RoPE: 192 column pairs), else 8. GAI_GEMV_FRAG_WAVES = 4 / 8 / 16 forces one (sweeps).
+constexpr int kGvFragStatic = 10 * 1024;  // bound on the frag kernel's static LDS (part[16][4][2][16] + red)
+constexpr int kGvFragMaxDyn = 160 * 1024 - kGvFragStatic;
+
+template <int EPI, int NW>
+void gemv_frag_launch_nw(const GemvArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)a.M * a.K * sizeof(bf16);
+  const int grid = a.N / (16 * gv_frag_cols<EPI>());
+#define GAI_GVF(MRV)                                                                                          \
+  if (a.M == MRV) {                                                                                           \
+    static bool once = false;                                                                                 \
+    if (!once) {                                                                                              \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_frag_kernel<MRV, EPI, NW>),                     \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kGvFragMaxDyn);                         \
+      once = true;                                                                                            \
+    }                                                                                                         \
+    gemv_frag_kernel<MRV, EPI, NW><<<grid, 64 * NW, lds, st>>>(a);                                            \
+    GAI_LAUNCH_CHECK();                                                                                       \
+    return;                                                                                                   \
+  }
+  GAI_GVF(1)
+  GAI_GVF(2)
+  GAI_GVF(3)
+  GAI_GVF(4)
+#undef GAI_GVF
+  gai_launch_error(__FILE__, __LINE__, "gemv: 1 <= M <= 4");
+}
+
 template <int EPI>
-void gemv_launch(const GemvArgs& a, hipStream_t st) {
+void gemv_frag_launch(const GemvArgs& a, hipStream_t st) {
+  static const int force = getenv("GAI_GEMV_FRAG_WAVES") ? atoi(getenv("GAI_GEMV_FRAG_WAVES")) : 0;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      ncu = 256;
+  }
+  const int grid = a.N / (16 * gv_frag_cols<EPI>());
+  const int nw = (force == 4 || force == 8 || force == 16) ? force : grid < ncu ? 16 : 8;
+  if (nw == 4) return gemv_frag_launch_nw<EPI, 4>(a, st);
+  if (nw == 16) return gemv_frag_launch_nw<EPI, 16>(a, st);
+  gemv_frag_launch_nw<EPI, 8>(a, st);
+}
+
+template <int EPI>
+void gemv_launch(const GemvArgs& a, hipStream_t st, int wfrag) {
+  if (wfrag) {
+    const int cols = gv_frag_cols<EPI>();
+    if (a.N % (16 * cols) || (a.K / 32) % (16 * kG) || (size_t)a.M * a.K * sizeof(bf16) > (size_t)kGvFragMaxDyn)
+      gai_launch_error(__FILE__, __LINE__, "gemv: fragment-ordered weight shape");
+    return gemv_frag_launch<EPI>(a, st);
+  }
   const int nw = gemv_waves(a.N, a.M);
   if (nw == 6) return gemv_launch_nw<EPI, 6>(a, st);
   if (nw == 12) return gemv_launch_nw<EPI, 12>(a, st);
@@ -302,7 +479,7 @@ int gai_gemv_ok(int M, int N, int K, int normed) {
 
 // epi: 0 plain bf16, 1 residual in place (res), 2 SwiGLU on the [gate16 | up16] interleave, 4 fp32 out.
 void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
-              void* res, hipStream_t st) {
+              void* res, hipStream_t st, int wfrag) {
   if (!gai_gemv_ok(M, N, K, gamma != nullptr)) gai_launch_error(__FILE__, __LINE__, "gemv: shape");
   if (epi == GV_SWIGLU && N % 32) gai_launch_error(__FILE__, __LINE__, "gemv: SwiGLU needs N % 32 == 0");
   GemvArgs a{};
@@ -316,10 +493,10 @@ void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M,
   a.out = out;
   a.res = (bf16*)res;
   switch (epi) {
-    case GV_PLAIN: gemv_launch<GV_PLAIN>(a, st); return;
-    case GV_RESIDUAL: gemv_launch<GV_RESIDUAL>(a, st); return;
-    case GV_SWIGLU: gemv_launch<GV_SWIGLU>(a, st); return;
-    case GV_F32: gemv_launch<GV_F32>(a, st); return;
+    case GV_PLAIN: gemv_launch<GV_PLAIN>(a, st, wfrag); return;
+    case GV_RESIDUAL: gemv_launch<GV_RESIDUAL>(a, st, wfrag); return;
+    case GV_SWIGLU: gemv_launch<GV_SWIGLU>(a, st, wfrag); return;
+    case GV_F32: gemv_launch<GV_F32>(a, st, wfrag); return;
     default: gai_launch_error(__FILE__, __LINE__, "gemv: unknown epilogue");
   }
 }
@@ -327,7 +504,7 @@ void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M,
 // QKV projection + RoPE + q / paged K, V^T stores (head_dim 128, bf16 cache), normalised input when gamma.
 void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W, int M, int K, const int* pos,
                       const float* cos_sin, const int* slots, void* q_out, void* k_cache, void* v_cache, int Hq,
-                      int Hkv, hipStream_t st) {
+                      int Hkv, hipStream_t st, int wfrag) {
   const int N = (Hq + 2 * Hkv) * 128;
   if (!gai_gemv_ok(M, N, K, gamma != nullptr)) gai_launch_error(__FILE__, __LINE__, "gemv_rope_kv: shape");
   GemvArgs a{};
@@ -346,5 +523,5 @@ void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W
   a.v_cache = (bf16*)v_cache;
   a.Hq = Hq;
   a.Hkv = Hkv;
-  gemv_launch<GV_ROPE>(a, st);
+  gemv_launch<GV_ROPE>(a, st, wfrag);
 }

@@ -63,6 +63,10 @@ class EngineConfig:
     # (non-temporal), +9 % decode / +4.9 % headline on the same box (profiles/r3/psw_ab) for a second copy of
     # the projection weights (17 GB for Llama-3-8B: 6 % of one MI355X's 288 GB)
     decode_preshuffle: bool = True
+    # "fragment": the decode projections are stored ONCE, in MFMA fragment order (rewritten in place; the prefill
+    # GEMMs, decode GEMMs and GEMV all read that layout), instead of row-major weights plus a fragment-ordered copy
+    # ("dual"). GAI_WEIGHT_LAYOUT overrides (same-box A/B).
+    weight_layout: str = "fragment"
     graph_batch_sizes: Sequence[int] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     # multi-step decode: when every running sequence is decoding (nothing waiting), run this many
     # decode steps in ONE captured HIP graph (forward -> sample -> feed the token back, on device)
@@ -148,7 +152,10 @@ class LLMEngine:
                 and hasattr(model, "preshuffle_decode_weights")):
             # before KV sizing: the fragment copies are resident; at most 20 % of the device's HBM
             total = torch.cuda.get_device_properties(self.device).total_memory
-            model.preshuffle_decode_weights(budget_bytes=int(0.2 * total))
+            layout = os.environ.get("GAI_WEIGHT_LAYOUT", cfg.weight_layout)
+            if layout not in ("fragment", "dual"):
+                raise ValueError(f"weight_layout {layout!r}: expected 'fragment' or 'dual'")
+            model.preshuffle_decode_weights(budget_bytes=int(0.2 * total), in_place=layout == "fragment")
         # tensor parallel: rank 0 of the TP group plans every step, the other members execute its plans
         ctx = getattr(model, "ctx", None)
         self.tp_size = ctx.tp_size if ctx is not None else 1

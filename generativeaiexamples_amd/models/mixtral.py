@@ -241,7 +241,7 @@ class MixtralModel(LlamaModel):
         tolerance covers. Returns CPU fp32 logits."""
         c = self.cfg
         dev = torch.device(device)
-        wf = {k: v.to(dev, torch.float32) for k, v in self.w.items()}
+        wf = {k: ops.natural_weight(v).to(dev, torch.float32) for k, v in self.w.items()}
         T, hd = token_ids.numel(), c.head_dim
         h = wf["embed"][token_ids.long().to(dev)]
         cs = self.cos_sin.to(dev)[:T]

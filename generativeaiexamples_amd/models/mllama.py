@@ -682,7 +682,7 @@ class MllamaModel(LlamaModel):
     def reference_forward(self, token_ids: torch.Tensor, image: Optional[ImageInput] = None) -> torch.Tensor:
         """Dense fp32 PyTorch forward of one sequence (+ optional image) -> logits [T, vocab]."""
         c, V = self.cfg, self.mcfg.vision
-        wf = {k: (v.dequantize(torch.float32) if isinstance(v, ops.Fp8Weight) else v.float()).cpu()
+        wf = {k: (v.dequantize(torch.float32) if isinstance(v, ops.Fp8Weight) else ops.natural_weight(v).float()).cpu()
               for k, v in self.w.items()}
         hd, H, Hkv = c.head_dim, c.num_heads, c.num_kv_heads
         states = None

@@ -194,7 +194,7 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
         # prefill: RoPE + paged KV write in the 256x256 GEMM's epilogue (no bf16 qkv round trip)
         ws = torch.empty(0, dtype=torch.float32, device=x.device)
         if native().gemm_rope_kv(x.reshape(M, K).contiguous(), w, bias, positions, cos_sin, slots, q_out, k_cache,
-                                 v_cache, Hq, Hkv, D, k_scale, v_scale, ws, False, None):
+                                 v_cache, Hq, Hkv, D, k_scale, v_scale, ws, is_frag(w), None):
             return
     qkv = linear(x, w, bias=bias)
     rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, D, True, k_scale, v_scale)
@@ -227,6 +227,51 @@ def shuffle_fragments(w: torch.Tensor) -> torch.Tensor:
     N, K = w.shape
     assert N % 16 == 0 and K % 32 == 0
     return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+def shuffle_fragments_(w: torch.Tensor, rows_per_chunk: int = 4096) -> torch.Tensor:
+    """shuffle_fragments in place, a chunk of rows (a multiple of 16) at a time: the permutation never leaves a 16-row
+    group, so chunk r of the result is the shuffle of chunk r (transient memory: one chunk, not a second weight)."""
+    step = max(16, rows_per_chunk - rows_per_chunk % 16)
+    with torch.no_grad():
+        for r0 in range(0, w.shape[0], step):
+            blk = w[r0:r0 + step]
+            blk.copy_(shuffle_fragments(blk))
+    return w
+
+
+def unshuffle_fragments(w: torch.Tensor) -> torch.Tensor:
+    """Inverse of shuffle_fragments: a fragment-ordered [N, K] weight back in row-major [N, K] order (a new tensor)."""
+    N, K = w.shape
+    return w.view(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
+
+
+def is_frag(w) -> bool:
+    """True when ``w`` itself is stored in MFMA fragment order (to_fragment_layout_): every GEMM / GEMV path reads it
+    so, and nothing keeps a row-major copy."""
+    return bool(getattr(w, "_gai_frag", False))
+
+
+def natural_weight(w) -> torch.Tensor:
+    """``w`` in row-major [N, K] order (a new tensor when it is stored fragment-ordered): for plain-PyTorch references,
+    checkpoint export and anything else outside the native kernels."""
+    return unshuffle_fragments(w) if is_frag(w) else w
+
+
+def to_fragment_layout_(w: torch.Tensor, rows_per_chunk: int = 4096) -> bool:
+    """Rewrite a bf16 [N, K] CUDA weight IN PLACE into MFMA fragment order (shuffle_fragments) and mark it: the one
+    weight layout (no second copy). The prefill GEMMs (tiled / 256x256 walks / stream-K / split walks, the QKV + RoPE
+    epilogue), the skinny and split-K decode GEMMs and the batch <= 4 GEMV all read it directly. The permutation stays
+    inside 16-row groups, so it runs in row chunks (transient memory: one chunk). Returns False (untouched) when the
+    shape does not qualify (psw_qualifies) or the weight is 2 GiB or more (the 32-bit-offset kernels)."""
+    if is_frag(w):
+        return True
+    if not psw_qualifies(w) or isinstance(w, Fp8Weight) or w.numel() * 2 >= (1 << 31) or not w.is_contiguous():
+        return False
+    shuffle_fragments_(w, rows_per_chunk)
+    w._gai_frag = True
+    w._gai_psw = w  # the decode paths' fragment-ordered operand is the weight itself
+    return True
 
 
 def psw_qualifies(w) -> bool:
@@ -283,14 +328,15 @@ def _decode_psw_linear(x, psw, bias, residual, act, out_dtype, out):
 
 def _native_gemm(x2, w, out, bias, residual, epi):
     """Hand-written MFMA GEMM: the weight-streaming split-K kernel for decode-sized M (<= 64),
-    otherwise the skinny / 128x128 / 256x256 kernels chosen inside gai_gemm."""
+    otherwise the skinny / 128x128 / 256x256 kernels chosen inside gai_gemm (fragment-ordered weights too)."""
     M, K = x2.shape
+    frag = is_frag(w)
     if _SPLITK and _GEMM_FORCE == 0 and M <= 64 and K % 512 == 0:
         nat = native()
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x2.device)
-        nat.gemm_splitk(x2, w, out, bias, residual, epi, ws)
+        nat.gemm_splitk(x2, w, out, bias, residual, epi, ws, frag)
     else:
-        native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE)
+        native().gemm(x2, w, out, bias, residual, epi, _GEMM_FORCE, frag)
 
 
 _FP8_FORCE = int(os.environ.get("GAI_FP8_FORCE", "0"))  # 0 auto, 2 tiled, 3 large
@@ -752,19 +798,20 @@ def gemv(x, W, gamma=None, eps: float = 1e-5, epi: str = "plain", res=None, out=
         return ref.gemv(x, W, gamma, eps, epi, res)
     M, N = x.shape[0], W.shape[0]
     if epi == "residual":
-        native().gemv(x.contiguous(), gamma, eps, W, 1, None, res)
+        native().gemv(x.contiguous(), gamma, eps, W, 1, None, res, is_frag(W))
         return res
     if out is None:
         cols = N // 2 if epi == "swiglu" else N
         out = torch.empty(M, cols, dtype=torch.float32 if epi == "f32" else x.dtype, device=x.device)
-    native().gemv(x.contiguous(), gamma, eps, W, _GEMV_EPI[epi], out, None)
+    native().gemv(x.contiguous(), gamma, eps, W, _GEMV_EPI[epi], out, None, is_frag(W))
     return out
 
 
 def gemv_rope_kv(x, W, gamma, eps, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq: int, Hkv: int):
     """QKV GEMV (+ the attention RMSNorm staged in) + RoPE + q / paged K, V^T stores: the batch <= 4 decode
     counterpart of linear_rope_kv, no split-K slabs and no tail launch."""
-    native().gemv_rope_kv(x.contiguous(), gamma, eps, W, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv)
+    native().gemv_rope_kv(x.contiguous(), gamma, eps, W, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv,
+                          is_frag(W))
 
 
 def ep_dispatch_plan(ids: torch.Tensor, world: int, e_local: int):

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def _fp32_logits(m: LlamaModel, ids: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
     """Dense causal fp32 forward on the GPU; logits [len(rows), vocab] at the given positions."""
     c, dev = m.cfg, ids.device
-    w = {k: v.float() for k, v in m.w.items()}
+    w = {k: ops.natural_weight(v).float() for k, v in m.w.items()}
     T, hd = ids.numel(), c.head_dim
     h = w["embed"][ids.long()]
     cs = m.cos_sin[:T].float()

@@ -3,6 +3,7 @@ gfx950 kernels: engine prefill logits vs the CPU fp32 reference of the same weig
 import pytest
 import torch
 
+from generativeaiexamples_amd import ops
 from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
 from generativeaiexamples_amd.engine.tokenizer import small_byte_tokenizer
 from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
@@ -25,7 +26,7 @@ def _pair(cuda, kw):
     g = LlamaModel(cfg, device=cuda).random_init(7)
     c = LlamaModel(cfg, device="cpu")
     for k in c.w:
-        c.w[k].copy_(g.w[k].cpu())
+        c.w[k].copy_(ops.natural_weight(g.w[k]).cpu())
     return g, c
 
 

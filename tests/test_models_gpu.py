@@ -3,6 +3,7 @@ weights, HIP-graph decode vs eager decode, and the embedder / index / engine end
 import pytest
 import torch
 
+from generativeaiexamples_amd import ops
 from generativeaiexamples_amd.engine import EngineConfig, LLMEngine, SamplingParams
 from generativeaiexamples_amd.engine.embedder import Embedder
 from generativeaiexamples_amd.engine.tokenizer import bert_byte_tokenizer, small_byte_tokenizer
@@ -17,7 +18,7 @@ def _pair_llama(cuda, **kw):
     g = LlamaModel(cfg, device=cuda).random_init(3)
     c = LlamaModel(cfg, device="cpu")
     for k in c.w:
-        c.w[k].copy_(g.w[k].cpu())
+        c.w[k].copy_(ops.natural_weight(g.w[k]).cpu())
     return g, c
 
 
@@ -59,7 +60,7 @@ def test_bert_embed_matches_cpu(cuda):
     g = BertModel(cfg, device=cuda).random_init(1)
     c = BertModel(cfg, device="cpu")
     for k in c.w:
-        c.w[k].copy_(g.w[k].cpu())
+        c.w[k].copy_(ops.natural_weight(g.w[k]).cpu())
     tok = bert_byte_tokenizer(cfg.vocab_size)
     texts = ["hello world", "a much longer passage about accelerators " * 5, "x"]
     eg = Embedder(g, tok).embed(texts).cpu()
@@ -75,7 +76,7 @@ def test_cross_encoder_scores(cuda):
     g = BertModel(cfg, device=cuda).random_init(2)
     c = BertModel(cfg, device="cpu")
     for k in c.w:
-        c.w[k].copy_(g.w[k].cpu())
+        c.w[k].copy_(ops.natural_weight(g.w[k]).cpu())
     tok = bert_byte_tokenizer(cfg.vocab_size)
     ps = ["first passage", "second, longer passage " * 4, "third"]
     sg = Reranker(g, tok).score("query text", ps)

@@ -38,7 +38,7 @@ def _pair(cuda):
     g = Qwen3NextModel(cfg, device=cuda).random_init(3)
     c = Qwen3NextModel(cfg, device="cpu", dtype=torch.float32)
     for k in c.w:
-        c.w[k].copy_(g.w[k].float().cpu())
+        c.w[k].copy_(ops.natural_weight(g.w[k]).float().cpu())
     return g, c
 
 

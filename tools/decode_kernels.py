@@ -3,6 +3,7 @@ B sequences at context C, N eager forward passes (kernel durations equal the in-
 
 rocprofv3 --kernel-trace --stats -d out -o run -- python3 tools/decode_kernels.py --batch 64 --ctx 2600
 """
+import os
 import argparse
 import time
 
@@ -24,7 +25,7 @@ def main():
     a = ap.parse_args()
     m, tok, name = build_llm(a.model, device="cuda")
     if not a.no_psw:
-        m.preshuffle_decode_weights()  # what LLMEngine does (EngineConfig.decode_preshuffle)
+        m.preshuffle_decode_weights(in_place=os.environ.get("GAI_WEIGHT_LAYOUT", "fragment") == "fragment")  # as LLMEngine
     c = m.cfg
     nbps = (a.ctx + 16) // 16 + 1
     kv = KVCache(getattr(m, "num_kv_layers", c.num_layers), a.batch * nbps + 1, m.hkv, c.head_dim, m.device, m.dtype)

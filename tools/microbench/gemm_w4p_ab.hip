@@ -47,9 +47,9 @@ float run_w4d(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int gr
   hipEvent_t ev0, ev1;
   CK(hipEventCreate(&ev0));
   CK(hipEventCreate(&ev1));
-  k<<<grid, 256, 2 * kDblBytes>>>(A, B, C, nullptr, nullptr, M, N, K, N, RopeKvArgs{});
+  k<<<grid, 256, 2 * kDblBytes>>>(A, B, C, nullptr, nullptr, M, N, K, N, RopeKvArgs{}, 0);
   CK(hipEventRecord(ev0));
-  for (int i = 0; i < iters; ++i) k<<<grid, 256, 2 * kDblBytes>>>(A, B, C, nullptr, nullptr, M, N, K, N, RopeKvArgs{});
+  for (int i = 0; i < iters; ++i) k<<<grid, 256, 2 * kDblBytes>>>(A, B, C, nullptr, nullptr, M, N, K, N, RopeKvArgs{}, 0);
   CK(hipEventRecord(ev1));
   CK(hipEventSynchronize(ev1));
   float ms = 0;
@@ -63,9 +63,9 @@ float run_w4r(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int gr
   hipEvent_t ev0, ev1;
   CK(hipEventCreate(&ev0));
   CK(hipEventCreate(&ev1));
-  k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N);
+  k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N, nullptr, nullptr, 1, 0);
   CK(hipEventRecord(ev0));
-  for (int i = 0; i < iters; ++i) k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N);
+  for (int i = 0; i < iters; ++i) k<<<grid, 256, 5 * kPart>>>(A, B, C, nullptr, nullptr, M, N, K, N, nullptr, nullptr, 1, 0);
   CK(hipEventRecord(ev1));
   CK(hipEventSynchronize(ev1));
   float ms = 0;

@@ -115,7 +115,7 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     m = build(a.model, a.tp, a.rank, a.layers)
-    m.preshuffle_decode_weights()  # what LLMEngine does (EngineConfig.decode_preshuffle)
+    m.preshuffle_decode_weights(in_place=os.environ.get("GAI_WEIGHT_LAYOUT", "fragment") == "fragment")  # as LLMEngine
     c = m.cfg
     shapes = {k: list(m.w["l0." + k].shape) for k in ("qkv", "o", "gate_up", "down")} | {
         "lm_head": list(m.w["lm_head"].shape)}
