@@ -255,110 +255,140 @@ __global__ __launch_bounds__(64 * NW) void gemv_kernel(GemvArgs a) {
 // Fragment-ordered weights (ops.shuffle_fragments: [N/16][K/32][64 lanes][8], the one layout of the decode
 // projections): a 16-row column of W is K/32 contiguous 1 KiB MFMA fragments, lane l of fragment kt holding row l & 15,
 // k 32 kt + 8 (l >> 4) .. + 8. A workgroup owns C whole columns - one for the plain / fp32 / residual epilogues, the
-// (gate, up) pair 2b, 2b + 1 for SwiGLU, the rotate-half pair c, c + 4 of one head for RoPE - and its NW waves split K:
-// wave w streams fragments [w KF / NW, (w + 1) KF / NW) of each column, kG per column in flight ahead of the
-// arithmetic (whole 1 KiB fragments, non-temporal), dotting each lane's 8 weights with the staged activation chunk.
-// The 4 lanes of a row (l, l + 16, l + 32, l + 48) reduce by cross-lane shuffles, the NW waves through LDS, and the
-// 16 C row results per token row leave through the row-pair epilogue gv_epilogue.
+// (gate, up) pair 2b, 2b + 1 for SwiGLU, the rotate-half pair c, c + 4 of one head for RoPE. Each wave streams ONE
+// column (a wave streaming two columns at once ran 25-35 % slower: SwiGLU 45-51 vs 36.9 us at any wave count,
+// profiles/r5/weight_layout): the NW / C waves of a column split its K range, kG whole 1 KiB fragments in flight ahead
+// of the arithmetic (non-temporal), each lane dotting its 8 weights with the staged activation chunk. The 4 lanes of a
+// row (l, l + 16, l + 32, l + 48) reduce by cross-lane shuffles, the waves through LDS.
+// KS > 1 (opt-in, GAI_GEMV_FRAG_KS: it did not pay where the grid has fewer column groups than CUs - Llama-3-8B
+// QKV + RoPE, 192 column pairs for 256 CUs: 13.6 us unsplit, 13.7-16.0 split in two): KS workgroups split K of one group; each stores its fp32 row sums write-through (sc1), waits for them, and draws a
+// relaxed agent-scope ticket (the stream-K GEMM's hand-over, gemm_impl.h gemm_w4r_kernel); the last one sums the KS
+// partials in K order (deterministic whichever finishes last), resets the ticket, and runs the row-pair epilogue
+// gv_epilogue.
 template <int EPI>
 constexpr int gv_frag_cols() { return (EPI == GV_SWIGLU || EPI == GV_ROPE) ? 2 : 1; }
 
+// fragments per wave per pipeline group (two groups in flight). 8-deep groups: batch-1 SwiGLU 44.2 -> 42.4 us but QKV
+// 13.7 -> 16.0, LM head 153 -> 167, the batch-4 step 4.01 -> 4.31 ms (profiles/r5/weight_layout)
+constexpr int kGf = 4;
+constexpr int kGvfMaxItems = 1024;  // split workspace: (group, K part) items
+__device__ float g_gvf_ws[kGvfMaxItems * 4 * 16 * 2];  // [item][MR <= 4][16 pairs][2] fp32 row sums
+__device__ int g_gvf_cnt[kGvfMaxItems];                // tickets per group, zero between launches
+
 template <int MR, int EPI, int NW>
-__global__ __launch_bounds__(64 * NW) void gemv_frag_kernel(GemvArgs a) {
+__global__ __launch_bounds__(64 * NW) void gemv_frag_kernel(GemvArgs a, int KS) {
   constexpr int C = gv_frag_cols<EPI>();
+  constexpr int NWC = NW / C;                 // waves per column
+  constexpr int NP = C == 1 ? 8 : 16;         // row pairs per group: rows (2i, 2i + 1) of one column, or row i of both
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [MR][K] bf16 activation image
   __shared__ float red[NW][MR];
   __shared__ float inv_s[MR];
-  __shared__ float part[NW][MR][C][16];
+  __shared__ float part[NW][MR][16];
+  __shared__ int last_s;
   bf16* xs = reinterpret_cast<bf16*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int K = a.K, KF = K / 32;
-  const int b = blockIdx.x;
-  int col[C];
-  if constexpr (EPI == GV_ROPE) {
-    col[0] = 8 * (b >> 2) + (b & 3);
-    col[C - 1] = col[0] + 4;
-  } else {
-#pragma unroll
-    for (int c = 0; c < C; ++c) col[c] = C * b + c;
-  }
-  const int nf = KF / NW, f0 = wid * nf;  // host: KF % (NW kG) == 0
-  const bf16* wp[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) wp[c] = a.W + ((size_t)col[c] * KF + f0) * 512 + 8 * lane;
-  bf16x8 cur[C][kG], nxt[C][kG];
-  auto load_group = [&](int g, bf16x8(&bq)[C][kG]) {
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int j = 0; j < kG; ++j)
-        bq[c][j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[c] + (size_t)(g * kG + j) * 512));
+  const int groups = (int)gridDim.x / KS;
+  const int b = (int)blockIdx.x % groups, h = (int)blockIdx.x / groups;  // column group, K part
+  auto column = [&](int c) {
+    if constexpr (EPI == GV_ROPE) return 8 * (b >> 2) + (b & 3) + 4 * c;
+    else return C * b + c;
   };
-  load_group(0, cur);  // in flight during the activation staging
+  const int wc = wid / NWC;                    // this wave's column (0 .. C-1)
+  const int nf = KF / (KS * NWC);              // fragments per wave (host: a multiple of kGf)
+  const int f0 = h * (KF / KS) + (wid % NWC) * nf;
+  const bf16* wp = a.W + ((size_t)column(wc) * KF + f0) * 512 + 8 * lane;
+  bf16x8 cur[kGf], nxt[kGf];
+  auto load_group = [&](int g, bf16x8(&bq)[kGf]) {
+#pragma unroll
+    for (int j = 0; j < kGf; ++j)
+      bq[j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + (size_t)(g * kGf + j) * 512));
+  };
+  const int ngroups = nf / kGf;
+  // both groups in flight during the activation staging (the RMSNorm of the normalised forms takes a few us)
+  load_group(0, cur);
+  if (ngroups > 1) load_group(1, nxt);
   gv_stage<MR, NW>(a, xs, &red[0][0], inv_s);
   __syncthreads();
 
-  float acc[MR][C];
+  float acc[MR];
 #pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int c = 0; c < C; ++c) acc[m][c] = 0.f;
+  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
   const int kl = 8 * (lane >> 4);  // the lane's k offset inside a fragment
-  auto compute_group = [&](int g, const bf16x8(&bq)[C][kG]) {
+  auto compute_group = [&](int g, const bf16x8(&bq)[kGf]) {
 #pragma unroll
-    for (int j = 0; j < kG; ++j) {
-      const int k0 = (f0 + g * kG + j) * 32 + kl;
+    for (int j = 0; j < kGf; ++j) {
+      const int k0 = (f0 + g * kGf + j) * 32 + kl;
 #pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0);
-#pragma unroll
-        for (int c = 0; c < C; ++c) acc[m][c] = dot8(xv, bq[c][j], acc[m][c]);
-      }
+      for (int m = 0; m < MR; ++m)
+        acc[m] = dot8(*reinterpret_cast<const bf16x8*>(xs + (size_t)m * K + k0), bq[j], acc[m]);
     }
   };
-  const int ngroups = nf / kG;
-  int g = 0;
-  for (; g + 2 <= ngroups; g += 2) {
-    load_group(g + 1, nxt);
+  for (int g = 0; g < ngroups; g += 2) {  // groups g, g + 1 in flight on entry
     compute_group(g, cur);
     if (g + 2 < ngroups) load_group(g + 2, cur);
-    compute_group(g + 1, nxt);
+    if (g + 1 < ngroups) {
+      compute_group(g + 1, nxt);
+      if (g + 3 < ngroups) load_group(g + 3, nxt);
+    }
   }
-  if (g < ngroups) compute_group(g, cur);
 
   // lanes l, l + 16, l + 32, l + 48 hold row l & 15's partials
 #pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      float v = acc[m][c];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lane < 16) part[wid][m][c][lane] = v;
-    }
-  __syncthreads();
-  // row pairs of this workgroup: 8 per column (rows 2i, 2i + 1) or 16 (SwiGLU / RoPE: row i of each column)
-  constexpr int NP = C == 1 ? 8 : 16;
-  for (int e = tid; e < MR * NP; e += 64 * NW) {
-    const int m = e / NP, i = e % NP;
-    const int ra = C == 1 ? 2 * i : i, rb = C == 1 ? 2 * i + 1 : i;  // rows inside columns ca / cb
-    const int ca = 0, cb = C - 1;
-    float v0 = 0.f, v1 = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      v0 += part[w][m][ca][ra];
-      v1 += part[w][m][cb][rb];
-    }
-    const int r0 = 16 * col[ca] + ra, r1 = 16 * col[cb] + rb;
-    int p;
-    if constexpr (EPI == GV_SWIGLU)
-      p = 16 * b + i;  // output column: gate row r0 = 32 b + i
-    else if constexpr (EPI == GV_ROPE)
-      p = 64 * (r0 >> 7) + (r0 & 63);  // head r0 / 128, dim r0 % 128 (< 64)
-    else
-      p = r0 >> 1;
-    gv_epilogue<EPI>(a, m, p, r0, r1, v0, v1);
+  for (int m = 0; m < MR; ++m) {
+    float v = acc[m];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 16) part[wid][m][lane] = v;
   }
+  __syncthreads();
+  const bool epi_thread = tid < MR * NP;
+  const int m = tid / NP, i = tid % NP;
+  const int ra = C == 1 ? 2 * i : i, rb = C == 1 ? 2 * i + 1 : i;  // rows inside columns 0 / C-1
+  float v0 = 0.f, v1 = 0.f;
+  if (epi_thread) {
+#pragma unroll
+    for (int w = 0; w < NWC; ++w) {
+      v0 += part[w][m][ra];
+      v1 += part[(C - 1) * NWC + w][m][rb];
+    }
+  }
+  if (KS > 1) {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(g_gvf_ws, (short)0, 0x7fffffff, 0x00020000);
+    using f32x2 = __attribute__((ext_vector_type(2))) float;
+    auto off = [&](int part_h) { return (unsigned)((((b * KS + part_h) * 4 + m) * 16 + i) * 8); };
+    if (epi_thread)  // write-through (sc1): visible to the other XCDs' L2s
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                               f32x2{v0, v1}), rw, off(h), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int tk = __hip_atomic_fetch_add(&g_gvf_cnt[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = tk == KS - 1;
+      if (tk == KS - 1) __hip_atomic_store(&g_gvf_cnt[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    if (epi_thread) {
+      v0 = v1 = 0.f;
+      for (int q = 0; q < KS; ++q) {  // K order
+        const f32x2 t = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rw, off(q), 0, 16));
+        v0 += t.x;
+        v1 += t.y;
+      }
+    }
+  }
+  if (!epi_thread) return;
+  const int r0 = 16 * column(0) + ra, r1 = 16 * column(C - 1) + rb;
+  int p;
+  if constexpr (EPI == GV_SWIGLU)
+    p = 16 * b + i;  // output column: gate row r0 = 32 b + i
+  else if constexpr (EPI == GV_ROPE)
+    p = 64 * (r0 >> 7) + (r0 & 63);  // head r0 / 128, dim r0 % 128 (< 64)
+  else
+    p = r0 >> 1;
+  gv_epilogue<EPI>(a, m, p, r0, r1, v0, v1);
 }
 
 // Waves per workgroup: 8, or 12 where that quantises the row pairs onto the CUs better (Llama-3-8B QKV, N 6144: 3072
@@ -408,15 +438,18 @@ void gemv_launch_nw(const GemvArgs& a, hipStream_t st) {
   gai_launch_error(__FILE__, __LINE__, "gemv: 1 <= M <= 4");
 }
 
-// Fragment-ordered launch: N / (16 C) workgroups; 16 waves when that grid leaves CUs without a workgroup (Llama-3-8B
-// QKV + RoPE: 192 column pairs), else 8. GAI_GEMV_FRAG_WAVES = 4 / 8 / 16 forces one (sweeps).
-constexpr int kGvFragStatic = 10 * 1024;  // bound on the frag kernel's static LDS (part[16][4][2][16] + red)
+// Fragment-ordered launch: N / (16 C) column groups. Waves per workgroup by epilogue (Llama-3-8B sweeps, batch 1 / 4,
+// profiles/r5/weight_layout): 16 for the one-column plain / residual forms (O / down 14.9 -> 14.0 us at batch 1,
+// 17.0 -> 15.8 at batch 4) and QKV + RoPE (13.1 -> 12.1 / 15.1 -> 14.8); 8 for the fp32 LM head (16: 154 -> 158 /
+// 178 -> 218) and batch > 1 SwiGLU (16: 48.1 -> 54.8), 4 for batch-1 SwiGLU (44.0 -> 42.8). GAI_GEMV_FRAG_WAVES =
+// 4 / 8 / 16 and GAI_GEMV_FRAG_KS = 2 / 4 / 8 (K parts per group where it fits) force others.
+constexpr int kGvFragStatic = 6 * 1024;  // bound on the frag kernel's static LDS (part[16][4][16] + red + inv_s)
 constexpr int kGvFragMaxDyn = 160 * 1024 - kGvFragStatic;
 
 template <int EPI, int NW>
-void gemv_frag_launch_nw(const GemvArgs& a, hipStream_t st) {
+void gemv_frag_launch_nw(const GemvArgs& a, int KS, hipStream_t st) {
   const size_t lds = (size_t)a.M * a.K * sizeof(bf16);
-  const int grid = a.N / (16 * gv_frag_cols<EPI>());
+  const int grid = a.N / (16 * gv_frag_cols<EPI>()) * KS;
 #define GAI_GVF(MRV)                                                                                          \
   if (a.M == MRV) {                                                                                           \
     static bool once = false;                                                                                 \
@@ -425,7 +458,7 @@ void gemv_frag_launch_nw(const GemvArgs& a, hipStream_t st) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, kGvFragMaxDyn);                         \
       once = true;                                                                                            \
     }                                                                                                         \
-    gemv_frag_kernel<MRV, EPI, NW><<<grid, 64 * NW, lds, st>>>(a);                                            \
+    gemv_frag_kernel<MRV, EPI, NW><<<grid, 64 * NW, lds, st>>>(a, KS);                                        \
     GAI_LAUNCH_CHECK();                                                                                       \
     return;                                                                                                   \
   }
@@ -439,26 +472,27 @@ void gemv_frag_launch_nw(const GemvArgs& a, hipStream_t st) {
 
 template <int EPI>
 void gemv_frag_launch(const GemvArgs& a, hipStream_t st) {
-  static const int force = getenv("GAI_GEMV_FRAG_WAVES") ? atoi(getenv("GAI_GEMV_FRAG_WAVES")) : 0;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
-      ncu = 256;
-  }
-  const int grid = a.N / (16 * gv_frag_cols<EPI>());
-  const int nw = (force == 4 || force == 8 || force == 16) ? force : grid < ncu ? 16 : 8;
-  if (nw == 4) return gemv_frag_launch_nw<EPI, 4>(a, st);
-  if (nw == 16) return gemv_frag_launch_nw<EPI, 16>(a, st);
-  gemv_frag_launch_nw<EPI, 8>(a, st);
+  static const int fnw = getenv("GAI_GEMV_FRAG_WAVES") ? atoi(getenv("GAI_GEMV_FRAG_WAVES")) : 0;
+  static const int fks = getenv("GAI_GEMV_FRAG_KS") ? atoi(getenv("GAI_GEMV_FRAG_KS")) : 0;
+  constexpr int C = gv_frag_cols<EPI>();
+  const int groups = a.N / (16 * C), KF = a.K / 32;
+  const int nw = (fnw == 4 || fnw == 8 || fnw == 16) ? fnw
+                 : EPI == GV_F32 ? 8
+                 : EPI == GV_SWIGLU ? (a.M == 1 ? 4 : 8)
+                 : 16;
+  auto fits = [&](int ks) { return (ks == 1 || groups * ks <= kGvfMaxItems) && KF % (ks * (nw / C) * kGf) == 0; };
+  const int KS = (fks == 2 || fks == 4 || fks == 8) && fits(fks) ? fks : 1;
+  if (!fits(KS)) gai_launch_error(__FILE__, __LINE__, "gemv: fragment-ordered K split");
+  if (nw == 4) return gemv_frag_launch_nw<EPI, 4>(a, KS, st);
+  if (nw == 16) return gemv_frag_launch_nw<EPI, 16>(a, KS, st);
+  gemv_frag_launch_nw<EPI, 8>(a, KS, st);
 }
 
 template <int EPI>
 void gemv_launch(const GemvArgs& a, hipStream_t st, int wfrag) {
   if (wfrag) {
     const int cols = gv_frag_cols<EPI>();
-    if (a.N % (16 * cols) || (a.K / 32) % (16 * kG) || (size_t)a.M * a.K * sizeof(bf16) > (size_t)kGvFragMaxDyn)
+    if (a.N % (16 * cols) || (a.K / 32) % (8 * kG) || (size_t)a.M * a.K * sizeof(bf16) > (size_t)kGvFragMaxDyn)
       gai_launch_error(__FILE__, __LINE__, "gemv: fragment-ordered weight shape");
     return gemv_frag_launch<EPI>(a, st);
   }

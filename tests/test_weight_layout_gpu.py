@@ -193,3 +193,27 @@ def test_engine_one_layout_same_tokens_no_copies(cuda, monkeypatch):
     assert extra["fragment"] == 0
     assert extra["dual"] >= proj
     assert outs["fragment"] == outs["dual"]
+
+
+def test_gemv_fragment_k_split_opt_in(cuda):
+    """GAI_GEMV_FRAG_KS = 2 (read once per process, so in a child): the cross-workgroup K split of the fragment GEMV
+    (write-through partials + ticket, the last workgroup sums in K order) matches the unsplit kernel's reference."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import torch, math\n"
+        "from tests.test_weight_layout_gpu import test_gemv_fragment_weight_matches_fp32 as t, "
+        "test_gemv_rope_kv_fragment_weight as r\n"
+        "d = torch.device('cuda:0')\n"
+        "for M in (1, 4):\n"
+        "    t(d, M, 2048, 8192, 'plain', False)\n"
+        "    t(d, M, 6144, 4096, 'plain', True)\n"
+        "    t(d, M, 28672, 4096, 'swiglu', True)\n"
+        "    r(d, M)\n"
+        "print('split ok')\n")
+    env = dict(os.environ, GAI_GEMV_FRAG_KS="2")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0 and "split ok" in out.stdout, out.stderr[-2000:]
