@@ -271,7 +271,7 @@ constexpr int gv_frag_cols() { return (EPI == GV_SWIGLU || EPI == GV_ROPE) ? 2 :
 // fragments per wave per pipeline group (two groups in flight). 8-deep groups: batch-1 SwiGLU 44.2 -> 42.4 us but QKV
 // 13.7 -> 16.0, LM head 153 -> 167, the batch-4 step 4.01 -> 4.31 ms (profiles/r5/weight_layout)
 constexpr int kGf = 4;
-constexpr int kGvfMaxItems = 1024;  // split workspace: (group, K part) items
+constexpr int kGvfMaxItems = 4096;  // split workspace: (group, K part) items (2 MiB)
 __device__ float g_gvf_ws[kGvfMaxItems * 4 * 16 * 2];  // [item][MR <= 4][16 pairs][2] fp32 row sums
 __device__ int g_gvf_cnt[kGvfMaxItems];                // tickets per group, zero between launches
 
