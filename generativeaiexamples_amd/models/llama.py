@@ -319,6 +319,14 @@ class LlamaModel:
             s += 1
         return self
 
+    def _put(self, name: str, t: torch.Tensor) -> None:
+        """Copy a row-major weight in; a weight an engine already rewrote into the one (fragment-ordered) layout
+        (ops.to_fragment_layout_) is stored fragment-ordered again."""
+        dst = self.w[name]
+        dst.copy_(t.to(self.dtype))
+        if ops.is_frag(dst):
+            ops.shuffle_fragments_(dst)
+
     def load_hf_state(self, sd: Dict[str, torch.Tensor]):
         """Load a HF Llama state dict (full weights; each TP rank keeps its shard)."""
         c, tp, r = self.cfg, self.ctx.tp_size, self.ctx.tp_rank
@@ -327,8 +335,7 @@ class LlamaModel:
         def shard_rows(t, n):  # column-parallel (output dim)
             return t.reshape(tp, n // tp, *t.shape[1:])[r] if tp > 1 else t
 
-        def put(name, t):
-            self.w[name].copy_(t.to(self.dtype))
+        put = self._put
 
         def norm_w(t):  # Gemma stores RMSNorm weights as w with y = x_hat * (1 + w): fold the 1 in
             return t.float() + 1.0 if c.arch == "gemma" else t
@@ -379,7 +386,7 @@ class LlamaModel:
             return t.reshape(tp, n // tp, *t.shape[1:])[r] if tp > 1 else t
 
         if c.mlp == "gelu_tanh":  # StarCoder2: c_fc -> gelu -> c_proj
-            self.w[p + "fc"].copy_(shard_rows(sd[h + "mlp.c_fc.weight"], c.intermediate_size).to(self.dtype))
+            self._put(p + "fc", shard_rows(sd[h + "mlp.c_fc.weight"], c.intermediate_size))
             dn = sd[h + "mlp.c_proj.weight"]
             if c.mlp_bias:
                 self.w[p + "fc_b"].copy_(shard_rows(sd[h + "mlp.c_fc.bias"], c.intermediate_size).to(self.dtype))
@@ -387,9 +394,9 @@ class LlamaModel:
         else:
             g = shard_rows(sd[h + "mlp.gate_proj.weight"], c.intermediate_size)
             u = shard_rows(sd[h + "mlp.up_proj.weight"], c.intermediate_size)
-            self.w[p + "gate_up"].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
+            self._put(p + "gate_up", ops.interleave_gate_up(g, u))
             dn = sd[h + "mlp.down_proj.weight"]
-        self.w[p + "down"].copy_((dn.reshape(dn.shape[0], tp, -1)[:, r] if tp > 1 else dn).to(self.dtype))
+        self._put(p + "down", dn.reshape(dn.shape[0], tp, -1)[:, r] if tp > 1 else dn)
 
     def export_hf_state(self) -> Dict[str, torch.Tensor]:
         """Inverse of load_hf_state for a TP=1 model (checkpoint export, TP-reshard tests)."""

@@ -76,6 +76,9 @@ class FullTrainer:
         torch.manual_seed(cfg.seed)
         seen, self.names, self.params = set(), [], []
         for k, t in model.w.items():
+            if getattr(t, "_gai_frag", False):
+                raise ValueError(f"{k} is stored in the fragment-ordered inference layout (an LLMEngine rewrote it): "
+                                 "train a model no engine has served, or EngineConfig.weight_layout='dual'")
             if t.data_ptr() in seen:  # tied embeddings: one leaf
                 continue
             seen.add(t.data_ptr())

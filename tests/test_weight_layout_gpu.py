@@ -217,3 +217,23 @@ def test_gemv_fragment_k_split_opt_in(cuda):
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0 and "split ok" in out.stdout, out.stderr[-2000:]
+
+
+def test_checkpoint_roundtrip_on_fragment_layout(cuda):
+    """export_hf_state hands out row-major weights, and load_hf_state into a model an engine already rewrote stores
+    them fragment-ordered again: reloading the export leaves every weight bitwise unchanged."""
+    from generativeaiexamples_amd.models import LlamaConfig, LlamaModel
+
+    cfg = LlamaConfig.llama3_8b(num_layers=1)
+    m = LlamaModel(cfg, device=cuda).random_init(3)
+    nat = {k: v.clone() for k, v in m.w.items()}
+    m.preshuffle_decode_weights(in_place=True)
+    assert ops.is_frag(m.w["l0.gate_up"]) and ops.is_frag(m.w["lm_head"])
+    sd = m.export_hf_state()
+    for k, v in m.w.items():
+        assert torch.equal(ops.natural_weight(v), nat[k]), k
+    before = {k: v.clone() for k, v in m.w.items()}
+    m.load_hf_state(sd)
+    for k, v in m.w.items():
+        assert torch.equal(v, before[k]), k
+    assert ops.is_frag(m.w["l0.qkv"])
