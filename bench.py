@@ -447,6 +447,8 @@ def main():
             "max_tokens": args.max_tokens,
             "top_k": args.top_k,
             "kv_cache_dtype": "bf16" if args.kv_cache_dtype == "auto" else "fp8_e4m3",
+            # decode projections stored once, fragment-ordered (EngineConfig.weight_layout; GAI_WEIGHT_LAYOUT overrides)
+            "weight_layout": os.environ.get("GAI_WEIGHT_LAYOUT", "fragment"),
         },
         "p50_ttft_s": round(p50, 4),
         "p90_ttft_s": round(p90, 4),
