@@ -41,7 +41,8 @@ EXAMPLE_DIR = os.environ.get("EXAMPLE_DIR") or (
     "RAG/examples/" if os.path.isdir("RAG/examples") else os.path.join(_REPO, "RAG", "examples"))
 UPLOAD_DIR = os.environ.get("UPLOAD_DIR", "/tmp-data/uploaded_files")
 
-app = FastAPI(title="RAG chain server", description="MI355X-native chain server", version="1.0.0")
+# FastAPI's default title / version, as the reference's ``FastAPI()`` (docs/api_reference/openapi_schema.json "info")
+app = FastAPI()
 app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=False, allow_methods=["*"],
                    allow_headers=["*"])
 
@@ -72,16 +73,31 @@ class Message(BaseModel):
 class Prompt(BaseModel):
     """Definition of the Prompt API data type."""
 
-    messages: List[Message] = Field(..., description="A list of messages comprising the conversation so far.",
-                                    max_length=50000)
+    messages: List[Message] = Field(
+        ..., max_length=50000,
+        description="A list of messages comprising the conversation so far. The roles of the messages must be "
+                    "alternating between user and assistant. The last input message should have role user. A message "
+                    "with the the system role is optional, and must be the very first message if it is present.")
     use_knowledge_base: bool = Field(..., description="Whether to use a knowledge base")
-    temperature: float = Field(0.2, description="The sampling temperature to use for text generation.", ge=0.1, le=1.0)
-    top_p: float = Field(0.7, description="The top-p sampling mass used for text generation.", ge=0.1, le=1.0)
-    max_tokens: int = Field(1024, description="The maximum number of tokens to generate in any given call.",
-                            ge=0, le=1024, json_schema_extra={"format": "int64"})
+    temperature: float = Field(
+        0.2, ge=0.1, le=1.0,
+        description="The sampling temperature to use for text generation. The higher the temperature value is, the "
+                    "less deterministic the output text will be. It is not recommended to modify both temperature and "
+                    "top_p in the same call.")
+    top_p: float = Field(
+        0.7, ge=0.1, le=1.0,
+        description="The top-p sampling mass used for text generation. The top-p value determines the probability "
+                    "mass that is sampled at sampling time. For example, if top_p = 0.2, only the most likely tokens "
+                    "(summing to 0.2 cumulative probability) will be sampled. It is not recommended to modify both "
+                    "temperature and top_p in the same call.")
+    max_tokens: int = Field(
+        1024, ge=0, le=1024, json_schema_extra={"format": "int64"},
+        description="The maximum number of tokens to generate in any given call. Note that the model is not aware of "
+                    "this value, and generation will simply stop at the number of tokens specified.")
     stop: List[constr(max_length=256, pattern=r"[\s\S]*")] = Field(
-        description="A string or a list of strings where the API will stop generating further tokens.",
-        max_length=256, default=[])
+        max_length=256, default=[],
+        description="A string or a list of strings where the API will stop generating further tokens. The returned "
+                    "text will not contain the stop sequence.")
 
     @field_validator("use_knowledge_base", mode="before")
     @classmethod
@@ -99,17 +115,23 @@ class Prompt(BaseModel):
 
 
 class ChainResponseChoices(BaseModel):
+    """Definition of Chain response choices"""
+
     index: int = Field(default=0, ge=0, le=256, json_schema_extra={"format": "int64"})
     message: Message = Field(default=Message(role="assistant", content=""))
     finish_reason: str = Field(default="", max_length=4096, pattern=r"[\s\S]*")
 
 
 class ChainResponse(BaseModel):
+    """Definition of Chain APIs resopnse data type"""
+
     id: str = Field(default="", max_length=100000, pattern=r"[\s\S]*")
     choices: List[ChainResponseChoices] = Field(default=[], max_length=256)
 
 
 class DocumentSearch(BaseModel):
+    """Definition of the DocumentSearch API data type."""
+
     query: str = Field(description="The content or keywords to search for within documents.", max_length=131072,
                        pattern=r"[\s\S]*", default="")
     top_k: int = Field(description="The maximum number of documents to return in the response.", default=4, ge=0,
@@ -117,6 +139,8 @@ class DocumentSearch(BaseModel):
 
 
 class DocumentChunk(BaseModel):
+    """Represents a chunk of a document."""
+
     content: str = Field(description="The content of the document chunk.", max_length=131072, pattern=r"[\s\S]*",
                          default="")
     filename: str = Field(description="The name of the file the chunk belongs to.", max_length=4096,
@@ -125,10 +149,14 @@ class DocumentChunk(BaseModel):
 
 
 class DocumentSearchResponse(BaseModel):
+    """Represents a response from a document search."""
+
     chunks: List[DocumentChunk] = Field(..., description="List of document chunks.", max_length=256)
 
 
 class DocumentsResponse(BaseModel):
+    """Represents the response containing a list of documents."""
+
     documents: List[constr(max_length=131072, pattern=r"[\s\S]*")] = Field(
         description="List of filenames.", max_length=1000000, default=[])
 
@@ -183,22 +211,52 @@ async def _validation(request: Request, exc: RequestValidationError) -> JSONResp
 
 
 # ------------------------------------------------------------------------------------ routes
-@app.get("/health", response_model=HealthResponse,
-         responses={500: {"description": "Internal Server Error"}})
+# every route documents its 500 like the reference (server.py:248-257 and the other decorators)
+_ERR500 = {500: {"description": "Internal Server Error",
+                 "content": {"application/json": {"example": {"detail": "Internal server error occurred"}}}}}
+_VALIDATION_ERROR = {"description": "Validation Error",
+                     "content": {"application/json": {"schema": {"$ref": "#/components/schemas/HTTPValidationError"}}}}
+# POST /documents takes ``file: UploadFile = File(...)`` in the reference (server.py:280). python-multipart is not
+# importable here, so the body is parsed by chain_server/multipart.py and the multipart requestBody that FastAPI
+# would derive from File(...) is declared explicitly (schema added to components in _openapi below).
+_UPLOAD_BODY_SCHEMA = {"properties": {"file": {"type": "string", "format": "binary", "title": "File"}},
+                       "type": "object", "required": ["file"], "title": "Body_upload_document_documents_post"}
+_UPLOAD_OPENAPI = {"requestBody": {"required": True, "content": {"multipart/form-data": {
+    "schema": {"$ref": "#/components/schemas/Body_upload_document_documents_post"}}}}}
+
+
+@app.get("/health", response_model=HealthResponse, responses=_ERR500)
 async def health_check():
+    """
+    Perform a Health Check
+
+    Returns 200 when service is up. This does not check the health of downstream services.
+    """
     return HealthResponse(message="Service is up.")
 
 
-@app.post("/documents", responses={500: {"description": "Internal Server Error"}})
+def _missing_file() -> JSONResponse:
+    """The 422 FastAPI gives a ``File(...)`` parameter whose part is absent (the reference's behaviour)."""
+    return JSONResponse(status_code=422, content={"detail": [
+        {"type": "missing", "loc": ["body", "file"], "msg": "Field required"}]})
+
+
+@app.post("/documents", responses={422: _VALIDATION_ERROR, **_ERR500}, openapi_extra=_UPLOAD_OPENAPI)
 @tracing.instrumentation_wrapper
 async def upload_document(request: Request) -> JSONResponse:
+    """Upload a document to the vector store."""
+    ctype = request.headers.get("content-type", "")
+    body = await request.body()
     try:
-        ctype = request.headers.get("content-type", "")
-        body = await request.body()
         parts = parse_multipart(ctype, body)
-        f = next((p for p in parts if p.name == "file" and p.filename), None)
-        if f is None:
-            return JSONResponse(content={"message": "No files provided"}, status_code=200)
+    except Exception:
+        parts = []
+    f = next((p for p in parts if p.name == "file"), None)
+    if f is None:
+        return _missing_file()
+    if not f.filename:  # a file part without a name: the reference's 200 "No files provided" (server.py:283-284)
+        return JSONResponse(content={"message": "No files provided"}, status_code=200)
+    try:
         name = os.path.basename(f.filename)
         os.makedirs(UPLOAD_DIR, exist_ok=True)
         path = os.path.join(UPLOAD_DIR, name)
@@ -220,9 +278,10 @@ def _frame(content: str, finish: str = "", rid: str | None = None) -> str:
     return "data: " + r.model_dump_json() + "\n\n"
 
 
-@app.post("/generate", responses={500: {"description": "Internal Server Error"}})
+@app.post("/generate", response_model=ChainResponse, responses=_ERR500)
 @tracing.instrumentation_wrapper
 async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse:
+    """Generate and stream the response to the provided prompt."""
     try:
         msgs = [m.model_dump() for m in prompt.messages]
         query, idx = None, None
@@ -236,6 +295,10 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
         if query is None:
             query = ""
         chain = ex.rag_chain if prompt.use_knowledge_base else ex.llm_chain
+        # conversation state keyed by an explicit session (X-Session-Id header) for chains that keep memory
+        sid = request.headers.get("x-session-id")
+        if sid and "session_id" in inspect.signature(chain).parameters:
+            settings["session_id"] = clean(sid)[:256]
         # retrieval + prompt building run in a worker thread (concurrent queries coalesce into one embed and
         # one index scan there); the token stream is then awaited on the event loop when the chain returns
         # an async-iterable stream (in-process engine), so no thread is held per open stream
@@ -268,9 +331,10 @@ async def generate_answer(request: Request, prompt: Prompt) -> StreamingResponse
         return StreamingResponse(iter([_frame(msg, "[DONE]")]), media_type="text/event-stream", status_code=500)
 
 
-@app.post("/search", response_model=DocumentSearchResponse, responses={500: {"description": "Internal Server Error"}})
+@app.post("/search", response_model=DocumentSearchResponse, responses=_ERR500)
 @tracing.instrumentation_wrapper
 async def document_search(request: Request, data: DocumentSearch) -> Dict[str, List[Dict[str, Any]]]:
+    """Search for the most relevant documents for the given search parameters."""
     try:
         ex = example()
         if not hasattr(ex, "document_search"):
@@ -284,9 +348,10 @@ async def document_search(request: Request, data: DocumentSearch) -> Dict[str, L
         return JSONResponse(content={"message": f"Error occurred while searching documents. {e}"}, status_code=500)
 
 
-@app.get("/documents", response_model=DocumentsResponse, responses={500: {"description": "Internal Server Error"}})
+@app.get("/documents", response_model=DocumentsResponse, responses=_ERR500)
 @tracing.instrumentation_wrapper
 async def get_documents(request: Request) -> DocumentsResponse:
+    """List available documents."""
     try:
         docs = await run_in_threadpool(example().get_documents)
         return DocumentsResponse(documents=docs)
@@ -295,9 +360,10 @@ async def get_documents(request: Request) -> DocumentsResponse:
         return JSONResponse(content={"message": f"Error occurred while fetching documents: {e}"}, status_code=500)
 
 
-@app.delete("/documents", responses={500: {"description": "Internal Server Error"}})
+@app.delete("/documents", responses=_ERR500)
 @tracing.instrumentation_wrapper
 async def delete_document(request: Request, filename: str = Query(...)) -> JSONResponse:
+    """Delete a document."""
     try:
         ok = await run_in_threadpool(example().delete_documents, [filename])
         if not ok:
@@ -306,3 +372,19 @@ async def delete_document(request: Request, filename: str = Query(...)) -> JSONR
     except Exception as e:
         log.exception("delete failed")
         return JSONResponse(content={"message": f"Failed to delete document {filename}. {e}"}, status_code=500)
+
+
+def _openapi() -> Dict[str, Any]:
+    """FastAPI's schema plus the multipart body component of POST /documents (see _UPLOAD_OPENAPI)."""
+    if app.openapi_schema is None:
+        from fastapi.openapi.utils import get_openapi
+
+        schema = get_openapi(title=app.title, version=app.version, openapi_version=app.openapi_version,
+                             description=app.description, routes=app.routes)
+        schema.setdefault("components", {}).setdefault("schemas", {})[
+            "Body_upload_document_documents_post"] = _UPLOAD_BODY_SCHEMA
+        app.openapi_schema = schema
+    return app.openapi_schema
+
+
+app.openapi = _openapi

@@ -539,15 +539,18 @@ class LLMEngine:
                           decode_block_tables=bt, max_decode_ctx=self.cfg.max_model_len, sample_rows=None,
                           tp_local_logits=self.tp_size > 1 and getattr(self.model, "supports_tp_sampling", False))
         dctx = getattr(self.model, "ctx", None)
+        # the closure holds the model / cache / workspace, never the engine: engine -> multi_graphs -> run -> engine
+        # would be a reference cycle that keeps the whole engine (KV cache, graphs) alive after `del` until a GC pass
+        model, kv, dws = self.model, self.kv, self.decode_ws
 
         def run():
             # every step first advances rows < n_valid from the previous sampled token: at j = 0 that is
             # toks[K-1], the last token of the previous run (pipelined) or the host-fed input token
             for j in range(K):
                 ops.decode_advance(toks[(j - 1) % K], ids, pos, ctx, slots, bt, n_valid)
-                logits = self.model.forward(fb, self.kv, self.decode_ws)
+                logits = model.forward(fb, kv, dws)
                 if fb.tp_local_logits:  # vocab-parallel logits: candidate exchange instead of a logits all-gather
-                    ops.sample_tp(logits, dctx, self.model.vstart, self.model.cfg.vocab_size, samp["temperature"],
+                    ops.sample_tp(logits, dctx, model.vstart, model.cfg.vocab_size, samp["temperature"],
                                   samp["top_p"], samp["top_k"], samp["seeds"], j, out=toks[j])
                 else:
                     ops.sample(logits, samp["temperature"], samp["top_p"], samp["top_k"], samp["seeds"], j,
@@ -1066,3 +1069,26 @@ class LLMEngine:
         while self.has_work():
             self.step()
         return reqs
+
+    # ------------------------------------------------------------------ teardown
+    def close(self) -> None:
+        """Release the engine's device state now: captured graphs (and their private memory pools), the paged KV
+        cache, the decode workspace and the pinned staging banks. A replacement engine (hub reload, LoRA swap, a
+        test) then sizes its KV cache against free memory, not against this engine's leftovers. The engine is
+        unusable afterwards."""
+        with self.lock:
+            if self._pending is not None and self._pending.done is not None:
+                self._pending.done.synchronize()
+            self._pending = None
+            self.graphs.clear()
+            self.multi_graphs.clear()
+            self.kv = None
+            self.decode_ws = None
+            self.stagers = []
+            self.stager = None
+            self._tok_host = self._single_host = None
+            self.requests.clear()
+            self.by_rid.clear()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+                torch.cuda.empty_cache()

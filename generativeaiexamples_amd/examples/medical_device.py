@@ -13,7 +13,7 @@ for the evaluation tool.
 from __future__ import annotations
 
 import re
-from typing import Dict, Generator, List
+from typing import Dict, Generator, List, Optional
 
 from ..chain_server.utils import get_llm
 from ..index.hbm_index import Document
@@ -29,8 +29,9 @@ DEFAULT_TEMPLATE = (
 
 
 class MedicalDeviceAssistant(MultiTurnRAG):
-    def rag_chain(self, query: str, chat_history: List[Dict[str, str]], **kwargs) -> Generator[str, None, None]:
-        conv_id = conversation_key(chat_history, query)
+    def rag_chain(self, query: str, chat_history: List[Dict[str, str]], session_id: Optional[str] = None,
+                  **kwargs) -> Generator[str, None, None]:
+        conv_id = conversation_key(chat_history, query, session_id)
         docs = self._fetch(self.store, query)
         memory = self._fetch(self.conv_store, query, conv_id) if len(self.conv_store) else []
         if not docs and not memory:

@@ -4,15 +4,17 @@ Two stores: the document store and a conversation-memory store. With a reranker,
 are retrieved from each and reranked down to top_k (chains.py:147,173-195); the answer is streamed
 and the (question, answer) turn is written back to memory.
 
-Fixed relative to the reference: memory is partitioned per conversation
-(keyed by the conversation's first user message) instead of one global collection shared by all
-users, and the fallback messages are actually delivered (the reference's generator swallowed them).
+Fixed relative to the reference: memory is partitioned per session instead of one
+global collection shared by all users (the reference's single ``conv_store``, chains.py:138). The session is the
+``X-Session-Id`` header of POST /generate (passed in as ``session_id``); a client that sends none falls back to a key
+derived from the conversation's first user message. The fallback messages are actually delivered (the reference's
+generator swallowed them).
 """
 from __future__ import annotations
 
 import hashlib
 import logging
-from typing import Dict, Generator, List
+from typing import Dict, Generator, List, Optional
 
 from ..chain_server.utils import get_llm, get_ranking_model, get_vectorstore
 from ..index.hbm_index import Document
@@ -22,7 +24,11 @@ log = logging.getLogger(__name__)
 CANDIDATES_WITH_RANKER = 40
 
 
-def conversation_key(chat_history: List[Dict[str, str]], query: str) -> str:
+def conversation_key(chat_history: List[Dict[str, str]], query: str, session_id: Optional[str] = None) -> str:
+    """Memory partition of a conversation: the explicit session id when the client sends one (two users who both
+    open with "Hi" then never share memory), else a hash of the first user message."""
+    if session_id:
+        return "s-" + hashlib.sha1(session_id.encode()).hexdigest()[:16]
     first = next((m["content"] for m in chat_history if m.get("role") == "user"), query)
     return hashlib.sha1(first.encode()).hexdigest()[:16]
 
@@ -62,8 +68,9 @@ class MultiTurnRAG(BasicRAG):
             docs = docs[: r.top_k]
         return docs
 
-    def rag_chain(self, query: str, chat_history: List[Dict[str, str]], **kwargs) -> Generator[str, None, None]:
-        conv_id = conversation_key(chat_history, query)
+    def rag_chain(self, query: str, chat_history: List[Dict[str, str]], session_id: Optional[str] = None,
+                  **kwargs) -> Generator[str, None, None]:
+        conv_id = conversation_key(chat_history, query, session_id)
         docs = self._fetch(self.store, query)
         memory = self._fetch(self.conv_store, query, conv_id) if len(self.conv_store) else []
         if not docs and not memory:

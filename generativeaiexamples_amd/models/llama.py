@@ -284,7 +284,7 @@ class LlamaModel:
         kinds: dict = {}
         for k, v in self.w.items():
             kind = k.rsplit(".", 1)[-1]
-            done = v.dec is not None if isinstance(v, ops.Fp8Weight) else getattr(v, "_gai_psw", None) is not None
+            done = v.dec is not None if isinstance(v, ops.Fp8Weight) else ops.decode_operand(v) is not None
             if kind in self.DECODE_PROJECTIONS and isinstance(v, (torch.Tensor, ops.Fp8Weight)) and not done:
                 if in_place and id(v) not in tied and ops.to_fragment_layout_(v):
                     continue

@@ -20,9 +20,8 @@ Expert parallelism, two modes:
 """
 from __future__ import annotations
 
-import os
-
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict
 
@@ -176,13 +175,44 @@ class MixtralModel(LlamaModel):
 
     def _moe_ep(self, x, ids, wts, w13, w2, residual):
         """All-to-all expert parallelism: pairs go to the rank owning their expert and come back weighted."""
-        from ..parallel import ep
-
         c = self.cfg
         # capacity: the step's largest per-rank token count (EP lockstep) x top-k - never drops a pair. Prefill-sized
         # steps (ep_exact) exchange the per-peer counts on the device and move only the valid rows; decode steps
         # move whole slabs (graph-capturable). Neither synchronises the host.
-        cap = max(self.ep_capacity_tokens, x.shape[0]) * c.top_k
+        cap_tok = max(self.ep_capacity_tokens, x.shape[0])
+        chunk = self._ep_chunk_tokens(x, cap_tok)
+        if chunk >= cap_tok:
+            return self._moe_ep_slab(x, ids, wts, w13, w2, residual, cap_tok * c.top_k)
+        # a prefill step whose per-peer segments would overflow the peer-memory buffers runs in row chunks that fit
+        # them: every rank makes the same number of exchanges (cap_tok is agreed by the lockstep), the slabs and the
+        # expert GEMM intermediates are sized by the chunk, never by W x the whole step (ADVICE r5); a rank whose
+        # rows ran out joins with one zero-weight row and drops its output
+        T, outs = x.shape[0], []
+        for lo in range(0, cap_tok, chunk):
+            hi = min(lo + chunk, T)
+            if hi > lo:
+                outs.append(self._moe_ep_slab(x[lo:hi], ids[lo:hi], wts[lo:hi], w13, w2,
+                                              None if residual is None else residual[lo:hi], chunk * c.top_k))
+            else:
+                self._moe_ep_slab(x[:1], ids[:1], torch.zeros_like(wts[:1]), w13, w2, None, chunk * c.top_k)
+        return torch.cat(outs)
+
+    def _ep_chunk_tokens(self, x, cap_tok: int) -> int:
+        """Tokens per MoE exchange of a prefill-sized EP step: all of them while one per-peer segment of capacity
+        cap_tok x top_k rows (D + 8 bf16 lanes each) fits the peer-memory slot, else as many as fit.
+        GAI_EP_PREFILL_CHUNK_TOKENS forces a chunk size (tests; the gloo control plane has no slot)."""
+        forced = int(os.environ.get("GAI_EP_PREFILL_CHUNK_TOKENS", "0"))
+        if forced > 0 and self.ep_exact:
+            return forced
+        if not (self.ep_exact and self.ep_xchg is not None and x.is_cuda):
+            return cap_tok
+        row_bytes = (x.shape[1] + 8) * x.element_size()
+        return max(1, self.ep_xchg.slot_bytes // (row_bytes * self.cfg.top_k))
+
+    def _moe_ep_slab(self, x, ids, wts, w13, w2, residual, cap: int):
+        from ..parallel import ep
+
+        c = self.cfg
         rows, eid, plan = ep.dispatch_padded(x, ids, c.num_experts, capacity=cap, group=self.ep_group,
                                              xchg=self.ep_xchg, exact_counts=self.ep_exact)
         y = ep.local_experts_padded(rows, eid, w13, w2)

@@ -319,8 +319,14 @@ class MllamaModel(LlamaModel):
             return
         for i in range(V.num_layers + V.num_global_layers):
             p = f"v{i}."
-            self.w[p + "qkv"].view(3, H, hp, -1)[:, :, hd:].zero_()
-            self.w[p + "o"].view(-1, H, hp)[:, :, hd:].zero_()
+            for k, view in (("qkv", lambda t: t.view(3, H, hp, -1)[:, :, hd:]), ("o", lambda t: t.view(-1, H, hp)[:, :, hd:])):
+                w = self.w[p + k]
+                if ops.is_frag(w):  # zero the padding in row-major order, then store fragment-ordered again
+                    nat = ops.natural_weight(w)
+                    view(nat).zero_()
+                    w.copy_(ops.shuffle_fragments(nat))
+                elif isinstance(w, torch.Tensor):
+                    view(w).zero_()
 
     def quantize_fp8(self, vision: bool = True, text: bool = True) -> int:
         """e4m3fn per-channel weights for the transformer linears (BASELINE config 4 'CDNA4 fp8 MFMA')."""
@@ -339,8 +345,7 @@ class MllamaModel(LlamaModel):
         c, V = self.cfg, self.mcfg.vision
         hd, hp, H = V.head_dim, V.head_dim_padded, V.num_heads
 
-        def put(name, t):
-            self.w[name].copy_(t.to(self.dtype))
+        put = self._put  # re-shuffles into the fragment-ordered layout a serving engine may have given the weight
 
         lm = "language_model.model."
         put("embed", sd[lm + "embed_tokens.weight"])
@@ -364,7 +369,7 @@ class MllamaModel(LlamaModel):
             else:
                 put(p + "qkv", torch.cat([sd[h + f"self_attn.{n}_proj.weight"] for n in "qkv"]))
                 put(p + "o", sd[h + "self_attn.o_proj.weight"])
-            self.w[p + "gate_up"].copy_(ops.interleave_gate_up(g, u).to(self.dtype))
+            put(p + "gate_up", ops.interleave_gate_up(g, u))
             put(p + "down", dn)
         put("norm", sd[lm + "norm.weight"])
         put("lm_head", sd["language_model.lm_head.weight"])

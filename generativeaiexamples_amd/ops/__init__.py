@@ -136,7 +136,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     x2 = x.reshape(M, K)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
-    psw = getattr(w, "_gai_psw", None)
+    psw = decode_operand(w)
     if psw is not None and M <= 64:  # decode: weight stream from the fragment-shuffled copy
         if out is None:
             out = torch.empty(*lead, ncol, dtype=out_dtype, device=x.device)
@@ -164,7 +164,7 @@ def linear_add_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
     if (x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and M <= 64
             and native().gemm_splitk_fusable_norm(M, N, K)):
         nat = native()
-        psw = getattr(w, "_gai_psw", None)
+        psw = decode_operand(w)
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x.device)
         out = torch.empty_like(residual)
         nat.gemm_splitk_add_rmsnorm(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, residual,
@@ -183,7 +183,7 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     M = x.numel() // K
     if x.is_cuda and not isinstance(w, Fp8Weight) and _SPLITK and _GEMM_FORCE == 0 and 1 <= M <= 64:
         nat = native()
-        psw = getattr(w, "_gai_psw", None)
+        psw = decode_operand(w)
         ws = torch.empty(nat.gemm_splitk_ws_floats(M, w.shape[0], K), dtype=torch.float32, device=x.device)
         if nat.gemm_rope_kv(x.reshape(M, K).contiguous(), w if psw is None else psw, bias, positions, cos_sin, slots,
                             q_out, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale, ws, psw is not None,
@@ -269,9 +269,16 @@ def to_fragment_layout_(w: torch.Tensor, rows_per_chunk: int = 4096) -> bool:
     if not psw_qualifies(w) or isinstance(w, Fp8Weight) or w.numel() * 2 >= (1 << 31) or not w.is_contiguous():
         return False
     shuffle_fragments_(w, rows_per_chunk)
-    w._gai_frag = True
-    w._gai_psw = w  # the decode paths' fragment-ordered operand is the weight itself
-    return True
+    w._gai_frag = True  # the decode paths' fragment-ordered operand is the weight itself (decode_operand); no
+    return True         # self-referencing attribute: that would be a reference cycle keeping the weight alive
+
+
+def decode_operand(w):
+    """The fragment-ordered bf16 operand the decode kernels stream for ``w``: the weight itself when it is stored
+    fragment-ordered, its attached decode copy in the two-layout mode, else None."""
+    if is_frag(w):
+        return w
+    return getattr(w, "_gai_psw", None)
 
 
 def psw_qualifies(w) -> bool:
@@ -601,7 +608,7 @@ def qkv_fold_partials(x: torch.Tensor, w, bias, k_cache, head_dim: int, ws: "Dec
     if not 1 <= M <= 64:
         return None
     nat = native()
-    psw = getattr(w, "_gai_psw", None)
+    psw = decode_operand(w)
     slabs = torch.empty(nat.gemm_splitk_ws_floats(M, N, K), dtype=torch.float32, device=x.device)
     ks = nat.gemm_qkv_partials(x.reshape(M, K).contiguous(), w if psw is None else psw, slabs, psw is not None)
     return (slabs, int(ks)) if ks else None

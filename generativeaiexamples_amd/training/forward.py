@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from .. import ops
 from .lora import LoRAAdapter
 from .tp import copy_to_tp, gather_last, reduce_from_tp
 
@@ -28,7 +29,9 @@ def _norm(model, x, name):
 
 
 def _lin(x, w, lora: LoRAAdapter | None, layer: int, target: str, bias=None):
-    y = x @ w.t()
+    # a frozen base weight may be stored in the fragment-ordered inference layout (an engine serves the same model):
+    # read its row-major values (FullTrainer, which updates the weights, refuses such models)
+    y = x @ ops.natural_weight(w).t()
     if bias is not None:
         y = y + bias
     if lora is not None:
@@ -95,7 +98,7 @@ def lm_loss(model, lora: LoRAAdapter | None, ids: torch.Tensor, labels: torch.Te
         else:
             x = block(x, i)
     h = copy_to_tp(_norm(model, x, "norm"), ctx)
-    logits = gather_last(h @ w["lm_head"].t(), ctx)[..., : c.vocab_size].float()
+    logits = gather_last(h @ ops.natural_weight(w["lm_head"]).t(), ctx)[..., : c.vocab_size].float()
     if not bool((labels[:, 1:] != -100).any()):  # nothing to learn in this micro-batch
         return logits.sum() * 0.0
     return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]), labels[:, 1:].reshape(-1), ignore_index=-100)

@@ -7,6 +7,8 @@ from typing import Dict, Tuple
 
 import torch
 
+from .. import ops
+
 DEFAULT_TARGETS = ("qkv", "o")
 
 
@@ -73,7 +75,10 @@ class LoRAAdapter:
             li, t = base.split(".", 1)
             d = self.delta_weight(int(li[1:]), t)
             w = model.w[base]
-            w.copy_((w.float() + d.to(w.device)).to(w.dtype))
+            # a weight an engine rewrote into the fragment-ordered inference layout: add the row-major delta to its
+            # row-major values, then store them fragment-ordered again (LlamaModel._put does the same on loads)
+            merged = (ops.natural_weight(w).float() + d.to(w.device)).to(w.dtype)
+            w.copy_(ops.shuffle_fragments(merged) if ops.is_frag(w) else merged)
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return {k: v.detach().float().cpu().contiguous() for k, v in self.params.items()}

@@ -114,10 +114,14 @@ def test_tp_linear_all_reduce_overlap(tmp_path):
         assert d["torch.bfloat16"] < 1e-2
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_ep_engine_matches_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,chunk", [(2, 0), (4, 0), (8, 0), (2, 5)])
+def test_ep_engine_matches_single_rank(tmp_path, monkeypatch, world, chunk):
     """Mixtral EP mode: DP attention + experts over the ranks with all-to-all exchange, lockstep steps (ranks
-    own different request sets): every rank's greedy tokens equal the single-process model's."""
+    own different request sets): every rank's greedy tokens equal the single-process model's. chunk > 0: prefill
+    exchanges run in row chunks of that many tokens (the path for slabs beyond the peer-memory buffers), ranks that
+    run out of rows join with a zero-weight dummy row."""
+    if chunk:
+        monkeypatch.setenv("GAI_EP_PREFILL_CHUNK_TOKENS", str(chunk))
     mp.spawn(W.ep_engine_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         d = json.loads((tmp_path / f"ep_{r}.json").read_text())

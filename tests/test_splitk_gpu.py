@@ -102,8 +102,8 @@ def test_engine_preshuffles_projections(cuda):
 
     m = LlamaModel(LlamaConfig.tiny(), device=cuda).random_init(0)
     added = m.preshuffle_decode_weights()
-    assert added > 0 and getattr(m.w["l0.down"], "_gai_psw", None) is not None  # K=512 qualifies
-    assert getattr(m.w["l0.attn_norm"], "_gai_psw", None) is None
+    assert added > 0 and ops.decode_operand(m.w["l0.down"]) is not None  # K=512 qualifies
+    assert ops.decode_operand(m.w["l0.attn_norm"]) is None
 
 
 def test_preshuffle_budget_takes_whole_kinds_by_priority(cuda):
@@ -118,10 +118,10 @@ def test_preshuffle_budget_takes_whole_kinds_by_priority(cuda):
     budget = size("gate_up") + size("down") + 1  # nothing after them fits
     assert m.preshuffle_decode_weights(budget_bytes=budget) == size("gate_up") + size("down")
     for i in range(m.cfg.num_layers):
-        assert getattr(m.w[f"l{i}.gate_up"], "_gai_psw", None) is not None
-        assert getattr(m.w[f"l{i}.down"], "_gai_psw", None) is not None
-        assert getattr(m.w[f"l{i}.qkv"], "_gai_psw", None) is None and getattr(m.w[f"l{i}.o"], "_gai_psw", None) is None
-    assert getattr(m.w["lm_head"], "_gai_psw", None) is None
+        assert ops.decode_operand(m.w[f"l{i}.gate_up"]) is not None
+        assert ops.decode_operand(m.w[f"l{i}.down"]) is not None
+        assert ops.decode_operand(m.w[f"l{i}.qkv"]) is None and ops.decode_operand(m.w[f"l{i}.o"]) is None
+    assert ops.decode_operand(m.w["lm_head"]) is None
 
 
 @pytest.mark.parametrize("M", [1, 17, 64])
