@@ -180,6 +180,10 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   check_i32(ctx_lens, "ctx_lens");
   check_bf16(out, "out");
   const int D = q.size(-1);
+  // q may be a strided view of the packed QKV rows ([T, Hq, D] with row stride q.stride(0)): encoders pass it
+  // without a copy
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == D && q.stride(0) >= Hq * D,
+              "attn_prefill: q must be [T, Hq, D] with dense heads");
   float* lse_p = nullptr;
   if (lse) {
     check_f32(*lse, "lse");
@@ -189,7 +193,22 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   gai_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                    block_tables.size(1), tiles.data_ptr<int>(), tiles.numel() / 2, cu_q.data_ptr<int>(),
                    ctx_lens.data_ptr<int>(), out.data_ptr(), Hq, Hkv, D, (float)scale, causal ? 1 : 0, lse_p, f8,
-                   (float)k_scale, (float)v_scale, cur_stream());
+                   (float)k_scale, (float)v_scale, cur_stream(), (int)q.stride(0));
+}
+
+void kv_pack(const Tensor& qkv, const Tensor& blk_tok, const Tensor& blk_n, Tensor& k_cache, Tensor& v_cache,
+             int64_t Hq, int64_t Hkv, int64_t D) {
+  check_bf16(qkv, "qkv");
+  check_i32(blk_tok, "blk_tok");
+  check_i32(blk_n, "blk_n");
+  TORCH_CHECK(kv_cache_fp8(k_cache, v_cache) == 0, "kv_pack: bf16 caches only");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous() && qkv.size(1) == (Hq + 2 * Hkv) * D, "kv_pack: qkv [T, (Hq + 2 Hkv) D]");
+  TORCH_CHECK(k_cache.size(-2) == 16 && k_cache.size(-1) == D && v_cache.size(-1) == 16 && k_cache.size(1) == Hkv,
+              "kv_pack: bad kv cache layout");
+  TORCH_CHECK(blk_tok.numel() == blk_n.numel() && blk_tok.numel() <= k_cache.size(0), "kv_pack: page list");
+  gai_kv_pack(qkv.data_ptr(), (int)qkv.size(1), (int)(Hq * D), (int)((Hq + Hkv) * D), blk_tok.data_ptr<int>(),
+              blk_n.data_ptr<int>(), (int)blk_tok.numel(), k_cache.data_ptr(), v_cache.data_ptr(), (int)Hkv, (int)D,
+              cur_stream());
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -846,6 +865,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vit_embed", &vit_embed);
   m.def("quant_rows_fp8", &quant_rows_fp8);
   m.def("attn_prefill", &attn_prefill);
+  m.def("kv_pack", &kv_pack);
   m.def("attn_prefill_rows_per_tile", [](int64_t hq, int64_t hkv, int64_t d) { return gai_attn_prefill_rows_per_tile(hq, hkv, d); },
         py::arg("hq"), py::arg("hkv"), py::arg("d") = 128);
   m.def("attn_prefill_set_hl", [](int64_t hl) { gai_attn_prefill_set_hl((int)hl); });

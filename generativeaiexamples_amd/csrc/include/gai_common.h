@@ -75,10 +75,26 @@ __device__ __forceinline__ bf16x8 load_kv8(const fp8* p, float s) {
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), branch-free: one v_rcp_f32, one v_exp_f32 and ~10 FMAs per
+// element. The device libm erff is piecewise with data-dependent branches: in the 256x256 GEMM epilogue of an encoder
+// FFN-up projection (K = 1024, so the epilogue is not hidden behind a long main loop) it made the bias + GELU GEMM
+// 2x slower than the bias-only one (e5-large ingest at M = 65536: 990 vs ~450 us per layer, profiles/r6).
+__device__ __forceinline__ float erf_fast(float x) {
+  const float z = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.0f - p * t * __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  return copysignf(y, x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// tanh-GELU as x * sigmoid(2u): 0.5 x (1 + tanh(u)) == x / (1 + e^{-2u}), no libm tanhf
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+  const float u = k0 * fmaf(k1 * x, x * x, x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.0f * 1.4426950408889634f * u));
 }
 
 // Block-level reduction for up to 1024 threads (16 waves). `scratch` holds >= 16 floats.

@@ -14,6 +14,11 @@ void gai_layernorm(const void* x, const void* residual_in, void* residual_out, c
 
 // rope_kv.hip
 // kv_fp8: caches hold OCP e4m3fn x / {k,v}_scale (fp8 KV cache option); scales are ignored for bf16 caches
+// Encoder self-attention K / V (no RoPE): the packed QKV rows of each transient page's tokens -> the page's K [16][D]
+// and V^T [D][16] images, whole-page 16-B stores (rope_kv.hip kv_pack_kernel). blk_tok[b] / blk_n[b]: first token and
+// row count of page b (rows past blk_n are zeroed).
+void gai_kv_pack(const void* qkv, int ld, int koff, int voff, const int* blk_tok, const int* blk_n, int nblk,
+                 void* k_cache, void* v_cache, int Hkv, int D, hipStream_t st);
 void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, const int* slots, void* q_out,
                        void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, int kv_fp8,
                        float k_scale, float v_scale, hipStream_t st);
@@ -65,7 +70,7 @@ int gai_gemm_dec2_partials(const void* A, const void* W, int M, int N, int K, fl
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
                       int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
-                      float v_scale, hipStream_t st);
+                      float v_scale, hipStream_t st, int q_ld = 0);
 int gai_attn_prefill_rows_per_tile(int Hq, int Hkv, int D = 128);
 void gai_attn_prefill_set_hl(int hl);
 // Decode QKV tail folded into the decode-attention launch: the split-K QKV partial slabs part[ks][B][n] (n = (Hq +

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
-    float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale, int xcd) {
+    float scale, int causal, float* __restrict__ lse, float k_scale, float v_scale, int xcd, int q_ld) {
   using Cfg = PrefillCfg<D>;
   static_assert(HL == 1 || HPW % HL == 0, "a wave's heads come from one workgroup head group");
   constexpr int WPR = HPW / HL;  // waves per row group
@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   char* sq = smem + 2 * Cfg::BUF + wid * (HL * 32 * Cfg::KRS);
 #pragma unroll
   for (int j = 0; j < HL; ++j) {
-    const bf16* qp = q + ((size_t)(qbeg + min(qrow, qlen - 1)) * Hq + head + j) * D + 8 * h;
+    // q rows are q_ld elements apart: Hq * D for a q tensor of its own, the packed QKV row for encoders
+    const bf16* qp = q + (size_t)(qbeg + min(qrow, qlen - 1)) * q_ld + (size_t)(head + j) * D + 8 * h;
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
       const bf16x8 v = load8(qp + 16 * t);
@@ -828,8 +829,9 @@ void gai_attn_prefill_set_hl(int hl) { g_prefill_hl = hl == 2 ? 2 : 1; }
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
                       int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
-                      float v_scale, hipStream_t st) {
+                      float v_scale, hipStream_t st, int q_ld) {
   if (ntiles == 0) return;
+  if (q_ld <= 0) q_ld = Hq * D;
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
   // XCD kv-head placement for causal decoder prefill at head_dim >= 128 (long K/V prefixes re-read by many q tiles).
@@ -849,13 +851,13 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
       set_max_lds(kern, lds);
       kern<<<dim3(ntiles, Hq / 4), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,
                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
-                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd);
+                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);
     } else {
       auto kern = attn_prefill_kernel<128, 4, bf16, 2>;
       set_max_lds(kern, lds);
       kern<<<dim3(ntiles, Hq / 4), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache,
                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
-                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd);
+                                                   Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);
     }
     GAI_LAUNCH_CHECK();
     return;
@@ -868,13 +870,13 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
       set_max_lds(kern, lds);                                                                                  \
       kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,  \
                                                     block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd);       \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);       \
     } else {                                                                                                   \
       auto kern = attn_prefill_kernel<DD, HP, bf16>;                                                           \
       set_max_lds(kern, lds);                                                                                  \
       kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, \
                                                     block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd);       \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);       \
     }                                                                                                          \
     GAI_LAUNCH_CHECK();                                                                                        \
     return;                                                                                                    \

@@ -216,6 +216,18 @@ __device__ __forceinline__ float epi_act(float v, const bf16* bias, int n) {
   return v;
 }
 
+// epi_act with the bias value already loaded
+template <int EPI>
+__device__ __forceinline__ float epi_act_b(float v, float b) {
+  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESIDUAL || EPI == EPI_BIAS_RELU ||
+      EPI == EPI_BIAS_QUICKGELU)
+    v += b;
+  if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+  if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+  if (EPI == EPI_BIAS_QUICKGELU) v = quick_gelu(v);
+  return v;
+}
+
 // Epilogue of the swapped-operand 256x256 kernels, one 16-row group: lane holds C[m = mrow + (lane&15)]
 // [n = nb + 16j + 4q + r] (q = lane>>4). Tile pairs (2jp, 2jp+1) are merged by one v_permlane16_swap
 // per value so each lane owns 8 consecutive columns (16-byte stores); SwiGLU pairs are (gate, up).
@@ -265,13 +277,21 @@ __device__ __forceinline__ void epilogue_rows(const f32x4 (&acc_i)[NJ], void* C,
     }
     return;
   }
+  constexpr bool kBias = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESIDUAL || EPI == EPI_BIAS_RELU ||
+                        EPI == EPI_BIAS_QUICKGELU;
 #pragma unroll
   for (int jp = 0; jp < NJ / 2; ++jp) {
     float x0[4], x1[4];
+    // the 4 columns a lane holds per tile are consecutive and N % 16 == 0 here: one 8-B bias load each
+    bf16x4 b0 = {}, b1 = {};
+    if constexpr (kBias) {
+      b0 = *reinterpret_cast<const bf16x4*>(bias + min(nb + 32 * jp + 4 * q, N - 4));
+      b1 = *reinterpret_cast<const bf16x4*>(bias + min(nb + 32 * jp + 16 + 4 * q, N - 4));
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      x0[r] = epi_act<EPI>(acc_i[2 * jp][r], bias, min(nb + 32 * jp + 4 * q + r, N - 1));
-      x1[r] = epi_act<EPI>(acc_i[2 * jp + 1][r], bias, min(nb + 32 * jp + 16 + 4 * q + r, N - 1));
+      x0[r] = epi_act_b<EPI>(acc_i[2 * jp][r], (float)b0[r]);
+      x1[r] = epi_act_b<EPI>(acc_i[2 * jp + 1][r], (float)b1[r]);
       swap16(x0[r], x1[r]);
     }
     // lanes q=0/2 now own tile 2jp columns 8(q>>1) .. +7; q=1/3 own tile 2jp+1

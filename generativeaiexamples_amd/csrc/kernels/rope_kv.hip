@@ -39,7 +39,65 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   rope_kv_store<D>(x1, x2, t, h, i0, pos, cos_sin, slots, q_out, k_cache, v_cache, Hq, Hkv, rope, inv_ks, inv_vs);
 }
 
+// Encoder self-attention (no RoPE, K / V straight from the packed QKV rows): one workgroup per (transient page, kv
+// head) writes the page's K image [16][D] and V^T image [D][16] whole, with 16-B stores; V is transposed through LDS.
+// Replaces rope_kv_kernel's per-(token, head) scatter for encoders, whose V^T half is 2-B stores 32 B apart and which
+// also copied q (the attention reads q from the QKV rows, q_ld): e5-large ingest at 65536 tokens spent 379 us per
+// layer there (profiles/r6).
+template <int D>
+__global__ __launch_bounds__(64) void kv_pack_kernel(const bf16* __restrict__ qkv, int ld, int koff, int voff,
+                                                     const int* __restrict__ blk_tok, const int* __restrict__ blk_n,
+                                                     bf16* __restrict__ k_cache, bf16* __restrict__ v_cache, int Hkv) {
+  constexpr int CPR = D / 8;       // 16-B chunks per row
+  constexpr int PIECES = 16 * CPR;
+  __shared__ __attribute__((aligned(16))) bf16 vs[16][D + 8];  // V rows, padded against bank conflicts
+  const int b = blockIdx.x, g = blockIdx.y, lane = threadIdx.x;
+  const int t0 = blk_tok[b], n = blk_n[b];
+  bf16* kp = k_cache + ((size_t)b * Hkv + g) * 16 * D;
+  bf16* vp = v_cache + ((size_t)b * Hkv + g) * D * 16;
+#pragma unroll
+  for (int p = lane; p < PIECES; p += 64) {
+    const int r = p / CPR, c = (p % CPR) * 8;
+    bf16x8 kv = {}, vv = {};
+    if (r < n) {
+      const bf16* src = qkv + (size_t)(t0 + r) * ld + (size_t)g * D + c;
+      kv = load8(src + koff);
+      vv = load8(src + voff);
+    }
+    store8(kp + r * D + c, kv);
+    *reinterpret_cast<bf16x8*>(&vs[r][c]) = vv;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = lane; p < PIECES; p += 64) {  // V^T row d = 16 tokens = two 16-B pieces
+    const int d = p >> 1, h8 = (p & 1) * 8;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = vs[h8 + e][d];
+    store8(vp + d * 16 + h8, o);
+  }
+}
+
 }  // namespace
+
+void gai_kv_pack(const void* qkv, int ld, int koff, int voff, const int* blk_tok, const int* blk_n, int nblk,
+                 void* k_cache, void* v_cache, int Hkv, int D, hipStream_t st) {
+  if (nblk == 0) return;
+  const dim3 grid(nblk, Hkv);
+#define GAI_KVP(DD)                                                                                          \
+  if (D == DD) {                                                                                             \
+    kv_pack_kernel<DD><<<grid, 64, 0, st>>>((const bf16*)qkv, ld, koff, voff, blk_tok, blk_n, (bf16*)k_cache, \
+                                            (bf16*)v_cache, Hkv);                                            \
+    GAI_LAUNCH_CHECK();                                                                                      \
+    return;                                                                                                  \
+  }
+  GAI_KVP(64)
+  GAI_KVP(96)
+  GAI_KVP(128)
+  GAI_KVP(256)
+#undef GAI_KVP
+  gai_launch_error(__FILE__, __LINE__, "kv_pack: head_dim must be 64, 96, 128 or 256");
+}
 
 void gai_rope_kv_write(const void* qkv, const int* pos, const float* cos_sin, const int* slots, void* q_out,
                        void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D, int rope, int kv_fp8,

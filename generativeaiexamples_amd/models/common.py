@@ -127,6 +127,18 @@ class PackedAttention:
         self.ctx = torch.tensor(kv_lens, dtype=torch.int32).to(dev, non_blocking=True)
         self.tiles = (ops.build_prefill_tiles(q_lens, self.H, self.Hkv, dev, head_dim=head_dim) if dev.type == "cuda"
                       else None)
+        # self-attention without RoPE (BERT / E5 / CLIP / ViT encoders): every page's K / V^T image is packed straight
+        # from the QKV rows by one kernel (ops.kv_pack) and the attention reads q from those rows - no q copy, no
+        # per-(token, head) scatter
+        self.pack = None
+        if cos_sin is None and kv_lens == q_lens and dtype == torch.bfloat16:
+            blk_tok, blk_n = [], []
+            for b, n in enumerate(kv_lens):
+                for i in range(nbs[b]):
+                    blk_tok.append(cu[b] + BS * i)
+                    blk_n.append(min(BS, n - BS * i))
+            self.pack = (torch.tensor(blk_tok, dtype=torch.int32).to(dev, non_blocking=True),
+                         torch.tensor(blk_n, dtype=torch.int32).to(dev, non_blocking=True))
         self.k_cache = torch.zeros(offs[-1] + 1, self.Hkv, BS, head_dim, device=dev, dtype=dtype)
         self.v_cache = torch.zeros(offs[-1] + 1, self.Hkv, head_dim, BS, device=dev, dtype=dtype)
         self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)
@@ -137,9 +149,14 @@ class PackedAttention:
     def __call__(self, qkv: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """qkv [T, (H + 2 Hkv) * hd] -> attention output [T, H * hd]."""
         from .. import ops
-        ops.rope_kv_write(qkv, self.positions, self.cs, self.slots, self.q, self.k_cache, self.v_cache, self.H,
-                          self.Hkv, self.hd, rope=self.rope)
+        if self.pack is not None:
+            ops.kv_pack(qkv, self.pack[0], self.pack[1], self.k_cache, self.v_cache, self.H, self.Hkv, self.hd)
+            q = qkv.view(self.T, self.H + 2 * self.Hkv, self.hd)[:, : self.H]
+        else:
+            ops.rope_kv_write(qkv, self.positions, self.cs, self.slots, self.q, self.k_cache, self.v_cache, self.H,
+                              self.Hkv, self.hd, rope=self.rope)
+            q = self.q
         o = torch.empty_like(self.q) if out is None else out.view(self.T, self.H, self.hd)
-        ops.attention_prefill(self.q, self.k_cache, self.v_cache, self.block_tables, self.cu_q, self.ctx, scale,
+        ops.attention_prefill(q, self.k_cache, self.v_cache, self.block_tables, self.cu_q, self.ctx, scale,
                               causal=self.causal, tiles=self.tiles, q_lens=self.q_lens, out=o)
         return o.view(self.T, self.H * self.hd)

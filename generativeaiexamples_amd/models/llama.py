@@ -28,7 +28,7 @@ import json
 import math
 import os
 from dataclasses import asdict, dataclass
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -799,6 +799,63 @@ class LlamaModel:
                 g = (act * gu[:, :, 1]).reshape(T, -1)
             h = h + g @ w[p + "down"].t() + bias(p + "down_b")
         return norm(h, "norm") @ w["lm_head"].t()
+
+    @torch.no_grad()
+    def reference_logits_at(self, token_ids: torch.Tensor, rows: List[int], device="cuda",
+                            q_chunk: int = 256) -> torch.Tensor:
+        """fp32 logits [len(rows), vocab] of a long sequence at the given positions, in plain PyTorch on ``device``
+        (the long-context oracle: reference_forward's [T, T] score matrix would be 128 GB at T = 32K). RMSNorm /
+        SwiGLU Llama layout, TP = 1. Causal attention runs in query chunks of ``q_chunk`` rows against the keys so
+        far; the last layer computes queries, attention and the MLP for ``rows`` only."""
+        c, dev = self.cfg, torch.device(device)
+        assert c.norm == "rms" and c.mlp == "swiglu" and not c.qk_norm and self.ctx.tp_size == 1
+        T, hd, hq, hkv = token_ids.numel(), c.head_dim, self.hq, self.hkv
+        rep = hq // hkv
+
+        def W(name):
+            return ops.natural_weight(self.w[name]).to(dev, torch.float32)
+
+        def rms(x, g):
+            return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + c.rms_eps) * g
+
+        cs = self.cos_sin[:T].to(dev)
+        cos, sin = cs[:, None, : hd // 2], cs[:, None, hd // 2:]
+
+        def rope(t, idx):
+            a, b = t[..., : hd // 2], t[..., hd // 2:]
+            return torch.cat([a * cos[idx] - b * sin[idx], b * cos[idx] + a * sin[idx]], -1)
+
+        h = W("embed")[token_ids.long().to(dev)]
+        if c.embed_scale:
+            h = h * self.embed_multiplier
+        sel = torch.tensor(rows, dtype=torch.long, device=dev)
+        all_rows = torch.arange(T, device=dev)
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            last = i + 1 == c.num_layers
+            wqkv, wo, wgu, wd = W(p + "qkv"), W(p + "o"), W(p + "gate_up"), W(p + "down")
+            x = rms(h, W(p + "attn_norm"))
+            kv = (x @ wqkv[hq * hd:].t()).view(T, 2 * hkv, hd)
+            k, v = rope(kv[:, :hkv], all_rows), kv[:, hkv:]
+            qrows = sel if last else all_rows
+            out = torch.empty(qrows.numel(), hq * hd, device=dev)
+            for s in range(0, qrows.numel(), q_chunk):
+                r = qrows[s:s + q_chunk]
+                q = rope((x[r] @ wqkv[: hq * hd].t()).view(-1, hq, hd), r)
+                kmax = int(r.max()) + 1
+                kk = k[:kmax].repeat_interleave(rep, 1)
+                vv = v[:kmax].repeat_interleave(rep, 1)
+                att = torch.einsum("qhd,khd->hqk", q, kk) * self.scale
+                att = att.masked_fill(torch.arange(kmax, device=dev)[None, None, :] > r[None, :, None], float("-inf"))
+                out[s:s + r.numel()] = torch.einsum("hqk,khd->qhd", att.softmax(-1), vv).reshape(r.numel(), -1)
+                del att, kk, vv
+            hr = h[qrows] + out @ wo.t()
+            xm = rms(hr, W(p + "mlp_norm"))
+            gu = (xm @ wgu.t()).reshape(hr.shape[0], -1, 2, 16)
+            g = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(hr.shape[0], -1)
+            h = hr + g @ wd.t()
+            del wqkv, wo, wgu, wd
+        return (rms(h, W("norm")) @ W("lm_head").t()).float().cpu()
 
     def config_dict(self):
         return asdict(self.cfg)

@@ -178,6 +178,13 @@ class _TileMaskAttention(PackedAttention):
         self.q = torch.empty(self.T, self.H, head_dim, device=dev, dtype=dtype)
         self.rope = False
         self.cs = torch.zeros(1, head_dim, dtype=torch.float32, device=dev)
+        # every image's tokens fill its nb pages in order: packed straight from the QKV rows (PackedAttention.pack)
+        self.pack = None
+        if dtype == torch.bfloat16:
+            tok = [b * L + BS * i for b in range(len(nvalid)) for i in range(nb)]
+            cnt = [min(BS, L - BS * i) for _ in nvalid for i in range(nb)]
+            self.pack = (torch.tensor(tok, dtype=torch.int32).to(dev, non_blocking=True),
+                         torch.tensor(cnt, dtype=torch.int32).to(dev, non_blocking=True))
 
 
 @dataclass

@@ -446,6 +446,23 @@ def rope_kv_write(qkv, positions, cos_sin, slots, q_out, k_cache, v_cache, Hq, H
                            v_scale)
 
 
+def kv_pack(qkv, blk_tok, blk_n, k_cache, v_cache, Hq: int, Hkv: int, D: int) -> None:
+    """Encoder self-attention K / V (no RoPE) from the packed QKV rows [T, (Hq + 2 Hkv) D] into the pages of a transient
+    paged cache: page b holds tokens blk_tok[b] .. + blk_n[b] (K [16][D], V^T [D][16]; rows past blk_n zeroed)."""
+    if not qkv.is_cuda:
+        kv = qkv.view(qkv.shape[0], Hq + 2 * Hkv, D)
+        nb = blk_tok.numel()
+        k_cache[:nb].zero_()
+        v_cache[:nb].zero_()
+        pages = torch.repeat_interleave(torch.arange(nb), blk_n.long())
+        rows = torch.cat([torch.arange(n) for n in blk_n.tolist()]) if nb else pages
+        tok = blk_tok.long()[pages] + rows
+        k_cache[pages, :, rows] = kv[tok, Hq:Hq + Hkv].to(k_cache.dtype)
+        v_cache[pages, :, :, rows] = kv[tok, Hq + Hkv:].to(v_cache.dtype)
+        return
+    native().kv_pack(qkv.contiguous(), blk_tok, blk_n, k_cache, v_cache, Hq, Hkv, D)
+
+
 def prefill_rows_per_tile(Hq: int, Hkv: int, head_dim: int = 128) -> int:
     """Query rows per attention_prefill tile; the kernel launcher owns the choice (it follows the heads per wave of
     the prefill kernel, attention.hip prefill_hl), so GPU builds ask it."""

@@ -52,3 +52,21 @@ def test_encoder_hip_kernels_match_transformers(cuda, hidden, heads):
         cos = torch.nn.functional.cosine_similarity(h[o:o + len(t)], ref, dim=-1)
         assert cos.min() > 0.995, cos.min()
         o += len(t)
+
+
+def test_kv_pack_cpu_matches_rope_kv_writer():
+    """ops.kv_pack's CPU path == rope_kv_write with rotation off (the transient encoder pages)."""
+    import torch
+
+    from generativeaiexamples_amd import ops
+    from generativeaiexamples_amd.models.common import PackedAttention
+
+    lens, H, D = [3, 16, 40], 2, 64
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * H * D).to(torch.bfloat16)
+    a = PackedAttention(lens, H, D, "cpu")
+    ops.kv_pack(qkv, a.pack[0], a.pack[1], a.k_cache, a.v_cache, H, H, D)
+    k2, v2 = torch.zeros_like(a.k_cache), torch.zeros_like(a.v_cache)
+    ops.rope_kv_write(qkv, a.positions, a.cs, a.slots, torch.empty(T, H, D, dtype=torch.bfloat16), k2, v2, H, H, D,
+                      rope=False)
+    assert torch.equal(a.k_cache, k2) and torch.equal(a.v_cache, v2)
