@@ -172,7 +172,8 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& tiles, const Tensor& cu_q, const Tensor& ctx_lens, Tensor& out, int64_t Hq,
                   int64_t Hkv, double scale, bool causal, const optional<Tensor>& lse, double k_scale,
                   double v_scale) {
-  check_bf16(q, "q");
+  // q: contiguous, or a row-strided view of the packed QKV rows (checked below)
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16, "q must be a bfloat16 GPU tensor");
   const int f8 = kv_cache_fp8(k_cache, v_cache);
   check_i32(block_tables, "block_tables");
   check_i32(tiles, "tiles");

@@ -19,7 +19,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from blas_ab import enable_tuned_blas  # noqa: E402  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
-          "e5_ffn_up": (4096, 1024), "e5_qkv": (3072, 1024)}
+          "e5_ffn_up": (4096, 1024), "e5_qkv": (3072, 1024), "e5_o": (1024, 1024), "e5_down": (1024, 4096),
+          # one rank of Llama-3-70B at TP = 8 (tools/tp_rank_profile.py)
+          "tp8_qkv": (1280, 8192), "tp8_o": (8192, 1024), "tp8_gate_up": (7168, 8192), "tp8_down": (8192, 3584)}
 
 
 def timeit(fn, iters=10):
