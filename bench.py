@@ -256,7 +256,7 @@ def main():
     index = HBMIndex(bcfg.hidden_size, "cosine", device=dev, capacity=args.index_size)
     ct = args.chunk_tokens
     index.add_random(args.index_size, seed=100 + rank, doc_fn=lambda r: synthetic.chunk_document(r, ct))
-    sharded = ShardedIndex(index)
+    sharded = ShardedIndex(index, max_queries=args.batch)  # every rank embeds args.batch queries per step: sync-free
     log(f"index ready: {args.index_size} x {bcfg.hidden_size} per shard, {world} shard(s)")
 
     # ---------------- engine

@@ -63,7 +63,7 @@ def run(args, ctx) -> dict:
     index = HBMIndex(bcfg.hidden_size, "cosine", device=dev, capacity=shard)
     ct = args.chunk_tokens
     index.add_random(shard, seed=700 + rank, doc_fn=lambda r: synthetic.chunk_document(r, ct))
-    sharded = ShardedIndex(index)
+    sharded = ShardedIndex(index, max_queries=(gbatch + world - 1) // world)  # per-rank share of the batch
     log(f"models ready: {lcfg.name} TP={world} ({llm.num_params() / 1e9:.1f}B params/rank), {rr_name}, "
         f"index {shard} x {bcfg.hidden_size} per rank ({shard * world} total)")
     sample_ctx = "\n\n".join(synthetic.chunk_document(r, ct).page_content for r in range(args.top_k))

@@ -883,6 +883,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("apply_penalties", &apply_penalties);
   m.def("token_mask", &token_mask);
   m.def("sim_topk", &sim_topk);
+  m.def("topk_merge", [](const Tensor& vals, const Tensor& idx, int64_t k, Tensor& out_v, Tensor& out_i) {
+    check_f32(vals, "vals");
+    check_i32(idx, "idx");
+    TORCH_CHECK(vals.dim() == 3 && idx.sizes() == vals.sizes(), "topk_merge: vals / idx [W, Q, cap]");
+    const int cap = (int)vals.size(2);
+    TORCH_CHECK(cap == gai_topk_cap(cap) && k >= 1 && k <= cap, "topk_merge: cap must be 4, 8, 16, 32 or 64, k <= cap");
+    TORCH_CHECK(out_v.numel() == vals.size(1) * k && out_i.numel() == vals.size(1) * k &&
+                    out_i.scalar_type() == at::kLong && out_v.scalar_type() == at::kFloat,
+                "topk_merge: outputs [Q, k]");
+    gai_topk_merge(vals.data_ptr<float>(), idx.data_ptr<int>(), (int)vals.size(0), (int)vals.size(1), cap, (int)k,
+                   out_v.data_ptr<float>(), out_i.data_ptr<int64_t>(), cur_stream());
+  });
   m.def("topk_cap", [](int64_t k) { return gai_topk_cap(k); });
   m.def("moe_route", &moe_route);
   m.def("moe_gemm", &moe_gemm);

@@ -109,6 +109,8 @@ void gai_apply_penalties(float* logits, int B, long ld, const int* tok_ids, cons
 
 // topk.hip
 int gai_topk_cap(int k);
+void gai_topk_merge(const float* vals, const int* idx, int nlists, int nq, int cap, int k, float* out_v, int64_t* out_i,
+                    hipStream_t st);
 void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,
                   int* ws_i, int nwg, int rows_per_wg, float* out_v, int64_t* out_i, hipStream_t st);
 

@@ -428,6 +428,21 @@ void run_topk_k(const void* Q, const void* X, const float* bias, int nq, int N, 
 
 }  // namespace
 
+// Cross-list merge (the sharded index's W shard lists per query): stage 2 alone over ws [nlists][nq][cap].
+void gai_topk_merge(const float* vals, const int* idx, int nlists, int nq, int cap, int k, float* out_v, int64_t* out_i,
+                    hipStream_t st) {
+  if (nq == 0) return;
+  switch (cap) {
+    case 4: sim_topk_stage2<4><<<nq, 256, 0, st>>>(vals, idx, nlists, nq, k, out_v, out_i); break;
+    case 8: sim_topk_stage2<8><<<nq, 256, 0, st>>>(vals, idx, nlists, nq, k, out_v, out_i); break;
+    case 16: sim_topk_stage2<16><<<nq, 256, 0, st>>>(vals, idx, nlists, nq, k, out_v, out_i); break;
+    case 32: sim_topk_stage2<32><<<nq, 256, 0, st>>>(vals, idx, nlists, nq, k, out_v, out_i); break;
+    case 64: sim_topk_stage2<64><<<nq, 256, 0, st>>>(vals, idx, nlists, nq, k, out_v, out_i); break;
+    default: gai_launch_error(__FILE__, __LINE__, "topk_merge: cap must be 4, 8, 16, 32 or 64");
+  }
+  GAI_LAUNCH_CHECK();
+}
+
 int gai_topk_cap(int k) { return k <= 4 ? 4 : k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
 
 void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,

@@ -746,6 +746,29 @@ def sim_topk(Q: torch.Tensor, X: torch.Tensor, bias: torch.Tensor, n_rows: int, 
     return out_v, out_i
 
 
+def topk_merge(vals: torch.Tensor, k: int):
+    """Merge W descending-sorted candidate lists per query: vals [W, Q, n] fp32 -> (top values [Q, k], positions
+    [Q, k] int64 into the flattened [W * n] candidates of the query, w * n + j). On the GPU: the similarity top-k's
+    second-stage kernel (topk.hip sim_topk_stage2). The sharded index's cross-shard merge."""
+    W, Q, n = vals.shape
+    k = min(k, W * n)
+    if not vals.is_cuda or Q == 0 or k > 64:
+        flat = vals.permute(1, 0, 2).reshape(Q, W * n)
+        return torch.topk(flat, k, dim=1)
+    cap = topk_cap(k)
+    v = vals.float()
+    if n != cap:  # every list holds exactly `cap` entries (the kernel's K), padded with -inf
+        pad = v.new_full((W, Q, cap), float("-inf"))
+        pad[:, :, : min(n, cap)] = v[:, :, :cap]
+        v = pad
+    pos = (torch.arange(W, device=v.device, dtype=torch.int32)[:, None, None] * n
+           + torch.arange(cap, device=v.device, dtype=torch.int32)[None, None, :]).expand(W, Q, cap).contiguous()
+    out_v = torch.empty(Q, k, dtype=torch.float32, device=v.device)
+    out_i = torch.empty(Q, k, dtype=torch.int64, device=v.device)
+    native().topk_merge(v.contiguous(), pos, k, out_v, out_i)
+    return out_v, out_i
+
+
 # ---------------------------------------------------------------------------------------------
 # misc
 # ---------------------------------------------------------------------------------------------

@@ -144,7 +144,7 @@ def ep_padded_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def sharded_index_worker(rank, world, port, out_dir):
+def sharded_index_worker(rank, world, port, out_dir, max_queries=None):
     _init(rank, world, port, 1)
     from generativeaiexamples_amd.index.hbm_index import HBMIndex
     from generativeaiexamples_amd.index.sharded import ShardedIndex
@@ -155,8 +155,10 @@ def sharded_index_worker(rank, world, port, out_dir):
     shard = full[rank * 300:(rank + 1) * 300]
     idx = HBMIndex(32, "cosine", device="cpu", capacity=16)
     idx.add(shard)
-    si = ShardedIndex(idx)
+    si = ShardedIndex(idx, max_queries=max_queries)
     my_q = queries[rank * 5:(rank + 1) * 5]
+    if max_queries is not None:  # uneven per-rank batches under the padded (sync-free) protocol
+        my_q = my_q[: 5 - rank]
     rel, rows = si.search_raw(my_q, 4)
     bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731  (the index stores bf16 vectors)
     exp = torch.topk(bf(my_q) @ bf(full).t(), 4, dim=-1)

@@ -54,8 +54,10 @@ def test_ep_padded_dispatch(tmp_path, world):
 
 
 @pytest.mark.timeout(300)
-def test_sharded_index_matches_global(tmp_path):
-    mp.spawn(W.sharded_index_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("max_queries", [None, 8])
+def test_sharded_index_matches_global(tmp_path, max_queries):
+    """max_queries: the padded, sync-free exchange (no count all-gather), uneven batches per rank."""
+    mp.spawn(W.sharded_index_worker, args=(2, _port(), str(tmp_path), max_queries), nprocs=2, join=True)
     for r in range(2):
         d = torch.load(tmp_path / f"idx_{r}.pt", weights_only=True)
         assert d["got"] == d["exp"]

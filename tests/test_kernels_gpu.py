@@ -598,3 +598,17 @@ def test_sample_tp_candidates_match_whole_row(cuda, R):
         assert torch.equal(got[:4], logits[:4].argmax(-1).int())
         agree = int((got == want).sum())
         assert agree >= B - 2, (step, agree, (got != want).nonzero().flatten().tolist(), int(flags))
+
+
+@pytest.mark.parametrize("W,Q,n,k", [(2, 64, 4, 4), (8, 5, 10, 10), (3, 33, 32, 17)])
+def test_topk_merge_matches_torch(cuda, W, Q, n, k):
+    """Cross-shard merge of W descending candidate lists per query (ops.topk_merge, the sharded index's merge) ==
+    torch.topk over the concatenated lists."""
+    torch.manual_seed(W * 100 + n)
+    vals = torch.randn(W, Q, n, device=cuda).sort(dim=-1, descending=True).values
+    vals[:, :, -1] = float("-inf")  # a shard short of n candidates pads with -inf
+    top, pos = ops.topk_merge(vals, k)
+    ref_v, ref_p = torch.topk(vals.permute(1, 0, 2).reshape(Q, W * n), k, dim=1)
+    assert torch.equal(top, ref_v)
+    flat = vals.permute(1, 0, 2).reshape(Q, W * n)
+    assert torch.equal(torch.gather(flat, 1, pos), ref_v)

@@ -40,7 +40,9 @@ def main():
     cfg = LlamaConfig.llama31_8b(num_layers=args.layers)
     m = LlamaModel(cfg, device=dev).random_init(3)
     tok = llama3_byte_tokenizer(cfg.vocab_size)
-    T = args.ctx
+    # the prompt and its generated tokens must fit the model's 131,072 positions: --ctx 131072 means the longest
+    # prompt that leaves room for --decode new tokens
+    T = min(args.ctx, cfg.max_position - args.decode - 16)
     eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=4, max_batched_tokens=args.chunk, prefill_chunk=args.chunk,
                                          max_model_len=T + args.decode + 16, prefix_cache=False, decode_steps=8,
                                          graph_batch_sizes=(1,), kv_memory_fraction=0.3))
