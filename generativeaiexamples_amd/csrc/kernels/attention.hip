@@ -90,7 +90,11 @@ __device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to
 // HL = q heads per wave (1 or 2, same 32 query rows): with 2, every K / V^T fragment a wave reads from LDS feeds two
 // MFMAs, halving the LDS read traffic per FLOP (with one head per wave the fragment reads + tile writes, ~2.5K LDS
 // cycles per CU per 64-key tile, exceed the ~2K MFMA cycles per SIMD); twice the registers, so one wave per SIMD.
-template <int D, int HPW, typename KV, int HL = 1>
+// PIPE (HL == 1): software-pipelined main loop - tile kt+1's QK^T MFMAs are issued interleaved with tile kt's softmax
+// exponentials and P.V MFMAs, so the matrix pipe has independent work while the VALU runs the softmax (the one-tile
+// loop serialised them: 36.5 % MFMA busy, 7.5 VALU per MFMA, profiles/r5 section 10). K runs one tile ahead of V in
+// LDS; the next K and V tiles are staged in two register sets during the iteration.
+template <int D, int HPW, typename KV, int HL = 1, bool PIPE = false>
 __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
@@ -163,31 +167,33 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
 #pragma unroll
   for (int c = 0; c < Cfg::CH; ++c) voff[c] = (unsigned)(((c * 256 + tid) % (2 * D)) * 8 * sizeof(KV));
   int nblk[Cfg::CH];
-  auto lookup = [&](int kt) {
+  auto lookup_into = [&](int kt, int(&nb)[Cfg::CH]) {
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
       const int pidx = kt * 4 + (c * 256 + wid_u * 64) / (2 * D);
-      nblk[c] = bt[pidx * kBS < ctx ? pidx : 0];
+      nb[c] = bt[pidx * kBS < ctx ? pidx : 0];
     }
   };
-  auto load_half = [&](const KV* base) {
+  auto lookup = [&](int kt) { lookup_into(kt, nblk); };
+  auto load_half_from = [&](const KV* base, const int(&nb)[Cfg::CH], Stage(&dst)[Cfg::CH]) {
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
       // K page is [16][D] contiguous, V^T page [D][16]
-      stg[c] = buf_load<Stage>(base + ((size_t)nblk[c] * Hkv + g) * (kBS * D), voff[c]);
+      dst[c] = buf_load<Stage>(base + ((size_t)nb[c] * Hkv + g) * (kBS * D), voff[c]);
     }
   };
-  auto write_k = [&](int buf) {
+  auto load_half = [&](const KV* base) { load_half_from(base, nblk, stg); };
+  auto write_k_from = [&](int buf, const Stage(&src)[Cfg::CH]) {
     char* sk = smem + buf * Cfg::BUF;
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
       const int id = c * 256 + tid;
       const int page = id / (2 * D), w = id % (2 * D);
       const int key = page * 16 + w / Cfg::KU, u = w % Cfg::KU;
-      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(stg[c], k_scale);
+      *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(src[c], k_scale);
     }
   };
-  auto write_v = [&](int buf) {
+  auto write_v_from = [&](int buf, const Stage(&src)[Cfg::CH]) {
     char* sv = smem + buf * Cfg::BUF + Cfg::KBYTES;
 #pragma unroll
     for (int c = 0; c < Cfg::CH; ++c) {
@@ -196,13 +202,15 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
       const int d = w >> 1, half = w & 1;
       const int u8 = 4 * page + 2 * half;
       typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-      const bf16x8 vv = kv_to_bf16(stg[c], v_scale);
+      const bf16x8 vv = kv_to_bf16(src[c], v_scale);
       const bf16x4_t lo = {vv[0], vv[1], vv[2], vv[3]};
       const bf16x4_t hi = {vv[4], vv[5], vv[6], vv[7]};
       *reinterpret_cast<bf16x4_t*>(sv + v_lds_off<D>(d, u8)) = lo;
       *reinterpret_cast<bf16x4_t*>(sv + v_lds_off<D>(d, u8 + 1)) = hi;
     }
   };
+  auto write_k = [&](int buf) { write_k_from(buf, stg); };
+  auto write_v = [&](int buf) { write_v_from(buf, stg); };
 
   f32x16 acc_o[HL][D / 32];
   float m_run[HL], l_run[HL];
@@ -215,6 +223,116 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   }
   const float sl2 = scale * kLog2e;
 
+  if constexpr (PIPE) {
+    static_assert(HL == 1, "the pipelined loop keeps one head per wave");
+    // K(kt + 1) and V(kt) are in LDS at iteration kt: K in slot (kt + 1) & 1, V in slot kt & 1 (each slot = K image,
+    // V^T image). During the iteration V(kt + 1) and K(kt + 2) stream into two register sets; after the MFMAs they
+    // are written to V slot (kt + 1) & 1 (last read by P.V(kt - 1)) and K slot kt & 1 (last read by QK^T(kt), which ran
+    // in iteration kt - 1); one barrier per iteration.
+    Stage stv[Cfg::CH];
+    int nb_v[Cfg::CH], nb_k[Cfg::CH];
+    auto qk_part = [&](int kslot, int sub, int t0, int nt, f32x16& acc) {
+      const char* skk = smem + kslot * Cfg::BUF;
+      const int key = 32 * sub + (lane & 31);
+#pragma unroll
+      for (int t = t0; t < t0 + nt; ++t) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(skk + k_lds_off<D>(key, 2 * t + h));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][t], acc, 0, 0, 0);
+      }
+    };
+    f32x16 sc[2], sn[2];
+    if (ntiles > 0) {
+      lookup_into(0, nblk);
+      load_half_from(kc, nblk, stg);
+      write_k_from(0, stg);
+      load_half_from(vc, nblk, stg);
+      write_v_from(0, stg);
+      if (ntiles > 1) {
+        lookup_into(1, nb_v);
+        load_half_from(kc, nb_v, stg);
+        write_k_from(1, stg);
+      }
+      lookup_into(2, nb_k);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the Q fragments and the prologue tiles
+    __syncthreads();
+    sc[0] = f32x16{};
+    sc[1] = f32x16{};
+    if (ntiles > 0) {
+      qk_part(0, 0, 0, D / 16, sc[0]);
+      qk_part(0, 1, 0, D / 16, sc[1]);
+    }
+    __syncthreads();  // every wave has read K(0) before iteration 0 overwrites K slot 0 with K(2)
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const bool more1 = kt + 1 < ntiles, more2 = kt + 2 < ntiles;
+      if (more1) load_half_from(vc, nb_v, stv);  // V(kt + 1)
+      if (more2) load_half_from(kc, nb_k, stg);  // K(kt + 2)
+      // ---- softmax statistics of tile kt (as the one-tile loop)
+      float mt = kNeg;
+      const int kend = kt * 64 + 63;
+      if (kend < ctx && (!causal || kend <= ctx - qlen + r0)) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sc[sub][r]);
+      } else {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool ok = key < ctx && (!causal || key <= qpos);
+            const float x = ok ? sc[sub][r] : kNeg;
+            sc[sub][r] = x;
+            mt = fmaxf(mt, x);
+          }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+      const float m_new = fmaxf(m_run[0], mt);
+      const float alpha = fexp2(m_run[0] - m_new);
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) acc_o[0][i] *= alpha;
+      }
+      m_run[0] = m_new;
+      // ---- tile kt+1's QK^T interleaved with tile kt's exponentials and P.V: per 8-key step, D / 32 QK^T MFMAs
+      // (independent of this tile's softmax) beside the step's 8 exps and its D / 32 P.V MFMAs
+      sn[0] = f32x16{};
+      sn[1] = f32x16{};
+      const char* sv = smem + (kt & 1) * Cfg::BUF + Cfg::KBYTES;
+      const int kslot = (kt + 1) & 1;
+      float rs = 0.f;
+      if (prio == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        if (more1) qk_part(kslot, st >> 1, (st & 1) * (D / 32), D / 32, sn[st >> 1]);
+        const int sub = st >> 1, sp = st & 1;
+        bf16x8 pf;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float pv = fexp2(fmaf(sc[sub][8 * sp + e], sl2, -m_new));
+          rs += pv;
+          pf[e] = (bf16)pv;
+        }
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off<D>(32 * dt + (lane & 31), 4 * st + h));
+          acc_o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[0][dt], 0, 0, 0);
+        }
+      }
+      if (prio == 2) __builtin_amdgcn_s_setprio(0);
+      rs += __shfl_xor(rs, 32, 64);
+      l_run[0] = l_run[0] * alpha + rs;
+      if (more2) write_k_from(kt & 1, stg);
+      if (more1) write_v_from((kt + 1) & 1, stv);
+#pragma unroll
+      for (int c = 0; c < Cfg::CH; ++c) nb_v[c] = nb_k[c];
+      lookup_into(kt + 3, nb_k);  // pages past the context resolve to entry 0 (never read unmasked)
+      __syncthreads();
+      sc[0] = sn[0];
+      sc[1] = sn[1];
+    }
+  } else {
   if (ntiles > 0) {
     lookup(0);
     load_half(kc);
@@ -353,6 +471,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     if (more) write_v(cur ^ 1);
     __syncthreads();
   }
+  }  // one-tile loop
 
   if (qrow < qlen) {
 #pragma unroll
@@ -862,7 +981,27 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
     GAI_LAUNCH_CHECK();
     return;
   }
+  // GAI_ATTN_PIPE = 1: the software-pipelined main loop (attn_prefill_kernel PIPE)
+  static const int pipe_env = getenv("GAI_ATTN_PIPE") ? atoi(getenv("GAI_ATTN_PIPE")) : 0;
 #define GAI_PF(DD, HP)                                                                                         \
+  if (D == DD && hpw == HP && pipe_env == 1) {                                                                 \
+    const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
+    if (kv_fp8) {                                                                                              \
+      auto kern = attn_prefill_kernel<DD, HP, fp8, 1, true>;                                                   \
+      set_max_lds(kern, lds);                                                                                  \
+      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,  \
+                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld); \
+    } else {                                                                                                   \
+      auto kern = attn_prefill_kernel<DD, HP, bf16, 1, true>;                                                  \
+      set_max_lds(kern, lds);                                                                                  \
+      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, \
+                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
+                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld); \
+    }                                                                                                          \
+    GAI_LAUNCH_CHECK();                                                                                        \
+    return;                                                                                                    \
+  }                                                                                                            \
   if (D == DD && hpw == HP) {                                                                                  \
     const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
     if (kv_fp8) {                                                                                              \
