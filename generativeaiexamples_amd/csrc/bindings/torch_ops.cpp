@@ -591,12 +591,22 @@ void geglu_interleaved(const Tensor& x, Tensor& y) {
 }
 
 void gemv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, int64_t epi,
-          const optional<Tensor>& out, const optional<Tensor>& res, bool frag) {
-  check_bf16(x, "x");
+          const optional<Tensor>& out, const optional<Tensor>& res, bool frag, const optional<Tensor>& swi,
+          int64_t ks) {
   check_bf16(W, "W");
-  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1) && x.is_contiguous() && W.is_contiguous(),
-              "gemv: x [M, K], W [N, K] contiguous");
-  const int M = x.size(0), N = W.size(0), K = W.size(1);
+  const float* swp = nullptr;
+  int M, N = W.size(0), K = W.size(1);
+  if (swi) {  // the input is bf16(silu(g) * u) of this fp32 [M, 2K] interleaved gate_up output (x is not read)
+    check_f32(*swi, "swi");
+    TORCH_CHECK(swi->dim() == 2 && swi->size(1) == 2 * (int64_t)K && W.is_contiguous(), "gemv: swi [M, 2K]");
+    M = swi->size(0);
+    swp = swi->data_ptr<float>();
+  } else {
+    check_bf16(x, "x");
+    TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1) && x.is_contiguous() && W.is_contiguous(),
+                "gemv: x [M, K], W [N, K] contiguous");
+    M = x.size(0);
+  }
   TORCH_CHECK(gai_gemv_ok(M, N, K, gamma.has_value()), "gemv: shape not supported");
   if (gamma) {
     check_bf16(*gamma, "gamma");
@@ -611,12 +621,12 @@ void gemv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tens
   } else {
     TORCH_CHECK(out && out->is_contiguous(), "gemv: out");
     const int64_t cols = epi == 2 ? N / 2 : N;
-    TORCH_CHECK(out->numel() == (int64_t)M * cols, "gemv: out size");
-    TORCH_CHECK(out->scalar_type() == (epi == 4 ? at::kFloat : at::kBFloat16), "gemv: out dtype");
+    TORCH_CHECK(out->numel() == (int64_t)M * cols * (epi == 5 ? ks : 1), "gemv: out size");
+    TORCH_CHECK(out->scalar_type() == (epi == 4 || epi == 5 ? at::kFloat : at::kBFloat16), "gemv: out dtype");
     o = out->data_ptr();
   }
-  gai_gemv(x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), M, N, K, (int)epi, o, r,
-           cur_stream(), frag ? 1 : 0);
+  gai_gemv(swi ? nullptr : x.data_ptr(), gamma ? gamma->data_ptr() : nullptr, (float)eps, W.data_ptr(), M, N, K,
+           (int)epi, o, r, cur_stream(), frag ? 1 : 0, swp, (int)ks);
 }
 
 void gemv_rope_kv(const Tensor& x, const optional<Tensor>& gamma, double eps, const Tensor& W, const Tensor& pos,
@@ -906,7 +916,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("custom_all_to_all", &custom_all_to_all);
   m.def("gemm_qkv_partials", &gemm_qkv_partials);
   m.def("gemv", &gemv, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("eps"), pybind11::arg("W"),
-        pybind11::arg("epi"), pybind11::arg("out"), pybind11::arg("res"), pybind11::arg("frag") = false);
+        pybind11::arg("epi"), pybind11::arg("out"), pybind11::arg("res"), pybind11::arg("frag") = false,
+        pybind11::arg("swi") = pybind11::none(), pybind11::arg("ks") = 1);
   m.def("gemv_rope_kv", &gemv_rope_kv, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("eps"),
         pybind11::arg("W"), pybind11::arg("pos"), pybind11::arg("cos_sin"), pybind11::arg("slots"),
         pybind11::arg("q_out"), pybind11::arg("k_cache"), pybind11::arg("v_cache"), pybind11::arg("Hq"),

@@ -120,8 +120,9 @@ void gai_moe_dispatch(const int* ids, int n, int k, int E, int* a_rows, int* off
 // gemv.hip: decode GEMV for 1..4 token rows with the RMSNorm staged in and the epilogue fused
 int gai_gemv_ok(int M, int N, int K, int normed);
 // wfrag: W stored in MFMA fragment order (ops.shuffle_fragments; N % 16 == 0, 32 for SwiGLU)
+// epi 5 (K parts): out = fp32 slabs [ks][M][N]; swi: stage bf16(silu(g) * u) of an fp32 [M, 2K] interleaved gate_up
 void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
-              void* res, hipStream_t st, int wfrag = 0);
+              void* res, hipStream_t st, int wfrag = 0, const float* swi = nullptr, int ks = 1);
 void gai_gemv_rope_kv(const void* x, const void* gamma, float eps, const void* W, int M, int K, const int* pos,
                       const float* cos_sin, const int* slots, void* q_out, void* k_cache, void* v_cache, int Hq,
                       int Hkv, hipStream_t st, int wfrag = 0);

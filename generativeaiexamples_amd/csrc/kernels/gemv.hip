@@ -32,7 +32,9 @@ constexpr int kG = 4;        // pieces per row per pipeline group
 // attribute call, and its error would surface at the next launch check)
 constexpr int kGvMaxDyn = 160 * 1024 - 1024;
 
-enum { GV_PLAIN = 0, GV_RESIDUAL = 1, GV_SWIGLU = 2, GV_ROPE = 3, GV_F32 = 4 };
+// GV_PART (fragment-ordered weights): K is split over KS workgroups per column, each storing its fp32 row sums as
+// slab h of out [KS][M][N] - the QKV split-K partials the decode-attention launch folds (sum, RoPE, KV write).
+enum { GV_PLAIN = 0, GV_RESIDUAL = 1, GV_SWIGLU = 2, GV_ROPE = 3, GV_F32 = 4, GV_PART = 5 };
 
 struct GemvArgs {
   const bf16* x;      // [M, K] activations, or the residual stream to normalise when gamma != null
@@ -49,6 +51,10 @@ struct GemvArgs {
   bf16* k_cache;
   bf16* v_cache;
   int Hq, Hkv;
+  // swi != null: the staged activations are bf16(silu(g) * u) of an fp32 [M, 2K] gate_up output in the [gate16 | up16]
+  // interleave (the GV_F32 gate_up GEMV), i.e. the down projection does the SwiGLU while staging its input
+  const float* swi;
+  int ks;  // GV_PART: K parts per column
 };
 
 __device__ __forceinline__ float dot8(const bf16x8& a, const bf16x8& b, float acc) {
@@ -77,7 +83,7 @@ __device__ __forceinline__ void gv_epilogue(const GemvArgs& a, int m, int p, int
     r[r1] = (bf16)((float)(bf16)v1 + (float)r[r1]);
   } else if constexpr (EPI == GV_SWIGLU) {
     reinterpret_cast<bf16*>(a.out)[(size_t)m * (N / 2) + p] = (bf16)(silu(v0) * v1);
-  } else {  // GV_ROPE: x = bf16(qkv) as the unfused GEMM output, then rotate (neox halves), store
+  } else if constexpr (EPI == GV_ROPE) {  // x = bf16(qkv) as the unfused GEMM output, then rotate (neox halves), store
     constexpr int D = 128, kBS = 16;
     const int h = p >> 6, i = p & 63;
     float x1 = (float)(bf16)v0, x2 = (float)(bf16)v1;
@@ -158,6 +164,21 @@ __device__ __forceinline__ void gv_stage(const GemvArgs& a, bf16* xs, float* red
           *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + 8 * ch) = o;
         }
       }
+    }
+  } else if (a.swi != nullptr) {
+    // chunk c = k 8c .. 8c + 7, inside one 16-group: gate at 32 (k / 16) + k % 16, up 16 further; the rounding of the
+    // GV_SWIGLU epilogue (bf16(silu(g) * u) of the fp32 sums)
+    for (int ch = tid; ch < MR * nch; ch += kThr) {
+      const int m = ch / nch, c = ch % nch, k0 = 8 * c;
+      const float* gp = a.swi + (size_t)m * 2 * K + 32 * (k0 >> 4) + (k0 & 15);
+      const float4 g0 = *reinterpret_cast<const float4*>(gp), g1 = *reinterpret_cast<const float4*>(gp + 4);
+      const float4 u0 = *reinterpret_cast<const float4*>(gp + 16), u1 = *reinterpret_cast<const float4*>(gp + 20);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float u[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)(silu(g[e]) * u[e]);
+      *reinterpret_cast<bf16x8*>(xs + (size_t)m * K + k0) = o;
     }
   } else {
     for (int ch = tid; ch < MR * nch; ch += kThr) {
@@ -353,6 +374,13 @@ __global__ __launch_bounds__(64 * NW) void gemv_frag_kernel(GemvArgs a, int KS) 
       v1 += part[(C - 1) * NWC + w][m][rb];
     }
   }
+  if constexpr (EPI == GV_PART) {  // slab h of out [KS][M][N]: this part's row sums, no hand-over
+    if (!epi_thread) return;
+    const int r0 = 16 * column(0) + ra;
+    float* o = reinterpret_cast<float*>(a.out) + ((size_t)h * a.M + m) * a.N + r0;
+    *reinterpret_cast<float2*>(o) = float2{v0, v1};
+    return;
+  }
   if (KS > 1) {
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(g_gvf_ws, (short)0, 0x7fffffff, 0x00020000);
     using f32x2 = __attribute__((ext_vector_type(2))) float;
@@ -476,12 +504,15 @@ void gemv_frag_launch(const GemvArgs& a, hipStream_t st) {
   static const int fks = getenv("GAI_GEMV_FRAG_KS") ? atoi(getenv("GAI_GEMV_FRAG_KS")) : 0;
   constexpr int C = gv_frag_cols<EPI>();
   const int groups = a.N / (16 * C), KF = a.K / 32;
+  // waves: 4 for the batch-1 gate_up as an fp32 GEMV (1792 one-column workgroups, 7 per CU: the SwiGLU moved into the
+  // down projection's staging) and for the QKV partials (K parts x 384 columns); 8 for the LM head
   const int nw = (fnw == 4 || fnw == 8 || fnw == 16) ? fnw
-                 : EPI == GV_F32 ? 8
+                 : EPI == GV_PART ? 4
+                 : EPI == GV_F32 ? (a.M == 1 && a.N <= 65536 ? 4 : 8)
                  : EPI == GV_SWIGLU ? (a.M == 1 ? 4 : 8)
                  : 16;
   auto fits = [&](int ks) { return (ks == 1 || groups * ks <= kGvfMaxItems) && KF % (ks * (nw / C) * kGf) == 0; };
-  const int KS = (fks == 2 || fks == 4 || fks == 8) && fits(fks) ? fks : 1;
+  const int KS = EPI == GV_PART ? a.ks : (fks == 2 || fks == 4 || fks == 8) && fits(fks) ? fks : 1;
   if (!fits(KS)) gai_launch_error(__FILE__, __LINE__, "gemv: fragment-ordered K split");
   if (nw == 4) return gemv_frag_launch_nw<EPI, 4>(a, KS, st);
   if (nw == 16) return gemv_frag_launch_nw<EPI, 16>(a, KS, st);
@@ -496,6 +527,7 @@ void gemv_launch(const GemvArgs& a, hipStream_t st, int wfrag) {
       gai_launch_error(__FILE__, __LINE__, "gemv: fragment-ordered weight shape");
     return gemv_frag_launch<EPI>(a, st);
   }
+  if constexpr (EPI == GV_PART) gai_launch_error(__FILE__, __LINE__, "gemv: K parts need fragment-ordered weights");
   const int nw = gemv_waves(a.N, a.M);
   if (nw == 6) return gemv_launch_nw<EPI, 6>(a, st);
   if (nw == 12) return gemv_launch_nw<EPI, 12>(a, st);
@@ -505,6 +537,7 @@ void gemv_launch(const GemvArgs& a, hipStream_t st, int wfrag) {
 }  // namespace
 
 int gai_gemv_ok(int M, int N, int K, int normed) {
+  // (also the shapes of GV_PART and of the swi staging form; their extra conditions are checked in gai_gemv)
   if (M < 1 || M > 4 || N % 2 || K % (kPiece * kG)) return 0;
   if ((size_t)M * K * sizeof(bf16) > (size_t)kGvMaxDyn) return 0;
   if (normed && K > 2 * 8 * kGvThreads) return 0;
@@ -513,10 +546,17 @@ int gai_gemv_ok(int M, int N, int K, int normed) {
 
 // epi: 0 plain bf16, 1 residual in place (res), 2 SwiGLU on the [gate16 | up16] interleave, 4 fp32 out.
 void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M, int N, int K, int epi, void* out,
-              void* res, hipStream_t st, int wfrag) {
+              void* res, hipStream_t st, int wfrag, const float* swi, int ks) {
   if (!gai_gemv_ok(M, N, K, gamma != nullptr)) gai_launch_error(__FILE__, __LINE__, "gemv: shape");
   if (epi == GV_SWIGLU && N % 32) gai_launch_error(__FILE__, __LINE__, "gemv: SwiGLU needs N % 32 == 0");
+  if ((epi == GV_PART || swi != nullptr) && !wfrag)
+    gai_launch_error(__FILE__, __LINE__, "gemv: K parts / SwiGLU staging need fragment-ordered weights");
+  if (swi != nullptr && gamma != nullptr) gai_launch_error(__FILE__, __LINE__, "gemv: SwiGLU staging has no norm");
+  if (epi == GV_PART && (ks < 1 || (K / 32) % (ks * 4 * kGf) || (N / 16) * ks > kGvfMaxItems))
+    gai_launch_error(__FILE__, __LINE__, "gemv: K parts do not divide the column");
   GemvArgs a{};
+  a.swi = swi;
+  a.ks = ks;
   a.x = (const bf16*)x;
   a.gamma = (const bf16*)gamma;
   a.eps = eps;
@@ -531,6 +571,7 @@ void gai_gemv(const void* x, const void* gamma, float eps, const void* W, int M,
     case GV_RESIDUAL: gemv_launch<GV_RESIDUAL>(a, st, wfrag); return;
     case GV_SWIGLU: gemv_launch<GV_SWIGLU>(a, st, wfrag); return;
     case GV_F32: gemv_launch<GV_F32>(a, st, wfrag); return;
+    case GV_PART: gemv_launch<GV_PART>(a, st, wfrag); return;
     default: gai_launch_error(__FILE__, __LINE__, "gemv: unknown epilogue");
   }
 }

@@ -36,6 +36,8 @@ from .. import ops
 from ..parallel.dist import DistContext, get_context
 from .common import ForwardBatch, randn_like_
 
+_GEMV_B1 = os.environ.get("GAI_GEMV_B1", "0") == "1"
+
 
 @dataclass
 class LlamaConfig:
@@ -562,17 +564,38 @@ class LlamaModel:
             res.mul_(self.embed_multiplier)
         q = torch.empty(T, self.hq, hd, device=res.device, dtype=self.dtype)
         attn = torch.empty_like(q)
+        # batch 1, opt-in (GAI_GEMV_B1=1): the launches rebalanced onto more workgroups - QKV as 2 K parts whose
+        # fp32 slabs the attention launch folds (sum, RoPE, KV write), gate_up as an fp32 GEMV of one 16-row column
+        # per workgroup (1792 for Llama-3-8B) with the SwiGLU applied while the down projection stages its input.
+        # Measured slower (graph replay 3.197 vs 3.135 ms, profiles/r6/decode_b1): gate_up was already streaming
+        # at 5.8 TB/s (40.8 vs 41.1 us), the fp32 staging costs down ~1.7 us, the fold costs attention ~1.1 us
+        b1 = T == 1 and _GEMV_B1 and ops.is_frag(w["l0.gate_up"]) and ops.is_frag(w["l0.down"])
+        slabs = gu = None
+        if b1:
+            slabs = torch.empty(2, T, w["l0.qkv"].shape[0], device=res.device, dtype=torch.float32)
+            gu = torch.empty(T, w["l0.gate_up"].shape[0], device=res.device, dtype=torch.float32)
         for i in range(c.num_layers):
             p = f"l{i}."
             kc, vc = kv.layer(i)
             ks, vs = kv.scales(i)
-            ops.gemv_rope_kv(res, w[p + "qkv"], w[p + "attn_norm"], c.rms_eps, fb.positions, self.cos_sin, fb.slots, q,
-                             kc, vc, self.hq, self.hkv)
+            fold = None
+            if b1:
+                fold = ops.gemv_qkv_partials(res, w[p + "qkv"], w[p + "attn_norm"], c.rms_eps, kc, hd, decode_ws, ks,
+                                             vs, out=slabs)
+            if fold is None:
+                ops.gemv_rope_kv(res, w[p + "qkv"], w[p + "attn_norm"], c.rms_eps, fb.positions, self.cos_sin,
+                                 fb.slots, q, kc, vc, self.hq, self.hkv)
+            else:
+                fold = fold + (fb.positions, self.cos_sin, fb.slots)
             ops.attention_decode(q, kc, vc, fb.decode_block_tables, fb.decode_ctx, self.scale, ws=decode_ws,
-                                 max_ctx=fb.max_decode_ctx, out=attn, k_scale=ks, v_scale=vs)
+                                 max_ctx=fb.max_decode_ctx, out=attn, k_scale=ks, v_scale=vs, qkv_fold=fold)
             ops.gemv(attn.view(T, -1), w[p + "o"], epi="residual", res=res)
-            g = ops.gemv(res, w[p + "gate_up"], gamma=w[p + "mlp_norm"], eps=c.rms_eps, epi="swiglu")
-            ops.gemv(g, w[p + "down"], epi="residual", res=res)
+            if b1:
+                ops.gemv(res, w[p + "gate_up"], gamma=w[p + "mlp_norm"], eps=c.rms_eps, epi="f32", out=gu)
+                ops.gemv(None, w[p + "down"], epi="residual", res=res, swi=gu)
+            else:
+                g = ops.gemv(res, w[p + "gate_up"], gamma=w[p + "mlp_norm"], eps=c.rms_eps, epi="swiglu")
+                ops.gemv(g, w[p + "down"], epi="residual", res=res)
         if fb.sample_rows is not None:
             res = res.index_select(0, fb.sample_rows)
         logits = ops.gemv(res, w["lm_head"], gamma=w["norm"], eps=c.rms_eps, epi="f32")

@@ -631,6 +631,19 @@ def qkv_fold_partials(x: torch.Tensor, w, bias, k_cache, head_dim: int, ws: "Dec
     return (slabs, int(ks)) if ks else None
 
 
+def gemv_qkv_partials(x, W, gamma, eps: float, k_cache, head_dim: int, ws: "DecodeWorkspace | None", k_scale=1.0,
+                      v_scale=1.0, ks: int = 2, out=None):
+    """Batch-1 decode QKV as a K-split GEMV (gemv.hip GV_PART, the attention RMSNorm staged in) for
+    attention_decode(qkv_fold=...): (slabs [ks, M, N] fp32, ks), or None when the fold does not apply (the caller
+    then runs gemv_rope_kv). 2 K parts x N / 16 columns of 4 waves: 768 workgroups for Llama-3-8B's 6144 rows instead
+    of gemv_rope_kv's 192 column pairs, and the RoPE / KV-write epilogue moves into the attention prologue."""
+    if not (_QKV_FOLD and _ATTN_FUSE and x.is_cuda and is_frag(W) and head_dim == 128
+            and k_cache.dtype == torch.bfloat16 and k_scale == 1.0 and v_scale == 1.0 and ws is not None
+            and ws.max_splits >= 2 and (W.shape[1] // 32) % (ks * 16) == 0):
+        return None
+    return gemv(x, W, gamma, eps, "part", out=out, ks=ks), ks
+
+
 # Decode-attention splits are merged inside the attention launch by the last-arriving split (write-through sc1
 # partials + a relaxed ticket, no fence): Llama-3-8B B = 64, ctx 2600 eager forward 7.918 -> 7.738 ms, headline
 # 16.92 -> 17.08 q/s (profiles/r3/attn_fused_merge_ab). The first form, with a per-workgroup agent release, was
@@ -827,7 +840,7 @@ def moe_dispatch(ids: torch.Tensor, num_experts: int):
     return a_rows, offs, pos.view(T, k)
 
 
-_GEMV_EPI = {"plain": 0, "residual": 1, "swiglu": 2, "f32": 4}
+_GEMV_EPI = {"plain": 0, "residual": 1, "swiglu": 2, "f32": 4, "part": 5}
 
 
 def gemv_ok(M: int, N: int, K: int, normed: bool = False) -> bool:
@@ -837,20 +850,26 @@ def gemv_ok(M: int, N: int, K: int, normed: bool = False) -> bool:
             and (not normed or K <= 8192))
 
 
-def gemv(x, W, gamma=None, eps: float = 1e-5, epi: str = "plain", res=None, out=None):
+def gemv(x, W, gamma=None, eps: float = 1e-5, epi: str = "plain", res=None, out=None, swi=None, ks: int = 1):
     """Decode GEMV for 1..4 token rows with the consumer's RMSNorm staged in (``gamma``) and the epilogue fused:
     plain bf16, ``residual`` (res = bf16(bf16(x W^T) + res) in place), ``swiglu`` on the [gate16 | up16]
-    interleave, ``f32`` logits."""
-    if not x.is_cuda:
-        return ref.gemv(x, W, gamma, eps, epi, res)
-    M, N = x.shape[0], W.shape[0]
+    interleave, ``f32`` logits, ``part`` = fp32 partial sums of ``ks`` K parts [ks, M, N] (the QKV slabs
+    attention_decode(qkv_fold=...) folds). ``swi`` (fragment-ordered W): the input is bf16(silu(g) * u) of that fp32
+    [M, 2K] gate_up interleave, computed while staging (x is then ignored)."""
+    src = swi if swi is not None else x
+    if not src.is_cuda:
+        r = ref.gemv(x, W, gamma, eps, epi, res, swi, ks)
+        return _into(out, r) if epi != "residual" else r
+    M, N = src.shape[0], W.shape[0]
+    xa = src if swi is not None else x.contiguous()  # (not read when swi is given)
     if epi == "residual":
-        native().gemv(x.contiguous(), gamma, eps, W, 1, None, res, is_frag(W))
+        native().gemv(xa, gamma, eps, W, 1, None, res, is_frag(W), swi, ks)
         return res
     if out is None:
         cols = N // 2 if epi == "swiglu" else N
-        out = torch.empty(M, cols, dtype=torch.float32 if epi == "f32" else x.dtype, device=x.device)
-    native().gemv(x.contiguous(), gamma, eps, W, _GEMV_EPI[epi], out, None, is_frag(W))
+        shape = (ks, M, N) if epi == "part" else (M, cols)
+        out = torch.empty(shape, dtype=torch.float32 if epi in ("f32", "part") else x.dtype, device=src.device)
+    native().gemv(xa, gamma, eps, W, _GEMV_EPI[epi], out, None, is_frag(W), swi, ks)
     return out
 
 

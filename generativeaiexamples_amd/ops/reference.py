@@ -281,11 +281,20 @@ def moe_combine(Y, pos, w, residual=None):
     return y.to(Y.dtype)
 
 
-def gemv(x, W, gamma=None, eps=1e-5, epi="plain", res=None):
-    """Small-batch decode GEMV oracle (gemv.hip): optional RMSNorm of x (rounded to bf16), fp32 product, epilogue."""
-    xf = x.float()
+def gemv(x, W, gamma=None, eps=1e-5, epi="plain", res=None, swi=None, ks=1):
+    """Small-batch decode GEMV oracle (gemv.hip): optional RMSNorm of x (rounded to bf16), fp32 product, epilogue.
+    ``swi``: the input is bf16(silu(g) * u) of an fp32 [M, 2K] [gate16 | up16] interleave (x unused); ``part``: the
+    fp32 row sums of ``ks`` equal K parts, [ks, M, N]."""
+    if swi is not None:
+        g = swi.float().view(swi.shape[0], -1, 2, 16)
+        xf = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(swi.shape[0], -1).to(torch.bfloat16).float()
+    else:
+        xf = x.float()
     if gamma is not None:
         xf = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(torch.bfloat16).float()
+    if epi == "part":
+        kp = xf.shape[1] // ks
+        return torch.stack([xf[:, h * kp:(h + 1) * kp] @ W.float()[:, h * kp:(h + 1) * kp].t() for h in range(ks)])
     y = xf @ W.float().t()
     if epi == "f32":
         return y

@@ -1,5 +1,6 @@
-"""Decode-step anatomy of the serving engine: wall time per engine.step() split into scheduler,
-batch upload, graph replay (GPU time via events), penalties+sampling, and token processing.
+"""Decode-step anatomy of the serving engine: steady-state wall time per generated token (TPOT at --batch
+concurrent sequences), plain engine.step() time, and the engine's own phase timers (schedule, upload, replay,
+sample, process).
 
 python tools/decode_profile.py [--model llama3-8b] [--batch 64] [--prompt 2400] [--steps 50]
 """
@@ -22,99 +23,28 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     a = ap.parse_args()
     m, tok, name = build_llm(a.model, device="cuda")
-    eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=a.batch, max_model_len=a.prompt + 6 * a.steps + 128,
+    eng = LLMEngine(m, tok, EngineConfig(max_num_seqs=a.batch, max_model_len=a.prompt + 16 * (a.steps + 30) + 128,
                                          max_batched_tokens=16384, use_graphs=not a.no_graphs))
     if not a.no_graphs:
         eng.capture_graphs(max_bs=a.batch)
     g = torch.Generator().manual_seed(0)
-    p = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=6 * a.steps + 64, ignore_eos=True)
+    p = SamplingParams(temperature=0.2, top_p=0.7, max_tokens=16 * (a.steps + 30), ignore_eos=True)
     for i in range(a.batch):
         eng.add_request(torch.randint(10, 120000, (a.prompt,), generator=g).tolist(), p)
     while eng.stats["decode_tokens"] == 0:  # run through prefill
         eng.step()
     torch.cuda.synchronize()
-    # wrap internals with timers
-    acc = {k: 0.0 for k in ("schedule", "graph_or_forward", "sample", "process", "gpu_forward_ms")}
-    orig_sched = eng.sched.schedule
-    orig_run, orig_process = eng._run_graph, eng._process
-    import generativeaiexamples_amd.ops as ops
-    orig_sample = ops.sample
-
-    def sched():
-        t = time.perf_counter(); r = orig_sched(); acc["schedule"] += time.perf_counter() - t; return r  # noqa: E702
-
-    def run_graph(b, n):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t = time.perf_counter(); s.record(); r = orig_run(b, n); e.record()  # noqa: E702
-        acc["graph_or_forward"] += time.perf_counter() - t
-        e.synchronize(); acc["gpu_forward_ms"] += s.elapsed_time(e)  # noqa: E702
-        return r
-
-    def sample(*args, **kw):
-        t = time.perf_counter(); r = orig_sample(*args, **kw); acc["sample"] += time.perf_counter() - t; return r  # noqa: E702
-
-    def process(*args, **kw):
-        t = time.perf_counter(); r = orig_process(*args, **kw); acc["process"] += time.perf_counter() - t; return r  # noqa: E702
-
-    class S:  # proxy scheduler
-        def __getattr__(self, k):
-            return sched if k == "schedule" else getattr(eng_sched, k)
-    eng_sched = eng.sched
-    eng.sched = S()
-    eng._run_graph, eng._process = run_graph, process
-    ops.sample = sample
-    # host-side pieces not covered above: sampling-parameter packing and the token sync
-    import generativeaiexamples_amd.engine.llm_engine as le
-    orig_sb = le.SamplingBatch
-    acc["sampling_batch"] = 0.0
-
-    def sb(*args, **kw):
-        t = time.perf_counter(); r = orig_sb(*args, **kw); acc["sampling_batch"] += time.perf_counter() - t; return r  # noqa: E702
-    le.SamplingBatch = sb
-    torch.cuda.synchronize()
+    # steady-state decode: wall time per generated token (engine.step() runs `decode_steps` tokens per call)
+    n0 = eng.stats["decode_tokens"]
     t0 = time.perf_counter()
     for _ in range(a.steps):
         eng.step()
     torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / a.steps
-    out = {"model": name, "batch": a.batch, "ctx": a.prompt, "wall_ms_per_step": round(1000 * wall, 3)}
-    out.update({k + ("" if k.endswith("_ms") else "_ms"): round((v if k.endswith("_ms") else 1000 * v) / a.steps, 3)
-                for k, v in acc.items()})
-    # phase attribution with a device sync after each phase (replicates LLMEngine.step for decode)
-    eng.sched = eng_sched
-    eng._run_graph, eng._process = orig_run, orig_process
-    ops.sample = orig_sample
-    le.SamplingBatch = orig_sb
-    ph = {k: 0.0 for k in ("schedule", "replay", "penalize_pack", "sample", "to_host", "process")}
-    n_ph = 20
-    for it in range(2 * n_ph):
-        if it == n_ph:  # second half: same loop under inference_mode (as LLMEngine.step)
-            out["synced_phases_ms"] = {k: round(1000 * v / n_ph, 3) for k, v in ph.items()}
-            ph = {k: 0.0 for k in ph}
-            im = torch.inference_mode()
-            im.__enter__()
-        t = time.perf_counter()
-        b = eng.sched.schedule()
-        eng.stager.reset()
-        nd = len(b.decode_seq_ids)
-        eng.step_count += 1
-        t1 = time.perf_counter(); ph["schedule"] += t1 - t
-        logits = eng._run_graph(b, nd) if not a.no_graphs else eng.model.forward(eng._make_batch(b)[0], eng.kv, eng.decode_ws)
-        torch.cuda.synchronize(); t2 = time.perf_counter(); ph["replay"] += t2 - t1  # noqa: E702
-        seq_order = list(b.decode_seq_ids)
-        reqs = [eng.requests.get(x) for x in seq_order]
-        params = [r.params for r in reqs]
-        eng._penalize(logits, reqs)
-        sbt = le.SamplingBatch(params, [r.seed for r in reqs], eng.device, eng.stager)
-        torch.cuda.synchronize(); t3 = time.perf_counter(); ph["penalize_pack"] += t3 - t2  # noqa: E702
-        toks = ops.sample(logits, sbt.temperature, sbt.top_p, sbt.top_k, sbt.seeds, eng.step_count)
-        torch.cuda.synchronize(); t4 = time.perf_counter(); ph["sample"] += t4 - t3  # noqa: E702
-        toks = toks.cpu().tolist()
-        t5 = time.perf_counter(); ph["to_host"] += t5 - t4  # noqa: E702
-        eng._process(seq_order, reqs, toks)
-        ph["process"] += time.perf_counter() - t5
-    im.__exit__(None, None, None)
-    out["synced_phases_inference_mode_ms"] = {k: round(1000 * v / n_ph, 3) for k, v in ph.items()}
+    wall = time.perf_counter() - t0
+    toks = (eng.stats["decode_tokens"] - n0) / a.batch
+    out = {"model": name, "batch": a.batch, "ctx": a.prompt, "steps": a.steps,
+           "ms_per_token": round(1000 * wall / max(toks, 1), 3), "tokens_per_seq": toks,
+           "graph_steps": eng.stats.get("graph_steps")}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(10):

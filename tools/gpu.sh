@@ -11,6 +11,7 @@
 #   prof  <name> <bench.py args...> rocprofv3 --kernel-trace --stats around bench.py, reduced to <name>_kernels.csv
 #   proftrace <name> <bench.py args...> the same, plus the raw kernel trace as <name>_trace.csv.gz
 #   py    <name> <script args...>   python <script> <args>
+#   pylong <name> <script args...>  the same with an 1100 s step limit
 #   pyprof <name> <script args...>  rocprofv3 --kernel-trace --stats around python3 <script> <args>
 #   smoke                           __graft_entry__.smoke()
 # Leading KEY=VALUE tokens after <name> are exported for that step only, e.g. "bench b2 GAI_X=1 --steps 2".
@@ -65,6 +66,7 @@ for spec in "$@"; do
              > /dev/null || exit $?
            f=$(find "/tmp/prof_$n" -name "*kernel_trace.csv" | head -1); gzip -c "$f" > "$O/${n}_trace.csv.gz" || exit $? ;;
     py)    step 600 "$O/$n.log" python "${rest[@]}" || exit $? ;;
+    pylong) step 1100 "$O/$n.log" python "${rest[@]}" || exit $? ;;  # long runs (1M-chunk ingest)
     pyprof) rm -rf "/tmp/prof_$n"
            step 600 "$O/$n.log" rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/prof_$n" -o run -- \
              python3 "${rest[@]}" || exit $?
