@@ -31,11 +31,23 @@ namespace {
 constexpr int kBS = 16;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNeg = -1e30f;
+constexpr float kRescaleTh = 8.f;  // deferred running-max update of the prefill softmax (log2 domain)
 
 // Raw v_exp_f32 (2^x). exp2f wraps it in a denormal range fix-up (cmp, 2x cndmask, add, ldexp: 6 VALU
 // ops per element); softmax arguments are <= 0, and results below 2^-126 are irrelevant next to the
 // row maximum's 1.0, so the bare instruction is exact enough and 6x cheaper on the VALU.
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max / sum of lane l and lane l ^ 32 in every lane: one v_permlane32_swap (lanes 32-63 of the first operand <->
+// lanes 0-31 of the second) instead of a ds_bpermute round trip through the LDS unit
+__device__ __forceinline__ float max_halves(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_halves(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 // ----------------------------------------------------------------------------------------------
 // Prefill
@@ -112,7 +124,11 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   // every XCD. MI355X (profiles/r3/attn_prefill_xcd): B 4 x S 2048 GQA 32/8 D 128 604 -> 660 TF/s, the headline
   // chunk (7 x 2406) 703 -> 728, Gemma D 256 315 -> 473; 64 x 512 MHA D 64 413 -> 394. GAI_ATTN_XCD=0: off.
   // xcd bits 1-2: wave priority around the MFMA phases (A/B, GAI_ATTN_PRIO): 1 = QK^T at priority 1, 2 = QK^T and P.V
-  const int prio = xcd >> 1;
+  // xcd bit 3: exact running maximum (GAI_ATTN_RESCALE_TH=0). Otherwise the running maximum only moves when a tile
+  // raises it by more than kRescaleTh (log2 units): probabilities then stay <= 2^kRescaleTh (bf16 / fp32 keep their
+  // relative precision) and the O / l rescale almost never runs after the first tiles
+  const float th = (xcd & 8) ? 0.f : kRescaleTh;
+  const int prio = (xcd >> 1) & 3;
   xcd &= 1;
   int bx = blockIdx.x, by = blockIdx.y;
   if (xcd) {
@@ -287,8 +303,8 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
             mt = fmaxf(mt, x);
           }
       }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
-      const float m_new = fmaxf(m_run[0], mt);
+      mt = max_halves(mt) * sl2;
+      const float m_new = mt > m_run[0] + th ? mt : m_run[0];
       const float alpha = fexp2(m_run[0] - m_new);
       if (__any(alpha != 1.f)) {
 #pragma unroll
@@ -321,8 +337,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
         }
       }
       if (prio == 2) __builtin_amdgcn_s_setprio(0);
-      rs += __shfl_xor(rs, 32, 64);
-      l_run[0] = l_run[0] * alpha + rs;
+      l_run[0] = l_run[0] * alpha + rs;  // this lane half's keys; the halves are summed after the loop
       if (more2) write_k_from(kt & 1, stg);
       if (more1) write_v_from((kt + 1) & 1, stv);
 #pragma unroll
@@ -357,10 +372,35 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     if (prio) __builtin_amdgcn_s_setprio(1);
     f32x16 s[HL][2];
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
+    for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int j = 0; j < HL; ++j) s[j][sub] = f32x16{};
-      if constexpr (QL) {
+    if constexpr (QL && D <= 128) {
+      // The first 32-key half's D / 16 K fragments are read together, the second half's one per first-half MFMA:
+      // no MFMA waits on its own LDS round trip (left to the compiler, one fragment register was re-used and
+      // every QK^T MFMA waited lgkmcnt(0) behind its read)
+      constexpr int NT = D / 16;
+      bf16x8 ka[NT], kb[NT];
+      const int key = lane & 31;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ka[t] = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        kb[t] = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(32 + key, 2 * t + h));
+        s[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[t], qf[0][t], s[0][0], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) s[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb[t], qf[0][t], s[0][1], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);  // DS reads: first half
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one second-half read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one first-half MFMA
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);  // second-half MFMAs
+    } else if constexpr (QL) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
         const int key = 32 * sub + (lane & 31);
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) {
@@ -388,7 +428,6 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
       write_k(cur ^ 1);
       load_half(vc);
     }
-    lookup(kt + 2);  // pages past the context resolve to entry 0 (never read unmasked)
     // online softmax (exp2 domain); lane owns query (lane&31), keys split across lane halves.
     // Interior tiles (every key < ctx and, causal, <= the wave's first query position) skip the
     // per-element mask: wave-uniform test, so only the diagonal / tail tiles pay for it.
@@ -422,8 +461,8 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     float m_new[HL], alpha[HL];
 #pragma unroll
     for (int j = 0; j < HL; ++j) {
-      mt[j] = fmaxf(mt[j], __shfl_xor(mt[j], 32, 64)) * sl2;
-      m_new[j] = fmaxf(m_run[j], mt[j]);
+      mt[j] = max_halves(mt[j]) * sl2;
+      m_new[j] = mt[j] > m_run[j] + th ? mt[j] : m_run[j];
       alpha[j] = fexp2(m_run[j] - m_new[j]);
       // lazy rescale: once the running maxima settle (most tiles after the first few) alpha == 1 in
       // every lane and the D/32 x 16 accumulator multiplies are skipped (bit-identical result)
@@ -464,14 +503,17 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     }
     if (prio == 2) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
-    for (int j = 0; j < HL; ++j) {
-      rs[j] += __shfl_xor(rs[j], 32, 64);
-      l_run[j] = l_run[j] * alpha[j] + rs[j];
-    }
+    for (int j = 0; j < HL; ++j) l_run[j] = l_run[j] * alpha[j] + rs[j];  // per lane half (summed after the loop)
+    // the next-but-one tile's page lookups (scalar loads) after the P.V reads: an SMEM load in flight makes every
+    // LDS wait a full lgkmcnt(0) (the two return out of order)
+    lookup(kt + 2);  // pages past the context resolve to entry 0 (never read unmasked)
     if (more) write_v(cur ^ 1);
     __syncthreads();
   }
   }  // one-tile loop
+  // each lane half accumulated the row sum of its own keys (every tile rescaled both by the same alpha)
+#pragma unroll
+  for (int j = 0; j < HL; ++j) l_run[j] = sum_halves(l_run[j]);
 
   if (qrow < qlen) {
 #pragma unroll
@@ -961,7 +1003,8 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   // wave priority 1 while a wave issues its QK^T / P.V MFMAs (0 in the softmax): +1-2 % on every head_dim-64/128 shape
   // (headline chunk 707-714 -> 721 TF/s, profiles/r5/attn_prefill/prio_ab.txt); GAI_ATTN_PRIO = 0 / 1 for A/B
   static const int prio_env = getenv("GAI_ATTN_PRIO") ? atoi(getenv("GAI_ATTN_PRIO")) : 2;
-  const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1);
+  static const bool exact_max = getenv("GAI_ATTN_RESCALE_TH") && atoi(getenv("GAI_ATTN_RESCALE_TH")) == 0;
+  const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1) | (exact_max ? 8 : 0);
   const int hl = prefill_hl(D, ratio);
   if (hl == 2) {  // D == 128, hpw == 4: 64 rows per tile; + the 4 waves' Q images (2 heads x 32 rows each)
     const int lds = 2 * PrefillCfg<128>::BUF + 4 * 2 * 32 * PrefillCfg<128>::KRS;
