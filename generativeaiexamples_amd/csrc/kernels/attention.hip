@@ -348,6 +348,9 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
       sc[1] = sn[1];
     }
   } else {
+  // K and V^T of the next tile staged through two register sets, both written at the end of the iteration (D <= 128,
+  // one head per wave: +16 VGPRs)
+  constexpr bool ESPLIT = HL == 1 && D <= 128;
   if (ntiles > 0) {
     lookup(0);
     load_half(kc);
@@ -364,7 +367,13 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < ntiles;
-    if (more) load_half(kc);
+    // tile kt + 1: K and V^T both loaded here and written at the end of the iteration (a whole iteration of load
+    // latency cover; writing K right after QK^T left the K loads only the QK^T MFMAs to land in)
+    Stage stv[ESPLIT ? Cfg::CH : 1];
+    if (more) {
+      load_half(kc);
+      if constexpr (ESPLIT) load_half_from(vc, nblk, stv);
+    }
     const char* sk = smem + cur * Cfg::BUF;
     const char* sv = sk + Cfg::KBYTES;
 
@@ -424,7 +433,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
       }
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
-    if (more) {  // buffer cur ^ 1 was released by the previous barrier
+    if (!ESPLIT && more) {  // buffer cur ^ 1 was released by the previous barrier
       write_k(cur ^ 1);
       load_half(vc);
     }
@@ -507,7 +516,14 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     // the next-but-one tile's page lookups (scalar loads) after the P.V reads: an SMEM load in flight makes every
     // LDS wait a full lgkmcnt(0) (the two return out of order)
     lookup(kt + 2);  // pages past the context resolve to entry 0 (never read unmasked)
-    if (more) write_v(cur ^ 1);
+    if (more) {
+      if constexpr (ESPLIT) {
+        write_k(cur ^ 1);
+        write_v_from(cur ^ 1, stv);
+      } else {
+        write_v(cur ^ 1);
+      }
+    }
     __syncthreads();
   }
   }  // one-tile loop
