@@ -106,8 +106,10 @@ __device__ __forceinline__ bf16x8 kv_to_bf16(uint2 v, float s) { return fp8x8_to
 // exponentials and P.V MFMAs, so the matrix pipe has independent work while the VALU runs the softmax (the one-tile
 // loop serialised them: 36.5 % MFMA busy, 7.5 VALU per MFMA, profiles/r5 section 10). K runs one tile ahead of V in
 // LDS; the next K and V tiles are staged in two register sets during the iteration.
-template <int D, int HPW, typename KV, int HL = 1, bool PIPE = false>
-__global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill_kernel(
+// NWV = waves per workgroup: 4 (two workgroups per CU) or 8 (one; the row groups of two 4-wave workgroups share each
+// staged K / V^T tile, halving the tile loads and LDS writes per FLOP; head_dim 64 / 128, one head per wave)
+template <int D, int HPW, typename KV, int HL = 1, bool PIPE = false, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, (D > 128 || HL > 1 || NWV == 8) ? 1 : 2) void attn_prefill_kernel(
     const bf16* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ tiles,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int Hq, int Hkv,
@@ -115,7 +117,10 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   using Cfg = PrefillCfg<D>;
   static_assert(HL == 1 || HPW % HL == 0, "a wave's heads come from one workgroup head group");
   constexpr int WPR = HPW / HL;  // waves per row group
-  constexpr int RPW = 4 / WPR;   // row groups per workgroup
+  constexpr int RPW = NWV / WPR;  // row groups per workgroup
+  constexpr int NTH = 64 * NWV;   // threads
+  static_assert(NWV == 4 || (NWV == 8 && HL == 1 && !PIPE && (D == 64 || D == 128)), "8-wave workgroups: D 64 / 128");
+  constexpr int CH = Cfg::CH * 4 / NWV;  // 16-B staging pieces per thread per tile half
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   // xcd: head group = linear workgroup id mod gridDim.y. Workgroups go to the 8 XCDs round-robin by linear id, so
@@ -172,48 +177,48 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
   // One set of staging registers (raw cache bytes: the fp8 conversion happens at the LDS write), used
   // twice per tile: the next tile's K is loaded at the top and written to the free buffer after QK^T,
   // then its V^T is loaded into the same registers and written before the barrier.
-  // Piece c of thread tid (16 B of a tile half) lies in page (c*256 + tid) / 2D of the tile, which is
+  // Piece c of thread tid (16 B of a tile half) lies in page (c*NTH + tid) / 2D of the tile, which is
   // wave-uniform (a wave's 64 pieces never straddle a page): the page's physical block is looked up with a
   // scalar load one tile ahead (nblk), and each load is a buffer load from that block's scalar base at a
   // loop-invariant 32-bit per-lane offset (no per-lane block-table round trip or 64-bit address math in the loop).
   using Stage = typename std::conditional<sizeof(KV) == 1, uint2, bf16x8>::type;
-  Stage stg[Cfg::CH];
+  Stage stg[CH];
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  unsigned voff[Cfg::CH];
+  unsigned voff[CH];
 #pragma unroll
-  for (int c = 0; c < Cfg::CH; ++c) voff[c] = (unsigned)(((c * 256 + tid) % (2 * D)) * 8 * sizeof(KV));
-  int nblk[Cfg::CH];
-  auto lookup_into = [&](int kt, int(&nb)[Cfg::CH]) {
+  for (int c = 0; c < CH; ++c) voff[c] = (unsigned)(((c * NTH + tid) % (2 * D)) * 8 * sizeof(KV));
+  int nblk[CH];
+  auto lookup_into = [&](int kt, int(&nb)[CH]) {
 #pragma unroll
-    for (int c = 0; c < Cfg::CH; ++c) {
-      const int pidx = kt * 4 + (c * 256 + wid_u * 64) / (2 * D);
+    for (int c = 0; c < CH; ++c) {
+      const int pidx = kt * 4 + (c * NTH + wid_u * 64) / (2 * D);
       nb[c] = bt[pidx * kBS < ctx ? pidx : 0];
     }
   };
   auto lookup = [&](int kt) { lookup_into(kt, nblk); };
-  auto load_half_from = [&](const KV* base, const int(&nb)[Cfg::CH], Stage(&dst)[Cfg::CH]) {
+  auto load_half_from = [&](const KV* base, const int(&nb)[CH], Stage(&dst)[CH]) {
 #pragma unroll
-    for (int c = 0; c < Cfg::CH; ++c) {
+    for (int c = 0; c < CH; ++c) {
       // K page is [16][D] contiguous, V^T page [D][16]
       dst[c] = buf_load<Stage>(base + ((size_t)nb[c] * Hkv + g) * (kBS * D), voff[c]);
     }
   };
   auto load_half = [&](const KV* base) { load_half_from(base, nblk, stg); };
-  auto write_k_from = [&](int buf, const Stage(&src)[Cfg::CH]) {
+  auto write_k_from = [&](int buf, const Stage(&src)[CH]) {
     char* sk = smem + buf * Cfg::BUF;
 #pragma unroll
-    for (int c = 0; c < Cfg::CH; ++c) {
-      const int id = c * 256 + tid;
+    for (int c = 0; c < CH; ++c) {
+      const int id = c * NTH + tid;
       const int page = id / (2 * D), w = id % (2 * D);
       const int key = page * 16 + w / Cfg::KU, u = w % Cfg::KU;
       *reinterpret_cast<bf16x8*>(sk + k_lds_off<D>(key, u)) = kv_to_bf16(src[c], k_scale);
     }
   };
-  auto write_v_from = [&](int buf, const Stage(&src)[Cfg::CH]) {
+  auto write_v_from = [&](int buf, const Stage(&src)[CH]) {
     char* sv = smem + buf * Cfg::BUF + Cfg::KBYTES;
 #pragma unroll
-    for (int c = 0; c < Cfg::CH; ++c) {
-      const int id = c * 256 + tid;
+    for (int c = 0; c < CH; ++c) {
+      const int id = c * NTH + tid;
       const int page = id / (2 * D), w = id % (2 * D);
       const int d = w >> 1, half = w & 1;
       const int u8 = 4 * page + 2 * half;
@@ -245,8 +250,8 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     // V^T image). During the iteration V(kt + 1) and K(kt + 2) stream into two register sets; after the MFMAs they
     // are written to V slot (kt + 1) & 1 (last read by P.V(kt - 1)) and K slot kt & 1 (last read by QK^T(kt), which ran
     // in iteration kt - 1); one barrier per iteration.
-    Stage stv[Cfg::CH];
-    int nb_v[Cfg::CH], nb_k[Cfg::CH];
+    Stage stv[CH];
+    int nb_v[CH], nb_k[CH];
     auto qk_part = [&](int kslot, int sub, int t0, int nt, f32x16& acc) {
       const char* skk = smem + kslot * Cfg::BUF;
       const int key = 32 * sub + (lane & 31);
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
       if (more2) write_k_from(kt & 1, stg);
       if (more1) write_v_from((kt + 1) & 1, stv);
 #pragma unroll
-      for (int c = 0; c < Cfg::CH; ++c) nb_v[c] = nb_k[c];
+      for (int c = 0; c < CH; ++c) nb_v[c] = nb_k[c];
       lookup_into(kt + 3, nb_k);  // pages past the context resolve to entry 0 (never read unmasked)
       __syncthreads();
       sc[0] = sn[0];
@@ -369,7 +374,7 @@ __global__ __launch_bounds__(256, (D > 128 || HL > 1) ? 1 : 2) void attn_prefill
     const bool more = kt + 1 < ntiles;
     // tile kt + 1: K and V^T both loaded here and written at the end of the iteration (a whole iteration of load
     // latency cover; writing K right after QK^T left the K loads only the QK^T MFMAs to land in)
-    Stage stv[ESPLIT ? Cfg::CH : 1];
+    Stage stv[ESPLIT ? CH : 1];
     if (more) {
       load_half(kc);
       if constexpr (ESPLIT) load_half_from(vc, nblk, stv);
@@ -1003,6 +1008,45 @@ int prefill_hl(int D, int ratio) {
 
 void gai_attn_prefill_set_hl(int hl) { g_prefill_hl = hl == 2 ? 2 : 1; }
 
+namespace {
+// Waves per workgroup of the one-tile prefill kernel: 8 for head_dim 64 / 128 at >= 4 q heads per kv head (one head
+// per wave: 2 row groups x 4 heads = 64 rows per tile share each staged K / V^T tile), else 4 (GAI_ATTN_WAVES=4 forces
+// it). Same box, interleaved (profiles/r6/attn_prefill/waves_ab_*): headline chunk 7 x 2406 GQA 32/8 782 / 779 ->
+// 796 / 828 TF/s, B 4 x 2048 693 / 689 -> 706 / 696. Not for MHA: the 256-row tiles of one head waste up to 3 of
+// their causal key tiles on the upper row groups (encoder shape, causal: 415 -> 295). The tile list's rows per tile
+// follow it (gai_attn_prefill_rows_per_tile).
+int prefill_waves(int D, int ratio) {
+  static const int env = getenv("GAI_ATTN_WAVES") ? atoi(getenv("GAI_ATTN_WAVES")) : 8;
+  static const int pipe = getenv("GAI_ATTN_PIPE") ? atoi(getenv("GAI_ATTN_PIPE")) : 0;
+  return env == 8 && (D == 64 || D == 128) && ratio >= 4 && prefill_hl(D, ratio) == 1 && pipe != 1 ? 8 : 4;
+}
+
+template <int DD, int HP, typename KV>
+void prefill_launch(const void* q, const void* k_cache, const void* v_cache, const int* block_tables, int max_blocks,
+                    const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out, int Hq, int Hkv,
+                    float scale, int causal, float* lse, float k_scale, float v_scale, int xcd, int q_ld, int nwv,
+                    hipStream_t st) {
+  const int lds = 2 * PrefillCfg<DD>::BUF;
+  if constexpr (DD == 64 || DD == 128) {
+    if (nwv == 8) {
+      auto kern = attn_prefill_kernel<DD, HP, KV, 1, false, 8>;
+      set_max_lds(kern, lds);
+      kern<<<dim3(ntiles, Hq / HP), 512, lds, st>>>((const bf16*)q, (const KV*)k_cache, (const KV*)v_cache,
+                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
+                                                    Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);
+      GAI_LAUNCH_CHECK();
+      return;
+    }
+  }
+  auto kern = attn_prefill_kernel<DD, HP, KV>;
+  set_max_lds(kern, lds);
+  kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const KV*)k_cache, (const KV*)v_cache, block_tables,
+                                                max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq, Hkv, scale, causal,
+                                                lse, k_scale, v_scale, xcd, q_ld);
+  GAI_LAUNCH_CHECK();
+}
+}  // namespace
+
 void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                       int max_blocks, const int* tiles, int ntiles, const int* cu_q, const int* ctx_lens, void* out,
                       int Hq, int Hkv, int D, float scale, int causal, float* lse, int kv_fp8, float k_scale,
@@ -1022,6 +1066,7 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   static const bool exact_max = getenv("GAI_ATTN_RESCALE_TH") && atoi(getenv("GAI_ATTN_RESCALE_TH")) == 0;
   const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1) | (exact_max ? 8 : 0);
   const int hl = prefill_hl(D, ratio);
+  const int nwv = prefill_waves(D, ratio);
   if (hl == 2) {  // D == 128, hpw == 4: 64 rows per tile; + the 4 waves' Q images (2 heads x 32 rows each)
     const int lds = 2 * PrefillCfg<128>::BUF + 4 * 2 * 32 * PrefillCfg<128>::KRS;
     if (kv_fp8) {
@@ -1062,21 +1107,12 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
     return;                                                                                                    \
   }                                                                                                            \
   if (D == DD && hpw == HP) {                                                                                  \
-    const int lds = 2 * PrefillCfg<DD>::BUF;                                                                   \
-    if (kv_fp8) {                                                                                              \
-      auto kern = attn_prefill_kernel<DD, HP, fp8>;                                                            \
-      set_max_lds(kern, lds);                                                                                  \
-      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const fp8*)k_cache, (const fp8*)v_cache,  \
-                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);       \
-    } else {                                                                                                   \
-      auto kern = attn_prefill_kernel<DD, HP, bf16>;                                                           \
-      set_max_lds(kern, lds);                                                                                  \
-      kern<<<dim3(ntiles, Hq / HP), 256, lds, st>>>((const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, \
-                                                    block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, \
-                                                    Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);       \
-    }                                                                                                          \
-    GAI_LAUNCH_CHECK();                                                                                        \
+    if (kv_fp8)                                                                                                \
+      prefill_launch<DD, HP, fp8>(q, k_cache, v_cache, block_tables, max_blocks, tiles, ntiles, cu_q, ctx_lens, \
+                                  out, Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld, nwv, st);     \
+    else                                                                                                       \
+      prefill_launch<DD, HP, bf16>(q, k_cache, v_cache, block_tables, max_blocks, tiles, ntiles, cu_q, ctx_lens, \
+                                   out, Hq, Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld, nwv, st);    \
     return;                                                                                                    \
   }
   GAI_PF(64, 1)
@@ -1098,7 +1134,7 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
 int gai_attn_prefill_rows_per_tile(int Hq, int Hkv, int D) {
   const int ratio = Hq / Hkv;
   const int hpw = ratio >= 4 ? 4 : ratio >= 2 ? 2 : 1;
-  return 32 * (4 / (hpw / prefill_hl(D, ratio)));
+  return 32 * (prefill_waves(D, ratio) / (hpw / prefill_hl(D, ratio)));
 }
 
 void gai_attn_decode(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,

@@ -470,7 +470,8 @@ def prefill_rows_per_tile(Hq: int, Hkv: int, head_dim: int = 128) -> int:
         return int(native().attn_prefill_rows_per_tile(Hq, Hkv, head_dim))
     r = Hq // Hkv
     hpw = 4 if r >= 4 else 2 if r >= 2 else 1
-    return 32 * (4 // hpw)
+    waves = 8 if hpw == 4 and head_dim in (64, 128) and os.environ.get("GAI_ATTN_WAVES", "8") == "8" else 4
+    return 32 * (waves // hpw)
 
 
 def set_prefill_heads_per_wave(hl: int) -> None:
