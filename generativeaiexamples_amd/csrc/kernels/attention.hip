@@ -133,6 +133,7 @@ __global__ __launch_bounds__(64 * NWV, (D > 128 || HL > 1 || NWV == 8) ? 1 : 2) 
   // raises it by more than kRescaleTh (log2 units): probabilities then stay <= 2^kRescaleTh (bf16 / fp32 keep their
   // relative precision) and the O / l rescale almost never runs after the first tiles
   const float th = (xcd & 8) ? 0.f : kRescaleTh;
+  const int xcd_flags = xcd;
   const int prio = (xcd >> 1) & 3;
   xcd &= 1;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -351,6 +352,133 @@ __global__ __launch_bounds__(64 * NWV, (D > 128 || HL > 1 || NWV == 8) ? 1 : 2) 
       __syncthreads();
       sc[0] = sn[0];
       sc[1] = sn[1];
+    }
+  } else if constexpr (NWV == 8) {
+    // Staggered 8-wave loop (MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7 (the second row group, each
+    // the SIMD partner of wave w - 4) run half an iteration behind - their P.V of tile kt - 1, then their QK^T of tile
+    // kt - so on every SIMD one wave's QK^T MFMAs meet the other's softmax VALU and P.V instead of both waves hitting
+    // the matrix pipe, then the VALU, together. Tile j lives in LDS slot j % 3 (3 x 35 KiB): in iteration kt the
+    // waves read slots kt % 3 and (kt - 1) % 3 while tile kt + 1 is written to the third; ntiles + 1 iterations, one
+    // barrier each. The K / V^T of tile kt + 1 are loaded at the top of iteration kt and written at its end.
+    const bool late = wid >= 4 && !(xcd_flags & 16);  // GAI_ATTN_STAGGER=0: every wave in step (A/B)
+    Stage stv[CH];
+    auto slot = [&](int t) { return smem + (t % 3) * Cfg::BUF; };
+    auto qk = [&](const char* sk, f32x16(&sc)[2]) {
+      constexpr int NT = D / 16;
+      bf16x8 ka[NT], kb[NT];
+      const int key = lane & 31;
+      sc[0] = f32x16{};
+      sc[1] = f32x16{};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ka[t] = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(key, 2 * t + h));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        kb[t] = *reinterpret_cast<const bf16x8*>(sk + k_lds_off<D>(32 + key, 2 * t + h));
+        sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[t], qf[0][t], sc[0], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb[t], qf[0][t], sc[1], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+    };
+    // masked row max, deferred running max, O and l rescaled at once (l += the tile's sum after its P.V)
+    auto stats = [&](int kt, f32x16(&sc)[2]) {
+      float mt = kNeg;
+      const int kend = kt * 64 + 63;
+      if (kend < ctx && (!causal || kend <= ctx - qlen + r0)) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sc[sub][r]);
+      } else {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * 64 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool ok = key < ctx && (!causal || key <= qpos);
+            const float x = ok ? sc[sub][r] : kNeg;
+            sc[sub][r] = x;
+            mt = fmaxf(mt, x);
+          }
+      }
+      mt = max_halves(mt) * sl2;
+      const float m_new = mt > m_run[0] + th ? mt : m_run[0];
+      const float alpha = fexp2(m_run[0] - m_new);
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) acc_o[0][i] *= alpha;
+      }
+      l_run[0] *= alpha;
+      m_run[0] = m_new;
+    };
+    auto pv = [&](const char* sv, const f32x16(&sc)[2]) {
+      float rs = 0.f;
+      if (prio == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int sub = st >> 1, sp = st & 1;
+        bf16x8 pf;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float p = fexp2(fmaf(sc[sub][8 * sp + e], sl2, -m_run[0]));
+          rs += p;
+          pf[e] = (bf16)p;
+        }
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + v_lds_off<D>(32 * dt + (lane & 31), 4 * st + h));
+          acc_o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[0][dt], 0, 0, 0);
+        }
+      }
+      if (prio == 2) __builtin_amdgcn_s_setprio(0);
+      l_run[0] += rs;  // per lane half (summed after the loop)
+    };
+    if (ntiles > 0) {
+      lookup(0);
+      load_half(kc);
+      write_k(0);
+      load_half(vc);
+      write_v(0);
+      lookup(1);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the Q fragments and tile 0
+    __syncthreads();
+    f32x16 sc[2];
+    for (int kt = 0; kt <= ntiles; ++kt) {
+      const bool more = kt + 1 < ntiles;
+      if (more) {
+        load_half(kc);
+        load_half_from(vc, nblk, stv);
+      }
+      if (!late) {
+        if (kt < ntiles) {
+          if (prio) __builtin_amdgcn_s_setprio(1);
+          qk(slot(kt), sc);
+          if (prio) __builtin_amdgcn_s_setprio(0);
+          stats(kt, sc);
+          pv(slot(kt) + Cfg::KBYTES, sc);
+        }
+      } else {
+        if (kt > 0) pv(slot(kt - 1) + Cfg::KBYTES, sc);  // tile kt - 1 (its statistics ran last iteration)
+        if (kt < ntiles) {
+          if (prio) __builtin_amdgcn_s_setprio(1);
+          qk(slot(kt), sc);
+          if (prio) __builtin_amdgcn_s_setprio(0);
+          stats(kt, sc);
+        }
+      }
+      lookup(kt + 2);  // after the LDS reads (an SMEM load in flight forces full lgkmcnt waits)
+      if (more) {
+        write_k_from((kt + 1) % 3, stg);
+        write_v_from((kt + 1) % 3, stv);
+      }
+      __syncthreads();
     }
   } else {
   // K and V^T of the next tile staged through two register sets, both written at the end of the iteration (D <= 128,
@@ -1028,10 +1156,10 @@ void prefill_launch(const void* q, const void* k_cache, const void* v_cache, con
                     hipStream_t st) {
   const int lds = 2 * PrefillCfg<DD>::BUF;
   if constexpr (DD == 64 || DD == 128) {
-    if (nwv == 8) {
+    if (nwv == 8) {  // the staggered loop keeps three tile slots
       auto kern = attn_prefill_kernel<DD, HP, KV, 1, false, 8>;
-      set_max_lds(kern, lds);
-      kern<<<dim3(ntiles, Hq / HP), 512, lds, st>>>((const bf16*)q, (const KV*)k_cache, (const KV*)v_cache,
+      set_max_lds(kern, 3 * PrefillCfg<DD>::BUF);
+      kern<<<dim3(ntiles, Hq / HP), 512, 3 * PrefillCfg<DD>::BUF, st>>>((const bf16*)q, (const KV*)k_cache, (const KV*)v_cache,
                                                     block_tables, max_blocks, tiles, cu_q, ctx_lens, (bf16*)out, Hq,
                                                     Hkv, scale, causal, lse, k_scale, v_scale, xcd, q_ld);
       GAI_LAUNCH_CHECK();
@@ -1064,7 +1192,9 @@ void gai_attn_prefill(const void* q, const void* k_cache, const void* v_cache, c
   // (headline chunk 707-714 -> 721 TF/s, profiles/r5/attn_prefill/prio_ab.txt); GAI_ATTN_PRIO = 0 / 1 for A/B
   static const int prio_env = getenv("GAI_ATTN_PRIO") ? atoi(getenv("GAI_ATTN_PRIO")) : 2;
   static const bool exact_max = getenv("GAI_ATTN_RESCALE_TH") && atoi(getenv("GAI_ATTN_RESCALE_TH")) == 0;
-  const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1) | (exact_max ? 8 : 0);
+  static const bool no_stagger = getenv("GAI_ATTN_STAGGER") && atoi(getenv("GAI_ATTN_STAGGER")) == 0;
+  const int xcd = (xcd_env == 2 || (xcd_env == 1 && D >= 128 && causal)) | ((prio_env & 3) << 1) | (exact_max ? 8 : 0) |
+                  (no_stagger ? 16 : 0);
   const int hl = prefill_hl(D, ratio);
   const int nwv = prefill_waves(D, ratio);
   if (hl == 2) {  // D == 128, hpw == 4: 64 rows per tile; + the 4 waves' Q images (2 heads x 32 rows each)
