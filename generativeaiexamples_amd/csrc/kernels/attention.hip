@@ -753,7 +753,7 @@ __device__ __forceinline__ void merge_splits(const float* ws_o, const float* ws_
   }
 }
 
-// NTL: the K / V cache loads are non-temporal (each decode step streams the cache once; keeps it from evicting the
+// NTL: the V^T cache loads are non-temporal (each decode step streams the cache once; keeps it from evicting the
 // L2-resident Q / block tables / split partials)
 // Occupancy: unconstrained, the compiler takes 138 VGPRs + 32 AGPRs (2 workgroups per CU, 512 resident), and two
 // splits per (sequence, kv head) at B = 64 are exactly two rounds. Held to 3 per CU (no spill) with three splits it
@@ -906,8 +906,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
           for (int t = 0; t < D / 32; ++t) {
             const Raw* kp = reinterpret_cast<const Raw*>(kc + pb + (size_t)(key & 15) * D + 32 * t + 8 * gq);
-            if constexpr (NTL) c.k[h][i][t] = __builtin_nontemporal_load(kp);
-            else c.k[h][i][t] = *kp;
+            // K is read with the default policy even under NTL: one load instruction covers 16 key rows x 64 B, so
+            // each 128-B line is requested in two halves by consecutive instructions, and the second half then hits
+            // the line the first one allocated in L2 (B = 64, ctx 2535 graph replay 7.251 / 7.236 -> 7.149 /
+            // 7.169 ms per step, profiles/r6/decode/k_policy_ab); V^T loads cover whole lines and stay non-temporal
+            c.k[h][i][t] = *kp;
           }
         }
         const size_t pbv = gq < 2 ? pb0 : pb1;

@@ -135,6 +135,37 @@ def test_attention_prefill(cuda, D, Hq, Hkv, causal):
     _close(o, o_ref, 2e-2, 2e-2, "prefill")
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (16, 16)])
+def test_attention_prefill_running_max_jumps(cuda, Hq, Hkv):
+    """Score scales that jump by far more than the deferred-max threshold between key tiles (keys 64-255 scaled x8,
+    keys from 448 on x24, so the running max moves by ~2^10 and more mid-row), and a chunked prefill over that prefix:
+    the kernel's deferred running max (rescale only past 2^8) still matches the fp32 reference, with the 8-wave GQA
+    workgroups and the 4-wave MHA ones."""
+    torch.manual_seed(17)
+    D = 128
+    ctx = [700, 333]
+    qlen = [700, 100]
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, cuda, seed=5)
+    kcf = kc.float()
+    for s, n in enumerate(ctx):
+        for pos in range(n):
+            f = 8.0 if 64 <= pos < 256 else 24.0 if pos >= 448 else 1.0
+            b, o = int(bt[s, pos // 16]), pos % 16
+            kcf[b, :, o] *= f
+    kc = kcf.to(torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(int(cu[-1]), Hq, D, device=cuda, dtype=torch.bfloat16)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    for causal in (True, False):
+        ql = qlen if causal else ctx
+        cu_c = torch.tensor([0] + list(torch.tensor(ql).cumsum(0)), dtype=torch.int32)
+        qq = q if causal else torch.randn(int(cu_c[-1]), Hq, D, device=cuda, dtype=torch.bfloat16)
+        o = ops.attention_prefill(qq, kc, vc, bt, cu_c.to(cuda), ctx_t.to(cuda), scale, causal, q_lens=ql)
+        o_ref = ref.attention_prefill(qq.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_c, ctx_t, scale, causal)
+        _close(o, o_ref, 3e-2, 3e-2, f"prefill with running-max jumps, causal={causal}")
+
+
 @pytest.mark.parametrize("L,D,Hq,Hkv", [(2048, 128, 32, 8), (4096, 128, 32, 8), (8192, 128, 32, 8),
                                          (2048, 256, 16, 8), (4096, 256, 8, 4), (8192, 256, 8, 1)])
 def test_attention_prefill_long(cuda, L, D, Hq, Hkv):
