@@ -18,7 +18,9 @@
 // column, so K and V^T are read once per kv head with 16-B / 8-B loads straight to
 // VGPRs (memory-bound decode row of the glds-vs-register table); the 4 waves
 // combine through LDS, splits are merged by attn_decode_reduce.
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "gai_common.h"
 #include "gai_rope.h"
@@ -1117,13 +1119,18 @@ __global__ void attn_decode_reduce_kernel(const float* __restrict__ ws_o, const 
   out[((size_t)seq * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 
+// Raise a kernel's dynamic-LDS limit once per KERNEL (a static flag inside a template over the function type would be
+// shared by every instantiation with the same signature, e.g. all bf16 prefill kernels).
 template <typename F>
 void set_max_lds(F* f, int bytes) {
-  static bool done = false;
-  if (!done) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    done = true;
-  }
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> done;
+  const void* key = reinterpret_cast<const void*>(f);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = done.find(key);
+  if (it != done.end() && it->second >= bytes) return;
+  hipFuncSetAttribute(key, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done[key] = bytes;
 }
 
 // Heads per wave of the prefill kernel (attn_prefill_kernel HL): 2 for head_dim 128 with >= 4 q heads per kv head when
