@@ -906,6 +906,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                    out_v.data_ptr<float>(), out_i.data_ptr<int64_t>(), cur_stream());
   });
   m.def("topk_cap", [](int64_t k) { return gai_topk_cap(k); });
+  // streaming-SDR DSP: complex64 tensors are passed as their float32 [n, 2] views
+  m.def("dsp_fir_complex", [](const Tensor& x, const Tensor& taps, Tensor& y) {
+    check_f32(x, "x");
+    check_f32(taps, "taps");
+    check_f32(y, "y");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == 2 && y.sizes() == x.sizes() && taps.dim() == 1 && x.is_contiguous() &&
+                    y.is_contiguous() && taps.is_contiguous(),
+                "dsp_fir_complex: x / y [n, 2] float32 (complex64 views), taps [T]");
+    gai_dsp_fir_complex(x.data_ptr(), taps.data_ptr<float>(), (int)x.size(0), (int)taps.numel(), y.data_ptr(),
+                        cur_stream());
+  });
+  m.def("dsp_fm_demod", [](const Tensor& x, Tensor& y) {
+    check_f32(x, "x");
+    check_f32(y, "y");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == 2 && y.numel() == std::max<int64_t>(x.size(0) - 1, 0) &&
+                    x.is_contiguous() && y.is_contiguous(),
+                "dsp_fm_demod: x [n, 2] (complex64 view), y [n - 1]");
+    gai_dsp_fm_demod(x.data_ptr(), (int)x.size(0), y.data_ptr<float>(), cur_stream());
+  });
+  m.def("dsp_upfirdn", [](const Tensor& x, const Tensor& taps, int64_t up, int64_t down, int64_t offset, double gain,
+                          Tensor& y) {
+    check_f32(x, "x");
+    check_f32(taps, "taps");
+    check_f32(y, "y");
+    TORCH_CHECK(x.dim() == 1 && taps.dim() == 1 && y.dim() == 1 && x.is_contiguous() && taps.is_contiguous() &&
+                    y.is_contiguous(),
+                "dsp_upfirdn: 1-D contiguous float32 x, taps, y");
+    gai_dsp_upfirdn(x.data_ptr<float>(), (int)x.numel(), taps.data_ptr<float>(), (int)taps.numel(), (int)up,
+                    (int)down, (int)offset, (int)y.numel(), (float)gain, y.data_ptr<float>(), cur_stream());
+  });
   m.def("moe_route", &moe_route);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);

@@ -109,6 +109,11 @@ void gai_apply_penalties(float* logits, int B, long ld, const int* tok_ids, cons
 
 // topk.hip
 int gai_topk_cap(int k);
+// Streaming-SDR DSP (dsp.hip): complex64 FIR with zero initial state, FM discriminator, polyphase rational resampler
+void gai_dsp_fir_complex(const void* x, const float* taps, int n, int ntaps, void* y, hipStream_t st);
+void gai_dsp_fm_demod(const void* x, int n, float* y, hipStream_t st);
+void gai_dsp_upfirdn(const float* x, int n, const float* taps, int ntaps, int up, int down, int offset, int nout,
+                     float gain, float* y, hipStream_t st);
 void gai_topk_merge(const float* vals, const int* idx, int nlists, int nq, int cap, int k, float* out_v, int64_t* out_i,
                     hipStream_t st);
 void gai_sim_topk(const void* Q, const void* X, const float* bias, int nq, int N, int D, int k, float* ws_v,
