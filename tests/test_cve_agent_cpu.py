@@ -1,6 +1,7 @@
 """Event-driven CVE triage community app (reference community/event-driven-rag-cve-analysis): checklist
 parsing, version ordering (PEP 440 / Debian), SBOM and code-search tools, the ReAct loop and the concurrent scan
 engine + /scan service, driven by a scripted LLM on the CPU."""
+import zlib
 import json
 import threading
 import time
@@ -63,7 +64,7 @@ def test_sbom_and_code_tools(tmp_path):
             out = torch.zeros(len(texts), self.dim)
             for i, t in enumerate(texts):
                 for w in t.lower().replace("(", " ").replace(".", " ").split():
-                    out[i, hash(w) % self.dim] += 1
+                    out[i, zlib.crc32(w.encode()) % self.dim] += 1
             return torch.nn.functional.normalize(out + 1e-3, dim=-1)
 
     store = VectorStore("code", HashEmb(), device="cpu")

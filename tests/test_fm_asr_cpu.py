@@ -1,6 +1,7 @@
 """FM-radio streaming RAG app (community/fm_asr; reference community/fm-asr-streaming-rag): the signal chain against
 scipy.signal (the reference runs cupyx.scipy.signal with the same calls), the packet receiver, the speech-pipeline
 plumbing, the transcript accumulator and its time-indexed database, intent-routed answers and the chain server."""
+import zlib
 import datetime as dt
 import json
 import math
@@ -121,7 +122,7 @@ class _HashEmb(Embeddings):
         out = torch.zeros(len(texts), self.dim)
         for i, t in enumerate(texts):
             for w in t.lower().split():
-                out[i, hash(w.strip(".,?")) % self.dim] += 1.0
+                out[i, zlib.crc32(w.strip(".,?").encode()) % self.dim] += 1.0
         return torch.nn.functional.normalize(out + 1e-3, dim=-1)
 
 

@@ -1,4 +1,5 @@
 """BM25 sparse index, reciprocal-rank fusion and the hybrid / ranked_hybrid retrieval pipelines (S7)."""
+import zlib
 import torch
 
 from generativeaiexamples_amd.chain_server.connectors import Embeddings
@@ -32,7 +33,7 @@ class _HashEmb(Embeddings):
         out = torch.zeros(len(texts), self.dim)
         for i, t in enumerate(texts):
             for w in t.lower().split():
-                out[i, hash(w) % self.dim] += 1.0
+                out[i, zlib.crc32(w.encode()) % self.dim] += 1.0
         return torch.nn.functional.normalize(out + 1e-3, dim=-1)
 
 

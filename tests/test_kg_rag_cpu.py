@@ -1,6 +1,7 @@
 """Knowledge-graph RAG community app (reference community/knowledge_graph_rag): triple parsing, the graph
 (k-hop facts, GraphML / CSV interchange), document ingest, text / graph / combined answers and the FastAPI backend,
 driven by a scripted LLM and a hashing embedder on the CPU."""
+import zlib
 import csv
 import json
 import os
@@ -35,7 +36,7 @@ class _HashEmb(Embeddings):
         out = torch.zeros(len(texts), self.dim)
         for i, t in enumerate(texts):
             for w in t.lower().split():
-                out[i, hash(w.strip(".,?")) % self.dim] += 1.0
+                out[i, zlib.crc32(w.strip(".,?").encode()) % self.dim] += 1.0
         return torch.nn.functional.normalize(out + 1e-3, dim=-1)
 
 

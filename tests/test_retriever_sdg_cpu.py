@@ -1,5 +1,6 @@
 """Retriever SDG pipeline: QA parsing, easiness / answerability filters, BEIR export and the IR
 metrics, end to end on CPU with a tiny in-process embedder and a scripted LLM."""
+import zlib
 import json
 import math
 import os
@@ -47,7 +48,7 @@ def _hash_embed(dim=64):
         out = np.zeros((len(texts), dim), np.float32)
         for i, t in enumerate(texts):
             for w in t.lower().split():
-                out[i, hash(w.strip(".,?")) % dim] += 1.0
+                out[i, zlib.crc32(w.strip(".,?").encode()) % dim] += 1.0
         return out / np.maximum(np.linalg.norm(out, axis=1, keepdims=True), 1e-12)
     return fn
 
