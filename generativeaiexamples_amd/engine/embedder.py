@@ -341,6 +341,23 @@ class DynamicBatcher:
             self.cv.notify()
         return f
 
+    def submit_many(self, items) -> List[Future]:
+        """Enqueue several items atomically: an idle worker takes them as ONE batch (e.g. the augmented queries of one
+        multi-query retrieval)."""
+        futs: List[Future] = []
+        with self.cv:
+            if self.stop:
+                raise RuntimeError("batcher closed")
+            for item in items:
+                f: Future = Future()
+                if self.gate is not None:
+                    self.gate.enter()
+                    f.add_done_callback(lambda _f: self.gate.exit())
+                self.q.append((item, f))
+                futs.append(f)
+            self.cv.notify()
+        return futs
+
     def __call__(self, item):
         return self.submit(item).result()
 
