@@ -9,7 +9,9 @@ Config: ``APP_SERVERURL`` / ``APP_SERVERPORT`` / ``APP_MODELNAME`` (same names a
 ``/speech`` is the reference's speech playground (rag_playground/speech): microphone -> streaming ASR into
 the question box, answers read back by TTS, through the pluggable backend of :mod:`.speech`
 (``RIVA_API_URI``; routes ``/api/speech/status``, ``/api/speech/asr`` (WAV in), ``/api/speech/tts``
-(WAV out)).
+(WAV out)). ``/prompt-design`` is the community prompt-design helper (:mod:`.prompt_designer`: per-model system
+prompt, few-shot examples and sampling settings in a YAML file (``PROMPT_DESIGN_CONFIG``), generate / compare models,
+optional retrieved context).
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ STATIC = Path(__file__).parent / "static"
 
 
 def create_app(server_url: str | None = None, model_name: str | None = None,
-               client: ChatClient | None = None, speech=None) -> FastAPI:
+               client: ChatClient | None = None, speech=None, designer=None) -> FastAPI:
     host = server_url or os.environ.get("APP_SERVERURL", "http://localhost")
     port = os.environ.get("APP_SERVERPORT", "8081")
     if server_url is None and ":" not in host.split("//")[-1]:
@@ -146,6 +148,13 @@ def create_app(server_url: str | None = None, model_name: str | None = None,
         from fastapi.responses import Response
 
         return Response(pcm_to_wav(pcm, speech.sample_rate_tts), media_type="audio/wav")
+
+    from .prompt_designer import PromptConfigStore, PromptDesigner, add_routes
+
+    designer = designer if designer is not None else PromptDesigner(
+        PromptConfigStore(os.environ.get("PROMPT_DESIGN_CONFIG")))
+    app.state.designer = designer
+    add_routes(app, designer)
 
     @app.get("/health")
     async def health():
