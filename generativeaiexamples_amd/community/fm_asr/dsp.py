@@ -13,12 +13,15 @@ reduces fs_out / fs_in exactly (2 / 125).
 """
 from __future__ import annotations
 
+import functools
 import math
 from fractions import Fraction
 from typing import Tuple
 
 import numpy as np
 import torch
+
+_CPU_BLOCK = 1 << 18  # CPU fallbacks work in blocks of outputs (bounded temporary memory)
 
 __all__ = ["firwin", "lowpass", "fm_demod", "resample_poly", "rational_factors", "float_to_pcm16", "resample_filter"]
 
@@ -53,16 +56,20 @@ def lowpass(taps, x: torch.Tensor) -> torch.Tensor:
     """Causal FIR of a complex64 burst, zero initial state: y[n] = sum_j taps[j] x[n - j]."""
     if x.dtype != torch.complex64 or x.dim() != 1:
         raise ValueError("lowpass: 1-D complex64 input")
-    h = torch.as_tensor(np.asarray(taps, dtype=np.float32), device=x.device)
+    h = taps.to(x.device, torch.float32) if isinstance(taps, torch.Tensor) else \
+        torch.as_tensor(np.asarray(taps, dtype=np.float32), device=x.device)
     if x.is_cuda:
         y = torch.empty_like(x)
         _native().dsp_fir_complex(torch.view_as_real(x.contiguous()), h.contiguous(), torch.view_as_real(y))
         return y
     xr = torch.view_as_real(x).double()  # [n, 2]
-    T = h.numel()
+    T, n = h.numel(), x.numel()
     xp = torch.nn.functional.pad(xr.t().unsqueeze(1), (T - 1, 0))  # [2, 1, n + T - 1]
-    y = torch.nn.functional.conv1d(xp, h.double().flip(0).view(1, 1, -1)).squeeze(1).t()
-    return torch.view_as_complex(y.float().contiguous())
+    w = h.double().flip(0).view(1, 1, -1)
+    # blocks of _CPU_BLOCK outputs (each reads T - 1 samples of history): bounded im2col memory for long inputs
+    y = torch.cat([torch.nn.functional.conv1d(xp[..., s:s + min(_CPU_BLOCK, n - s) + T - 1], w)
+                   for s in range(0, n, _CPU_BLOCK)], dim=-1) if n else xp[..., :0]
+    return torch.view_as_complex(y.squeeze(1).t().float().contiguous())
 
 
 def fm_demod(x: torch.Tensor) -> torch.Tensor:
@@ -102,6 +109,18 @@ def resample_filter(up: int, down: int, window: str = "hamming") -> Tuple[np.nda
     return np.concatenate([np.zeros(n_pre_pad), h]), n_pre_remove, n_pre_pad
 
 
+_DEVICE_TAPS: dict = {}
+
+
+@functools.lru_cache(maxsize=64)
+def _padded_filter(up: int, down: int, window: str, n: int) -> Tuple[np.ndarray, int, int]:
+    h, pre_remove, _ = resample_filter(up, down, window)
+    n_out = -(-n * up // down)
+    while _upfirdn_len(len(h), n, up, down) < n_out + pre_remove:  # post padding, as scipy does
+        h = np.concatenate([h, np.zeros(1)])
+    return h, pre_remove, n_out
+
+
 def resample_poly(x: torch.Tensor, up: int, down: int, window: str = "hamming", gain: float = 1.0) -> torch.Tensor:
     """Rational resampling of a real signal by up / down (scipy.signal.resample_poly semantics; output length
     ceil(n up / down)), times ``gain``."""
@@ -113,22 +132,34 @@ def resample_poly(x: torch.Tensor, up: int, down: int, window: str = "hamming", 
     if up == down == 1:
         return x * gain if gain != 1.0 else x.clone()
     n = x.numel()
-    h, pre_remove, _ = resample_filter(up, down, window)
-    n_out = -(-n * up // down)
-    while _upfirdn_len(len(h), n, up, down) < n_out + pre_remove:  # post padding, as scipy does
-        h = np.concatenate([h, np.zeros(1)])
-    ht = torch.as_tensor(h.astype(np.float32), device=x.device)
+    h, pre_remove, n_out = _padded_filter(up, down, window, n)
     if x.is_cuda:
+        key = (up, down, window, n, str(x.device))
+        ht = _DEVICE_TAPS.get(key)
+        if ht is None:  # bursts have one size: the filter goes to the device once, not per call
+            ht = _DEVICE_TAPS[key] = torch.as_tensor(h.astype(np.float32), device=x.device)
         y = torch.empty(n_out, dtype=torch.float32, device=x.device)
         _native().dsp_upfirdn(x.contiguous(), ht.contiguous(), up, down, pre_remove, float(gain), y)
         return y
-    # CPU: zero-stuff, full convolution, keep every down-th sample from pre_remove on
-    xu = torch.zeros(n * up, dtype=torch.float64)
-    xu[::up] = x.double()
-    full = torch.nn.functional.conv1d(torch.nn.functional.pad(xu.view(1, 1, -1), (len(h) - 1, len(h) - 1)),
-                                      torch.as_tensor(h).flip(0).view(1, 1, -1)).view(-1)
-    idx = torch.arange(n_out, dtype=torch.long) * down + pre_remove * down
-    return (full[idx] * gain).float()
+    # CPU: only the kept outputs, polyphase - output m sits at t = (m + pre_remove) down of the zero-stuffed
+    # convolution, where only taps i = t mod up + j up meet nonzero input x[(t - t mod up) / up - j]
+    hd = torch.as_tensor(h, dtype=torch.float64)
+    L = -(-len(h) // up)
+    hp = torch.zeros(up, L, dtype=torch.float64)
+    for k in range(up):
+        hk = hd[k::up]
+        hp[k, :hk.numel()] = hk
+    xd = torch.nn.functional.pad(x.double(), (L, L))  # zero history / future
+    j = torch.arange(L)
+    out = torch.empty(n_out, dtype=torch.float64)
+    for s0 in range(0, n_out, _CPU_BLOCK // 8):
+        m = torch.arange(s0, min(n_out, s0 + _CPU_BLOCK // 8))
+        t = (m + pre_remove) * down
+        k = t % up
+        base = (t - k) // up
+        idx = (base[:, None] - j[None, :] + L).clamp_(0, xd.numel() - 1)
+        out[m] = (xd[idx] * hp[k]).sum(1)
+    return (out * gain).float()
 
 
 def float_to_pcm16(x: torch.Tensor) -> torch.Tensor:

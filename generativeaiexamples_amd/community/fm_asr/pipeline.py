@@ -70,11 +70,12 @@ class SignalChain:
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self.taps = dsp.firwin(p.numtaps, p.cutoff, fs=p.sample_rate, window="hamming")
+        self.taps_dev = torch.as_tensor(self.taps.astype("float32"), device=self.device)  # uploaded once
         self.up, self.down = dsp.rational_factors(p.sample_rate, p.sample_rate_out)
 
     def __call__(self, samples: torch.Tensor) -> torch.Tensor:
         x = samples.to(self.device, torch.complex64)
-        y = dsp.lowpass(self.taps, x)
+        y = dsp.lowpass(self.taps_dev, x)
         d = dsp.fm_demod(y)
         return dsp.resample_poly(d, self.up, self.down, window="hamming", gain=self.p.gain)
 
