@@ -69,6 +69,14 @@ class KnowledgeGraph:
             n += self.add_triple(*tr)
         return n
 
+    def merge(self, other: "KnowledgeGraph") -> int:
+        """Add every edge of ``other`` (with its entity types); returns the number of new edges."""
+        n = 0
+        for h, es in other.out.items():
+            for r, t in es:
+                n += self.add_triple(other.names[h], other.types.get(h), r, other.names[t], other.types.get(t))
+        return n
+
     # ---- queries
     def __contains__(self, name: str) -> bool:
         return _key(name) in self.names

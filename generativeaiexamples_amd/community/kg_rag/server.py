@@ -33,6 +33,7 @@ from typing import Callable, Dict, List, Optional
 from fastapi import BackgroundTasks, FastAPI, HTTPException
 from fastapi.responses import JSONResponse, StreamingResponse
 from pydantic import BaseModel
+from starlette.concurrency import iterate_in_threadpool
 
 from ...index.hbm_index import Document
 from .extract import generate_qa_pair, judge_answer, process_documents, sample_documents
@@ -112,7 +113,7 @@ def create_app(llm_factory: Callable[[str], object], store, data_dir: str, model
                 w.writerows([c.page_content] for c in chunks)
             with lock:
                 merged = state["graph"]
-                merged.add_triples(graph.triples())
+                merged.merge(graph)
                 merged.to_csvs(data_dir)
                 merged.write_graphml(graphml)
             state["progress"] = 1.0
@@ -143,10 +144,10 @@ def create_app(llm_factory: Callable[[str], object], store, data_dir: str, model
         return await asyncio.to_thread(rag(req.model_id).chat, req.user_input, req.use_kg)
 
     def _ndjson(rows):
+        # the rows come from blocking model calls: produced in the thread pool, never on the event loop
         async def gen():
-            for row in rows():
+            async for row in iterate_in_threadpool(rows()):
                 yield json.dumps(row) + "\n"
-                await asyncio.sleep(0)
         return StreamingResponse(gen(), media_type="text/event-stream")
 
     @app.post("/create-qa-pairs/")

@@ -215,6 +215,7 @@ def test_server_endpoints(tmp_path):
     # a restarted backend re-reads the GraphML
     app2 = create_app(lambda model_id: _LLM(), store, str(data))
     assert app2.state.kg["graph"].num_edges == 5
+    assert app2.state.kg["graph"].types["alice smith"] == "PERSON"  # entity types survive the merge + GraphML
 
 
 @pytest.mark.parametrize("depth", [0, 1, 3])
