@@ -551,10 +551,12 @@ class DecodeWorkspace:
         768-key splits (2048 WGs = 2.67 waves, a 1/3-empty last wave) 5.04 TB/s; 256-key splits
         4.5 TB/s (per-workgroup prologue / combine not amortised)."""
         if target_wgs is None:
-            # few (sequence, kv head) pairs - a TP shard with one kv head per rank - take one resident wave (2
-            # workgroups per CU): Llama-3-70B TP = 8 rank, B = 64, ctx 2500: 10.63 -> 10.27 ms per decode step
-            # (profiles/r5/tp8_rank); Llama-3-8B at B = 64 (512 pairs) keeps 1024
-            target_wgs = _DECODE_TARGET_WGS if batch * hkv > 64 or hkv > 2 or _DECODE_TARGET_ENV else 512
+            # few (sequence, kv head) pairs - a TP shard with one kv head per rank, or <= 16 sequences at 8 kv heads -
+            # take one resident wave (2 workgroups per CU): Llama-3-70B TP = 8 rank, B = 64, ctx 2500: 10.63 ->
+            # 10.27 ms per decode step (profiles/r5/tp8_rank); Llama-3-8B ctx 2471 graph replay, B = 16: 4.51 ->
+            # 4.36 ms, B = 8: 4.15 -> 3.92 ms (profiles/r6/decode/small_batch_split/); B = 64 (512 pairs) keeps 1024
+            one_wave = batch * hkv <= (64 if hkv <= 2 else _DECODE_ONE_WAVE_PAIRS)
+            target_wgs = 512 if one_wave and not _DECODE_TARGET_ENV else _DECODE_TARGET_WGS
         nsplit = max(1, -(-target_wgs // max(1, batch * hkv)))
         s = -(-max_ctx // nsplit)
         s = (s + 127) // 128 * 128
@@ -576,6 +578,8 @@ class DecodeWorkspace:
 _DECODE_TARGET_ENV = "GAI_DECODE_TARGET_WGS" in os.environ
 _DECODE_TARGET_WGS = int(os.environ.get("GAI_DECODE_TARGET_WGS", "1024"))
 _DECODE_MAX_SPLIT = int(os.environ.get("GAI_DECODE_MAX_SPLIT", "2048"))  # keys per split, upper bound (sweeps)
+# up to this many (sequence, kv head) pairs the split targets one resident wave of workgroups (512) instead of 1024
+_DECODE_ONE_WAVE_PAIRS = int(os.environ.get("GAI_DECODE_ONE_WAVE_PAIRS", "128"))
 _DECODE_ADAPTIVE = os.environ.get("GAI_DECODE_ADAPTIVE", "1") == "1"
 
 
