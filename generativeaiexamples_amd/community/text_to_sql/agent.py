@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import re
 import sqlite3
+import threading
 import uuid
 from typing import Dict, List, Optional, Tuple
 
@@ -49,6 +50,7 @@ class SqlAgent:
         self.llm, self.store, self.dialect = llm, store, dialect
         self.n_examples, self.n_ddl, self.n_docs = n_examples, n_ddl, n_docs
         self.conn: Optional[sqlite3.Connection] = None
+        self.db_lock = threading.Lock()  # one connection shared by request threads: one statement at a time
         self.training: Dict[str, Tuple[str, Document]] = {}
 
     # ---- database
@@ -62,13 +64,16 @@ class SqlAgent:
 
         if self.conn is None:
             raise RuntimeError("connect_to_sqlite first")
-        cur = self.conn.execute(sql)
-        cols = [c[0] for c in cur.description or []]
-        return pd.DataFrame(cur.fetchall(), columns=cols)
+        with self.db_lock:
+            cur = self.conn.execute(sql)
+            cols = [c[0] for c in cur.description or []]
+            rows = cur.fetchall()
+        return pd.DataFrame(rows, columns=cols)
 
     def schema_ddl(self) -> List[str]:
-        rows = self.conn.execute("SELECT sql FROM sqlite_master WHERE sql IS NOT NULL AND type IN ('table', 'view')"
-                                 ).fetchall()
+        with self.db_lock:
+            rows = self.conn.execute("SELECT sql FROM sqlite_master WHERE sql IS NOT NULL AND type IN ('table', 'view')"
+                                     ).fetchall()
         return [r[0] for r in rows]
 
     # ---- training data
