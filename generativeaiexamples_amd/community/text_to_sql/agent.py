@@ -14,6 +14,7 @@ from __future__ import annotations
 import re
 import sqlite3
 import threading
+import time
 import uuid
 from typing import Dict, List, Optional, Tuple
 
@@ -46,8 +47,11 @@ def extract_sql(text: str) -> Optional[str]:
 
 
 class SqlAgent:
-    def __init__(self, llm, store, dialect: str = "SQLite", n_examples: int = 5, n_ddl: int = 6, n_docs: int = 4):
+    def __init__(self, llm, store, dialect: str = "SQLite", n_examples: int = 5, n_ddl: int = 6, n_docs: int = 4,
+                 query_timeout_s: float = 30.0):
         self.llm, self.store, self.dialect = llm, store, dialect
+        self.query_timeout_s = query_timeout_s
+        self._deadline = float("inf")
         self.n_examples, self.n_ddl, self.n_docs = n_examples, n_ddl, n_docs
         self.conn: Optional[sqlite3.Connection] = None
         self.db_lock = threading.Lock()  # one connection shared by request threads: one statement at a time
@@ -58,6 +62,8 @@ class SqlAgent:
         self.conn = sqlite3.connect(path, check_same_thread=False)
         if read_only:
             self.conn.set_authorizer(_authorizer)
+        # a runaway statement (an unbounded recursive CTE, a huge cross join) is interrupted at the deadline
+        self.conn.set_progress_handler(lambda: int(time.monotonic() > self._deadline), 10_000)
 
     def run_sql(self, sql: str):
         import pandas as pd
@@ -65,9 +71,13 @@ class SqlAgent:
         if self.conn is None:
             raise RuntimeError("connect_to_sqlite first")
         with self.db_lock:
-            cur = self.conn.execute(sql)
-            cols = [c[0] for c in cur.description or []]
-            rows = cur.fetchall()
+            self._deadline = time.monotonic() + self.query_timeout_s
+            try:
+                cur = self.conn.execute(sql)
+                cols = [c[0] for c in cur.description or []]
+                rows = cur.fetchall()
+            finally:
+                self._deadline = float("inf")
         return pd.DataFrame(rows, columns=cols)
 
     def schema_ddl(self) -> List[str]:

@@ -90,6 +90,10 @@ def test_sql_agent_read_only(db):
         with pytest.raises(sqlite3.DatabaseError):
             ag.run_sql(stmt)
     assert len(ag.run_sql("SELECT * FROM games")) == 4
+    ag.query_timeout_s = 0.2  # an unbounded recursive CTE is interrupted at the deadline
+    with pytest.raises(sqlite3.OperationalError):
+        ag.run_sql("WITH RECURSIVE n(i) AS (SELECT 1 UNION ALL SELECT i + 1 FROM n) SELECT max(i) FROM n")
+    ag.query_timeout_s = 30.0
 
     class Bad:
         def invoke(self, messages, **kw):
