@@ -489,7 +489,10 @@ int legacy_ks(int M, int N, int K) {
   // 192: Llama-3-8B B = 64 QKV takes 4 K-slices (192 workgroups, half the fp32 partial traffic of 8), O keeps 8
   // (4 would leave 128 workgroups): decode step 7.325 -> 7.226 ms (512: 8 slices for both; 128: 4 for both, 7.294;
   // profiles/r4/decode/decode_nt_split_ab.txt)
-  static const int min_wg = getenv("GAI_SPLITK_LEGACY_MINWG") ? atoi(getenv("GAI_SPLITK_LEGACY_MINWG")) : 192;
+  // M <= 16 (16-row activation slab: less partial traffic per slice) takes twice the workgroups: Llama-3-8B ctx 2471
+  // graph replay B = 8 3.921 -> 3.863 ms, B = 16 4.349 -> 4.309-4.322 ms (profiles/r6/decode/small_batch_split/)
+  static const int env_wg = getenv("GAI_SPLITK_LEGACY_MINWG") ? atoi(getenv("GAI_SPLITK_LEGACY_MINWG")) : 0;
+  const int min_wg = env_wg ? env_wg : (M <= 16 ? 384 : 192);
   int best = units;  // KS = units / d for a divisor d of units
   for (int d = units; d >= 1; --d) {
     if (units % d) continue;
