@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import json
 import re
-from typing import Any, Dict, Optional, Tuple
+from typing import Any, Dict, Tuple
 
 PLOT_WORDS = ("plot", "chart", "graph", "visuali", "histogram", "scatter", "bar chart", "line chart", "trend")
 UNDERSTAND = ("Does the user's request ask for a plot, chart or other visualisation? Reply with one word: yes or no.")

@@ -23,9 +23,9 @@ import os
 import re
 import time
 import uuid
-from typing import Callable, Dict, Iterator, List, Literal, Optional
+from typing import Callable, Iterator, List, Literal, Optional
 
-from fastapi import FastAPI, HTTPException, Request
+from fastapi import FastAPI, HTTPException
 from fastapi.responses import FileResponse, JSONResponse, StreamingResponse
 from pydantic import BaseModel, Field
 from starlette.concurrency import iterate_in_threadpool, run_in_threadpool
