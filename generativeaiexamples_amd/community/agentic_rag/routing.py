@@ -77,7 +77,9 @@ class RoutedRag:
         tok = getattr(getattr(llm, "engine", None), "tokenizer", None)
         self.count = count_tokens or ((lambda s: len(tok.encode(s))) if tok is not None
                                       else (lambda s: max(1, len(s) // 4)))
-        self.pool = ThreadPoolExecutor(max_workers=max(2, len(self.sources)))
+        # several workers per source: concurrent requests (and a source call still running past its timeout) must not
+        # queue the next request's calls behind them, or every later gather would time out too
+        self.pool = ThreadPoolExecutor(max_workers=max(16, 8 * len(self.sources)))
 
     def _ask(self, llm, system: str, user: str, max_tokens: int) -> str:
         r = llm.invoke([{"role": "system", "content": system}, {"role": "user", "content": user}], temperature=0.0,
