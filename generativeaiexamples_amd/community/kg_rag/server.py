@@ -112,10 +112,13 @@ def create_app(llm_factory: Callable[[str], object], store, data_dir: str, model
                 w.writerow(["content"])
                 w.writerows([c.page_content] for c in chunks)
             with lock:
-                merged = state["graph"]
+                # merged into a copy and swapped in: chat requests read the current graph without the lock
+                merged = KnowledgeGraph()
+                merged.merge(state["graph"])
                 merged.merge(graph)
                 merged.to_csvs(data_dir)
                 merged.write_graphml(graphml)
+                state["graph"] = merged
             state["progress"] = 1.0
         except Exception as e:  # noqa: BLE001 - surfaced through /progress/
             state["error"] = str(e)
@@ -255,8 +258,8 @@ def create_app(llm_factory: Callable[[str], object], store, data_dir: str, model
     async def visualization(entity: Optional[str] = None, depth: int = 2, limit: int = 2000):
         g = state["graph"]
         if entity:
-            facts = g.entity_knowledge(entity, depth=depth, both_directions=True)
-            edges = [e for e in g.triples() if f"{e[0]} {e[1]} {e[2]}" in set(facts)]
+            facts = set(g.entity_knowledge(entity, depth=depth, both_directions=True))
+            edges = [e for e in g.triples() if f"{e[0]} {e[1]} {e[2]}" in facts]
         else:
             edges = g.triples()
         edges = edges[:limit]
