@@ -65,10 +65,11 @@ class CVEEngine:
             res.response = [f.result().answer for f in futs]
             if self.summarize and res.checklist:
                 findings = "\n".join(f"- {c}\n  Finding: {r}" for c, r in zip(res.checklist, res.response))
-                res.summary = self.agent_llm.invoke(
+                r = self.agent_llm.invoke(
                     [{"role": "system", "content": SUMMARY_PROMPT},
                      {"role": "user", "content": f"CVE: {cve_info}\n\nChecklist findings:\n{findings}"}],
                     temperature=0.0, max_tokens=200)
+                res.summary = str(getattr(r, "content", r) or "")  # message objects and plain strings alike
         except Exception as e:  # noqa: BLE001 - one bad CVE does not fail the batch
             res.error = f"{type(e).__name__}: {e}"
         res.latency_ms = (time.perf_counter() - t0) * 1e3
