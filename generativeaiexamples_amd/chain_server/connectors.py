@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import json
 import logging
+import threading
 from typing import Any, Dict, Iterator, List, Optional, Sequence
 
 import httpx
@@ -185,6 +186,23 @@ class RemoteEmbeddings(Embeddings):
 
 
 # ------------------------------------------------------------------------------------------ ranking
+_FOREIGN_RANKER_LOCK = threading.Lock()
+
+
+def rerank(ranker, documents: Sequence[Document], query: str, top_n: int) -> List[Document]:
+    """``ranker.compress_documents`` keeping ``top_n`` documents. This framework's rankers take ``top_n`` per call; a
+    foreign (LangChain-style) compressor keeps it as state, so it is set for the call and restored under a lock -
+    one ranker object is shared by every request of a server."""
+    if isinstance(ranker, Ranker):
+        return ranker.compress_documents(documents, query, top_n=top_n)
+    with _FOREIGN_RANKER_LOCK:
+        saved, ranker.top_n = ranker.top_n, top_n
+        try:
+            return ranker.compress_documents(documents, query)
+        finally:
+            ranker.top_n = saved
+
+
 class Ranker:
     def __init__(self, top_n: int = 4):
         self.top_n = top_n
@@ -193,12 +211,14 @@ class Ranker:
         raise NotImplementedError
 
     @tracing.traced("reranker")
-    def compress_documents(self, documents: Sequence[Document], query: str) -> List[Document]:
-        """Reorders documents by relevance, keeps top_n, stores ``relevance_score`` in metadata."""
+    def compress_documents(self, documents: Sequence[Document], query: str,
+                           top_n: Optional[int] = None) -> List[Document]:
+        """Reorders documents by relevance, keeps ``top_n`` (default: the ranker's own), stores ``relevance_score`` in
+        metadata. A per-call ``top_n`` leaves the shared ranker untouched, so concurrent requests can differ."""
         docs = list(documents)
         if not docs:
             return []
-        ranked = self.rank(query, [d.page_content for d in docs])[: self.top_n]
+        ranked = self.rank(query, [d.page_content for d in docs])[: top_n or self.top_n]
         out = []
         for i, s in ranked:
             d = docs[i]

@@ -16,6 +16,7 @@ import re
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
+from ...chain_server.connectors import rerank
 from ...index.hbm_index import Document
 from ...rag.text_splitter import RecursiveCharacterTextSplitter
 from .graph import END, START, StateGraph
@@ -89,11 +90,7 @@ class CorrectiveRag:
         docs = s["documents"]
         if self.ranker is None or not docs:
             return {}
-        saved, self.ranker.top_n = self.ranker.top_n, len(docs)
-        try:
-            return {"documents": self.ranker.compress_documents(docs, s["question"])}
-        finally:
-            self.ranker.top_n = saved
+        return {"documents": rerank(self.ranker, docs, s["question"], len(docs))}
 
     def grade_documents(self, s: dict) -> dict:
         docs = s["documents"]

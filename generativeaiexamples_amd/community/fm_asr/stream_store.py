@@ -18,6 +18,7 @@ import statistics
 import threading
 from typing import Callable, Dict, List, Optional
 
+from ...chain_server.connectors import rerank
 from ...index.hbm_index import Document
 from ...rag.text_splitter import RecursiveCharacterTextSplitter
 
@@ -97,11 +98,7 @@ class StreamRetriever:
             md.setdefault("relevance_score", float(s))
             docs.append(Document(d.page_content, md))
         if self.ranker is not None and docs:
-            top_n, self.ranker.top_n = self.ranker.top_n, len(docs)
-            try:
-                docs = self.ranker.compress_documents(docs, query)
-            finally:
-                self.ranker.top_n = top_n
+            docs = rerank(self.ranker, docs, query, len(docs))
         docs.sort(key=lambda d: -float(d.metadata.get("relevance_score", 0.0)))
         if len(docs) > self.outlier_min_docs:
             docs = drop_outliers(docs)

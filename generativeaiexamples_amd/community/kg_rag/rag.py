@@ -16,6 +16,7 @@ import re
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Tuple
 
+from ...chain_server.connectors import rerank
 from ...index.hbm_index import Document
 from .graph import KnowledgeGraph
 
@@ -75,11 +76,7 @@ class KGRag:
         hits = search(question, max(self.k * 4, self.k) if self.ranker is not None else self.k)
         docs = [Document(d.page_content, dict(d.metadata, relevance_score=float(s))) for d, s in hits]
         if self.ranker is not None and docs:
-            top_n, self.ranker.top_n = self.ranker.top_n, self.k
-            try:
-                docs = self.ranker.compress_documents(docs, question)
-            finally:
-                self.ranker.top_n = top_n
+            docs = rerank(self.ranker, docs, question, self.k)
         return [d.page_content for d in docs[: self.k]]
 
     # ---- answers: (answer, contexts)

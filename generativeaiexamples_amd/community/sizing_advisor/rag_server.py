@@ -30,6 +30,7 @@ from fastapi.responses import FileResponse, JSONResponse, StreamingResponse
 from pydantic import BaseModel, Field
 from starlette.concurrency import iterate_in_threadpool, run_in_threadpool
 
+from ...chain_server.connectors import rerank
 from ...index.hbm_index import Document
 from .store import CollectionManager
 
@@ -157,11 +158,7 @@ class BlueprintRag:
         docs = [Document(d.page_content, dict(d.metadata, relevance_score=float(s))) for d, s in hits]
         k = reranker_top_k or len(docs)
         if use_reranker and self.ranker is not None and docs:
-            top_n, self.ranker.top_n = self.ranker.top_n, k
-            try:
-                docs = self.ranker.compress_documents(docs, query)
-            finally:
-                self.ranker.top_n = top_n
+            docs = rerank(self.ranker, docs, query, k)
         return docs[:k]
 
     def _messages(self, p: Prompt, query: str, docs: List[Document]) -> List[dict]:

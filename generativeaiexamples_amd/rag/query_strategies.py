@@ -14,6 +14,7 @@ import re
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 
+from ..chain_server.connectors import rerank
 from ..index.hbm_index import Document
 
 RELATED_QUESTIONS = (
@@ -115,11 +116,7 @@ def retrieve(strategy: str, llm, store, query: str, k: int = 4, top_n: int = 10,
         queries = [query] + related_questions(llm, query, 3, REPHRASINGS)
     docs = dedupe(batched_search(store, queries, k))
     if ranker is not None and docs and strategy != "plain":
-        saved, ranker.top_n = ranker.top_n, top_n
-        try:
-            docs = ranker.compress_documents(docs, query)  # scored against the ORIGINAL question
-        finally:
-            ranker.top_n = saved
+        docs = rerank(ranker, docs, query, top_n)  # scored against the ORIGINAL question
     return Retrieval(query, queries, docs[:top_n] if strategy != "plain" else docs[:k])
 
 

@@ -102,6 +102,33 @@ def test_reranker_scores_against_original_question(store):
     assert rk.top_n == 3  # restored
 
 
+def test_framework_ranker_takes_top_n_per_call_concurrently():
+    """Concurrent requests with different top_n never see each other's value (the shared ranker is not mutated)."""
+    import threading
+
+    from generativeaiexamples_amd.chain_server.connectors import Ranker, rerank
+    from generativeaiexamples_amd.index.hbm_index import Document
+
+    gate = threading.Barrier(8)
+
+    class Slow(Ranker):
+        def rank(self, query, passages):
+            gate.wait(timeout=10)  # every call is inside compress_documents at once
+            return [(i, 1.0 / (i + 1)) for i in range(len(passages))]
+
+    rk, docs, got = Slow(top_n=4), [Document(f"d{i}", {}) for i in range(10)], {}
+
+    def call(n):
+        got[n] = len(rerank(rk, docs, "q", n))
+
+    ts = [threading.Thread(target=call, args=(n,)) for n in range(1, 9)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert got == {n: n for n in range(1, 9)} and rk.top_n == 4
+
+
 def test_fact_check_and_assistant_turn(store):
     assert qs.parse_fact_check("TRUE. fine").verdict is True
     assert qs.parse_fact_check("**FALSE** the context does not say").verdict is False
