@@ -25,7 +25,7 @@ from pydantic import BaseModel, Field
 from starlette.concurrency import run_in_threadpool
 
 from ...chain_server.multipart import parse_multipart
-from .store import CollectionManager, TaskHandler
+from .store import _NAME, CollectionManager, TaskHandler
 
 DEFAULT_COLLECTION = os.environ.get("COLLECTION_NAME", "multimodal_data")
 
@@ -80,6 +80,8 @@ def create_ingestor_app(manager: CollectionManager, tasks: Optional[TaskHandler]
         data = next((p.data.decode("utf-8", "replace") for p in parts if p.name == "data" and p.filename is None),
                     "{}")
         req = _parse(data)
+        if not _NAME.match(req.collection_name or ""):
+            raise HTTPException(400, f"invalid collection name {req.collection_name!r}")
         files = [p for p in parts if p.name == "documents"]
         if not files:
             raise HTTPException(400, "No files provided for uploading.")

@@ -80,6 +80,8 @@ class CollectionManager:
             if name not in self.stores:
                 if not create:
                     raise KeyError(f"collection {name} does not exist")
+                if not _NAME.match(name or ""):
+                    raise ValueError(f"invalid collection name {name!r}")
                 self.create([name])
             return self.stores[name]
 
@@ -100,6 +102,8 @@ class CollectionManager:
                 "total_documents": len(gone), "documents": [{"document_name": n} for n in gone]}
 
     def save_upload(self, name: str, filename: str, data: bytes) -> str:
+        if not _NAME.match(name or ""):  # the name becomes a directory: never a path
+            raise ValueError(f"invalid collection name {name!r}")
         d = os.path.join(self.upload_dir, name)
         os.makedirs(d, exist_ok=True)
         p = os.path.join(d, os.path.basename(filename))

@@ -3,6 +3,7 @@ ingestion, streaming generate with citations and usage, search, structured MI355
 the test / apply configuration event streams - scripted LLM, hashing embedder, CPU."""
 import zlib
 import json
+import os
 import time
 
 import pytest
@@ -102,6 +103,11 @@ def test_collections_and_documents(servers):
     assert ing.get("/documents", params={"collection_name": "kb"}).json()["documents"] == [
         {"document_name": "mi355x.txt"}]
     assert ing.delete("/collections", params={"collection_names": ["other", "ghost"]}).json()["total_failed"] == 1
+    # a collection name is a directory under the upload dir: path-like names are refused before anything is written
+    r = _upload(ing, ["falcon.txt"], collection_name="../escape")
+    assert r.status_code == 400 and not os.path.exists(os.path.join(mgr.upload_dir, "..", "escape"))
+    with pytest.raises(ValueError):
+        mgr.save_upload("../x", "a.txt", b"")
 
 
 def test_generate_stream_citations_usage(servers):
