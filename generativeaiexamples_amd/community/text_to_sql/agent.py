@@ -41,9 +41,22 @@ def extract_sql(text: str) -> Optional[str]:
     m = re.search(r"\b(WITH|SELECT)\b.*", body, re.S | re.I)
     if not m:
         return None
-    sql = m.group(0).strip()
-    sql = sql.split(";")[0].strip()  # one statement only
+    sql = _first_statement(m.group(0)).strip()
     return sql or None
+
+
+def _first_statement(sql: str) -> str:
+    """Text up to the first ``;`` outside quoted literals / identifiers (one statement; trailing prose dropped)."""
+    quote = None
+    for i, ch in enumerate(sql):
+        if quote:
+            if ch == quote:
+                quote = None
+        elif ch in "'\"`[":
+            quote = "]" if ch == "[" else ch
+        elif ch == ";":
+            return sql[:i]
+    return sql
 
 
 class SqlAgent:

@@ -43,6 +43,9 @@ def test_extract_sql():
     assert extract_sql("Here:\n```sql\nSELECT name FROM games;\nDROP TABLE games;\n```") == "SELECT name FROM games"
     assert extract_sql("WITH t AS (SELECT 1) SELECT * FROM t") == "WITH t AS (SELECT 1) SELECT * FROM t"
     assert extract_sql("I can't help") is None
+    # a ';' inside a literal or quoted identifier does not end the statement
+    assert extract_sql("SELECT * FROM t WHERE a = 'x;y'; DROP TABLE t") == "SELECT * FROM t WHERE a = 'x;y'"
+    assert extract_sql("SELECT 'it''s;' AS \"c;d\" FROM t; trailing prose") == "SELECT 'it''s;' AS \"c;d\" FROM t"
 
 
 def test_sql_agent_train_generate_run(db):
