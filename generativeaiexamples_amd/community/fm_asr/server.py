@@ -13,9 +13,10 @@ import datetime as _dt
 import os
 from typing import Callable, Optional
 
-from fastapi import FastAPI, Request
+from fastapi import FastAPI, HTTPException, Request
 from fastapi.responses import JSONResponse, StreamingResponse
-from pydantic import BaseModel, Field
+from pydantic import BaseModel, Field, ValidationError
+from starlette.concurrency import run_in_threadpool
 
 from .chains import StreamQuery, StreamRagChain
 from .stream_store import StreamRetriever, TextAccumulator, TimestampDatabase
@@ -53,7 +54,8 @@ def create_app(llm_factory: Callable[[], object], accumulator: TextAccumulator, 
 
     @app.post("/storeStreamingText")
     async def store_streaming_text(data: TextEntry):
-        return JSONResponse(accumulator.update(data.source_id, data.transcript))
+        # the accumulator embeds the finished chunks: a blocking model call, kept off the event loop
+        return JSONResponse(await run_in_threadpool(accumulator.update, data.source_id, data.transcript))
 
     async def _generate(cfg: StreamConfig):
         q = StreamQuery(question=cfg.question, use_knowledge_base=cfg.use_knowledge_base,
@@ -66,7 +68,10 @@ def create_app(llm_factory: Callable[[], object], accumulator: TextAccumulator, 
     async def generate_get(request: Request):
         # the reference's client sends the config as a JSON body on GET
         body = await request.body()
-        cfg = StreamConfig.model_validate_json(body) if body else StreamConfig(**dict(request.query_params))
+        try:
+            cfg = StreamConfig.model_validate_json(body) if body else StreamConfig(**dict(request.query_params))
+        except ValidationError as e:
+            raise HTTPException(422, e.errors(include_url=False, include_context=False)) from e
         return await _generate(cfg)
 
     @app.post("/generate")

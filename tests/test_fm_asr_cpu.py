@@ -216,3 +216,4 @@ def test_chain_server_endpoints():
     r = c.post("/generate", json={"question": "hi", "use_knowledge_base": False})
     assert r.text == "ANSWER<hi>"
     assert c.post("/generate", json={"max_docs": 3}).status_code == 422
+    assert c.request("GET", "/generate", content=json.dumps({"max_docs": 3})).status_code == 422
