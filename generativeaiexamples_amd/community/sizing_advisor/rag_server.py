@@ -21,6 +21,7 @@ from __future__ import annotations
 import json
 import os
 import re
+import threading
 import time
 import uuid
 from typing import Callable, Iterator, List, Literal, Optional
@@ -326,6 +327,8 @@ def create_rag_app(llm_factory: Callable[[str], object], manager: CollectionMana
             return JSONResponse({"error": "No GPU detected"}, status_code=404)
         return info
 
+    measure_lock = threading.Lock()
+
     def _events(it: Iterator[dict]):
         return StreamingResponse(iterate_in_threadpool(f"data: {json.dumps(e)}\n\n" for e in it),
                                  media_type="text/event-stream", headers={"Cache-Control": "no-cache"})
@@ -357,12 +360,18 @@ def create_rag_app(llm_factory: Callable[[str], object], manager: CollectionMana
                                                        "and a served benchmark"}
                 return
             n = req.measure_concurrency or min(c.concurrency, plan["max_concurrent_sequences"] or 1)
-            yield {"status": "measuring", "gpu": gpu, "concurrency": n}
+            # a measurement loads the model on this process's GPU: one at a time, never two models side by side
+            if not measure_lock.acquire(blocking=False):
+                yield {"status": "busy", "message": "another configuration is being measured; retry when it ends"}
+                return
             try:
+                yield {"status": "measuring", "gpu": gpu, "concurrency": n}
                 m = measure_fn(c.model, concurrency=n, prompt=c.prompt_tokens, response=c.response_tokens)
             except Exception as e:  # noqa: BLE001
                 yield {"status": "error", "message": "measurement failed", "error": str(e)}
                 return
+            finally:
+                measure_lock.release()
             yield {"status": "done", "measured": m,
                    "estimated": {"tpot_ms": plan["tpot_ms"], "ttft_s_single": plan["ttft_s_single"]}}
 

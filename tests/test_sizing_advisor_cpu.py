@@ -185,6 +185,33 @@ def test_models_gpu_and_configuration_events(servers, tmp_path):
                    ).status_code == 404
 
 
+def test_one_measurement_at_a_time(tmp_path):
+    import threading
+
+    from fastapi.testclient import TestClient
+
+    started, release = threading.Event(), threading.Event()
+
+    def measure(preset, **kw):
+        started.set()
+        release.wait(10)
+        return {"model": preset, **kw}
+
+    app = create_rag_app(lambda model: None, CollectionManager(_HashEmb(), str(tmp_path / "u"), device="cpu"),
+                         measure_fn=measure, detect_fn=lambda: {"gpu_model": "MI355X"})
+    c = TestClient(app)
+    cfg = {"configuration": {"model": "llama3-8b", "concurrency": 4, "prompt_tokens": 128, "response_tokens": 16}}
+    first = {}
+    t = threading.Thread(target=lambda: first.update(r=_sse(c.post("/test-configuration", json=cfg))))
+    t.start()
+    assert started.wait(10)
+    assert _sse(c.post("/test-configuration", json=cfg))[-1]["status"] == "busy"
+    release.set()
+    t.join(10)
+    assert first["r"][-1]["status"] == "done"
+    assert _sse(c.post("/test-configuration", json=cfg))[-1]["status"] == "done"  # the lock was released
+
+
 def test_no_gpu_paths(tmp_path):
     from fastapi.testclient import TestClient
 
