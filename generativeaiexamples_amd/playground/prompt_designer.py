@@ -115,7 +115,7 @@ class PromptDesigner:
                               seed=s.get("seed"))
 
     def compare(self, models: List[str], user_input: str, use_context: bool = False) -> Dict[str, str]:
-        with ThreadPoolExecutor(max_workers=max(1, len(models))) as ex:
+        with ThreadPoolExecutor(max_workers=max(1, min(8, len(models)))) as ex:  # request-sized list: bounded
             futs = {m: ex.submit(lambda m=m: "".join(self.stream(m, user_input, use_context))) for m in models}
             out = {}
             for m, f in futs.items():
