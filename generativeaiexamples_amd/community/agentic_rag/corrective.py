@@ -96,7 +96,7 @@ class CorrectiveRag:
         docs = s["documents"]
         if not docs:
             return {"documents": []}
-        with ThreadPoolExecutor(max_workers=len(docs)) as ex:
+        with ThreadPoolExecutor(max_workers=min(32, len(docs))) as ex:
             grades = list(ex.map(lambda d: _yes(self._ask(
                 GRADE_DOC, f"Log excerpt:\n{d.page_content}\n\nQuestion: {s['question']}")), docs))
         return {"documents": [d for d, ok in zip(docs, grades) if ok]}
