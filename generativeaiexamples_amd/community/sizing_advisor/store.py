@@ -152,8 +152,13 @@ class TaskHandler:
         self.pool = ThreadPoolExecutor(max_workers=workers)
         self.tasks: Dict[str, Future] = {}
 
+    MAX_TASKS = 4096  # finished tasks kept for /status; the oldest finished ones are forgotten first
+
     def submit(self, fn: Callable[[], dict]) -> str:
         tid = str(uuid.uuid4())
+        if len(self.tasks) >= self.MAX_TASKS:
+            for old in [t for t, f in self.tasks.items() if f.done()][: len(self.tasks) - self.MAX_TASKS + 1]:
+                self.tasks.pop(old, None)
         self.tasks[tid] = self.pool.submit(fn)
         return tid
 
