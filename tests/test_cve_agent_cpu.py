@@ -1,10 +1,10 @@
 """Event-driven CVE triage community app (reference community/event-driven-rag-cve-analysis): checklist
 parsing, version ordering (PEP 440 / Debian), SBOM and code-search tools, the ReAct loop and the concurrent scan
 engine + /scan service, driven by a scripted LLM on the CPU."""
-import zlib
 import json
 import threading
 import time
+import zlib
 
 import pytest
 import torch

@@ -1,5 +1,6 @@
 """BM25 sparse index, reciprocal-rank fusion and the hybrid / ranked_hybrid retrieval pipelines (S7)."""
 import zlib
+
 import torch
 
 from generativeaiexamples_amd.chain_server.connectors import Embeddings

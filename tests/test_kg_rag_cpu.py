@@ -1,10 +1,10 @@
 """Knowledge-graph RAG community app (reference community/knowledge_graph_rag): triple parsing, the graph
 (k-hop facts, GraphML / CSV interchange), document ingest, text / graph / combined answers and the FastAPI backend,
 driven by a scripted LLM and a hashing embedder on the CPU."""
-import zlib
 import csv
 import json
 import os
+import zlib
 
 import pandas as pd
 import pytest

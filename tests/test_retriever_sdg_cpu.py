@@ -1,9 +1,9 @@
 """Retriever SDG pipeline: QA parsing, easiness / answerability filters, BEIR export and the IR
 metrics, end to end on CPU with a tiny in-process embedder and a scripted LLM."""
-import zlib
 import json
 import math
 import os
+import zlib
 
 import numpy as np
 import pytest

@@ -1,10 +1,10 @@
 """Sizing advisor on the RAG-Blueprint-2.x API (SURVEY §2.9 vgpu-sizing-advisor): collections / documents / task
 ingestion, streaming generate with citations and usage, search, structured MI355X recommendations, GPU detection and
 the test / apply configuration event streams - scripted LLM, hashing embedder, CPU."""
-import zlib
 import json
 import os
 import time
+import zlib
 
 import pytest
 import torch
