@@ -28,13 +28,30 @@ def _key(name: str) -> str:
     return re.sub(r"\s+", " ", str(name)).strip().lower()
 
 
+_WORD = re.compile(r"\w")
+
+
+def _occurs(k: str, text: str) -> bool:
+    """``k`` occurs in ``text`` with no word character on either side (the regex ``(?<!\\w)k(?!\\w)`` without
+    compiling one pattern per entity)."""
+    i = text.find(k)
+    while i >= 0:
+        j = i + len(k)
+        if (i == 0 or not _WORD.match(text[i - 1])) and (j >= len(text) or not _WORD.match(text[j])):
+            return True
+        i = text.find(k, i + 1)
+    return False
+
+
 class KnowledgeGraph:
     def __init__(self):
         self.names: Dict[str, str] = {}           # key -> display name
         self.types: Dict[str, str] = {}           # key -> entity type
         self.out: Dict[str, List[Tuple[str, str]]] = defaultdict(list)  # key -> [(relation, tail key)]
         self.inc: Dict[str, List[Tuple[str, str]]] = defaultdict(list)  # key -> [(relation, head key)]
+        self.edges: set = set()                   # (head key, relation, tail key): O(1) duplicate check on hubs
         self.lock = threading.Lock()
+        self._first: Optional[Dict[Optional[str], List[str]]] = None  # first word -> keys (find_entities index)
 
     # ---- building
     def _entity(self, name: str, etype: Optional[str]) -> Optional[str]:
@@ -43,6 +60,7 @@ class KnowledgeGraph:
             return None
         if k not in self.names:
             self.names[k] = re.sub(r"\s+", " ", str(name)).strip()
+            self._first = None
         if etype and (k not in self.types or self.types[k] in ("", "Unknown")):
             self.types[k] = str(etype)
         return k
@@ -52,8 +70,9 @@ class KnowledgeGraph:
         with self.lock:
             h, t = self._entity(head, head_type), self._entity(tail, tail_type)
             rel = str(relation).strip()
-            if h is None or t is None or not rel or (rel, t) in self.out[h]:
+            if h is None or t is None or not rel or (h, rel, t) in self.edges:
                 return False
+            self.edges.add((h, rel, t))
             self.out[h].append((rel, t))
             self.inc[t].append((rel, h))
             return True
@@ -91,11 +110,27 @@ class KnowledgeGraph:
     def triples(self) -> List[Tuple[str, str, str]]:
         return [(self.names[h], r, self.names[t]) for h, es in self.out.items() for r, t in es]
 
+    def _first_word_index(self) -> Dict[Optional[str], List[str]]:
+        idx = self._first
+        if idx is None:
+            idx = defaultdict(list)
+            for k in list(self.names):
+                m = re.match(r"\w+", k)
+                idx[m.group(0) if m else None].append(k)
+            self._first = idx
+        return idx
+
     def find_entities(self, text: str) -> List[str]:
-        """Entities whose name occurs in ``text`` (word-bounded, longest first)."""
+        """Entities whose name occurs in ``text`` (word-bounded, longest first). Only the names whose first word is a
+        word of the text are tried (a word-bounded match starts exactly at one of the text's words), so a query costs
+        O(its words), not O(entities)."""
         low = " " + _key(text) + " "
-        hits = [k for k in self.names if len(k) > 1 and re.search(r"(?<![\w])" + re.escape(k) + r"(?![\w])", low)]
-        return [self.names[k] for k in sorted(hits, key=len, reverse=True)]
+        idx = self._first_word_index()
+        cands = set(idx.get(None, ()))
+        for w in set(re.findall(r"\w+", low)):
+            cands.update(idx.get(w, ()))
+        hits = [k for k in cands if len(k) > 1 and _occurs(k, low)]
+        return [self.names[k] for k in sorted(hits, key=lambda k: (-len(k), k))]
 
     def entity_knowledge(self, entity: str, depth: int = 2, both_directions: bool = False) -> List[str]:
         """Facts "head relation tail" within ``depth`` hops of ``entity`` (depth-first from it, each edge once)."""

@@ -100,6 +100,32 @@ def test_graph_entity_knowledge():
     assert g.types["c"] == "METRIC"  # a later untyped mention does not erase the type
 
 
+def test_find_entities_matches_word_bounded_regex():
+    """The first-word index + find() lookup gives exactly the word-bounded regex hits, and sees entities added later."""
+    import random
+    import re
+
+    g = KnowledgeGraph()
+    rnd = random.Random(0)
+    words = [f"w{i}" for i in range(50)]
+    for i in range(300):
+        g.add_triple(" ".join(rnd.sample(words, 2)), "T", "rel", f"ent {i}", "T")
+    g.add_triple("C++", "Lang", "used_by", "u.s. navy", "Org")
+    g.add_triple("(paren) thing", "X", "near", "_under", "X")
+    texts = ["about " + " ".join(rnd.sample(words, 12)) + " and C++ at the u.s. navy, ent 17 and (paren) thing _under",
+             "ent 12x c++x w1w2 the_under ent 3."]
+    for t in texts:
+        low = " " + " ".join(t.split()).lower() + " "
+        want = {g.names[k] for k in g.names if len(k) > 1 and re.search(r"(?<![\w])" + re.escape(k) + r"(?![\w])", low)}
+        got = g.find_entities(t)
+        assert set(got) == want and len(got) == len(want)
+        assert [len(x) for x in got] == sorted((len(x) for x in got), reverse=True)
+    assert "new thing" not in g.find_entities("a new thing")
+    g.add_triple("new thing", "T", "rel", "ent 1", "T")  # the index is rebuilt after a new entity
+    assert "new thing" in g.find_entities("a new thing")
+    assert g.add_triple("new thing", "T", "rel", "ent 1", "T") is False  # duplicate edge
+
+
 def test_graphml_and_csv_roundtrip(tmp_path):
     g = _graph()
     p = str(tmp_path / "kg.graphml")
