@@ -132,7 +132,9 @@ class TabularAutoEncoder:
         for _ in range(epochs):
             self.net.train()
             perm = torch.randperm(n, generator=g, device=self.device)
-            tot = 0.0
+            # the epoch loss is summed on the device and read once per epoch: a host read per batch would stall the
+            # launch-bound loop (512-row batches) on every step
+            tot = torch.zeros((), device=self.device)
             for i in range(0, n, bs):
                 idx = perm[i:i + bs]
                 bn, bb, bc = num[idx], binf[idx], cat[idx]
@@ -141,9 +143,9 @@ class TabularAutoEncoder:
                 opt.zero_grad(set_to_none=True)
                 loss.backward()
                 opt.step()
-                tot += float(loss.detach()) * len(idx)
+                tot += loss.detach() * len(idx)
             sched.step()
-            history.append(tot / n)
+            history.append(float(tot) / n)
         # z-score statistics of each feature's loss over the (clean) training rows
         losses = self.feature_losses(df)
         self.loss_stats = {c: (float(losses[:, j].mean()), float(losses[:, j].std()) or 1.0)
