@@ -125,6 +125,74 @@ class TabularAutoEncoder:
         num, binf, cat = self._encode(df)
         self.net = _Net(len(self.num_cols), len(self.bin_cols), [len(self.cat_maps[c]) + 1 for c in self.cat_cols],
                         self.cfg).to(self.device)
+        n, bs = num.shape[0], self.cfg.batch_size
+        if self.cfg.optimizer == "sgd" and torch.device(self.device).type == "cuda" and n >= 4 * bs:
+            history = self._fit_graphed(num, binf, cat, epochs, g)
+        else:
+            history = self._fit_eager(num, binf, cat, epochs, g)
+        # z-score statistics of each feature's loss over the (clean) training rows
+        losses = self.feature_losses(df)
+        self.loss_stats = {c: (float(losses[:, j].mean()), float(losses[:, j].std()) or 1.0)
+                           for j, c in enumerate(self.feature_names)}
+        if validation_data is not None:
+            self.validation_loss = float(self.feature_losses(validation_data).mean())
+        return history
+
+    def _fit_graphed(self, num, binf, cat, epochs: int, g: torch.Generator) -> List[float]:
+        """SGD with every full 512-row step replayed from one captured HIP graph (the step is ~100 small launches:
+        launch-bound when issued one by one). Same update as ``torch.optim.SGD`` without momentum, p -= lr * grad,
+        with lr a device scalar so the per-epoch decay needs no re-capture; the swap noise draws from the default
+        device generator (graph-safe) instead of ``g``; the last partial batch of an epoch runs eagerly."""
+        from ...utils.graphs import hip_graph_capture
+
+        n, bs, history = num.shape[0], self.cfg.batch_size, []
+        params = [p for p in self.net.parameters() if p.requires_grad]
+        lr = torch.tensor(self.cfg.learning_rate, dtype=torch.float32, device=self.device)
+        s_num, s_bin, s_cat = num[:bs].clone(), binf[:bs].clone(), cat[:bs].clone()
+        s_loss = torch.zeros((), device=self.device)
+
+        def step(bn, bb, bc, gen):
+            out = self.net(self._swap(bn, gen), self._swap(bb, gen), self._swap(bc, gen))
+            loss = self._losses(out, bn, bb, bc).mean()
+            grads = torch.autograd.grad(loss, params)
+            with torch.no_grad():
+                torch._foreach_sub_(params, torch._foreach_mul(grads, lr))
+            return loss.detach()
+
+        self.net.train()
+        graph = None
+        for _ in range(epochs):
+            perm = torch.randperm(n, generator=g, device=self.device)
+            tot = torch.zeros((), device=self.device)
+            full = n // bs
+            for b in range(full):
+                idx = perm[b * bs:(b + 1) * bs]
+                torch.index_select(num, 0, idx, out=s_num)
+                torch.index_select(binf, 0, idx, out=s_bin)
+                torch.index_select(cat, 0, idx, out=s_cat)
+                if graph is None:
+                    # first step: run once on a side stream (allocator / library warm-up - a real training step),
+                    # then capture the same step; replays start with the next batch
+                    side = torch.cuda.Stream(device=self.device)
+                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(side):
+                        s_loss.copy_(step(s_num, s_bin, s_cat, None))
+                    torch.cuda.current_stream(self.device).wait_stream(side)
+                    tot += s_loss * bs
+                    graph = torch.cuda.CUDAGraph()
+                    with hip_graph_capture(graph, side):
+                        s_loss.copy_(step(s_num, s_bin, s_cat, None))
+                    continue
+                graph.replay()
+                tot += s_loss * bs
+            if n % bs:
+                idx = perm[full * bs:]
+                tot += step(num[idx], binf[idx], cat[idx], g) * (n - full * bs)
+            lr.mul_(self.cfg.learning_rate_decay)
+            history.append(float(tot) / n)
+        return history
+
+    def _fit_eager(self, num, binf, cat, epochs: int, g: torch.Generator) -> List[float]:
         opt_cls = {"sgd": torch.optim.SGD, "adam": torch.optim.Adam, "adamw": torch.optim.AdamW}[self.cfg.optimizer]
         opt = opt_cls(self.net.parameters(), lr=self.cfg.learning_rate)
         sched = torch.optim.lr_scheduler.ExponentialLR(opt, gamma=self.cfg.learning_rate_decay)
@@ -146,12 +214,6 @@ class TabularAutoEncoder:
                 tot += loss.detach() * len(idx)
             sched.step()
             history.append(float(tot) / n)
-        # z-score statistics of each feature's loss over the (clean) training rows
-        losses = self.feature_losses(df)
-        self.loss_stats = {c: (float(losses[:, j].mean()), float(losses[:, j].std()) or 1.0)
-                           for j, c in enumerate(self.feature_names)}
-        if validation_data is not None:
-            self.validation_loss = float(self.feature_losses(validation_data).mean())
         return history
 
     @torch.no_grad()
