@@ -205,6 +205,16 @@ def _startup() -> None:
         example()
 
 
+@app.on_event("startup")
+async def _worker_threads() -> None:
+    # every streaming /generate holds a worker thread while it waits for its next token, and retrieval / prompt
+    # building run in worker threads too: with anyio's default of 40, a 64-request burst would queue behind the streams
+    # already running (benchmarks/served.py measured with 256)
+    import anyio
+
+    anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("GAI_SERVER_THREADS", "256"))
+
+
 @app.exception_handler(RequestValidationError)
 async def _validation(request: Request, exc: RequestValidationError) -> JSONResponse:
     return JSONResponse(status_code=422, content={"detail": jsonable_encoder(exc.errors(), exclude={"input", "ctx"})})
