@@ -83,6 +83,13 @@ def create_app(llm_factory: Callable[[str], object], store, data_dir: str, model
                reward_fn: Optional[Callable[[str, str], Optional[Dict[str, float]]]] = None,
                max_workers: int = 8) -> FastAPI:
     app = FastAPI(title="Knowledge-graph RAG")
+
+    @app.on_event("startup")
+    async def _worker_threads():
+        # streamed responses hold a worker thread per waiting stream: anyio's default 40 would queue a burst
+        import anyio
+
+        anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("GAI_SERVER_THREADS", "256"))
     os.makedirs(data_dir, exist_ok=True)
     graphml = os.path.join(data_dir, "knowledge_graph.graphml")
     state = {"graph": KnowledgeGraph.read_graphml(graphml) if os.path.exists(graphml) else KnowledgeGraph(),

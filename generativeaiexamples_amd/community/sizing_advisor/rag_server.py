@@ -281,6 +281,13 @@ def create_rag_app(llm_factory: Callable[[str], object], manager: CollectionMana
     detect_fn = detect_fn or deploy.detect_gpu
     app = FastAPI(title="RAG server (sizing advisor)")
 
+    @app.on_event("startup")
+    async def _worker_threads():
+        # streamed responses hold a worker thread per waiting stream: anyio's default 40 would queue a burst
+        import anyio
+
+        anyio.to_thread.current_default_thread_limiter().total_tokens = int(os.environ.get("GAI_SERVER_THREADS", "256"))
+
     @app.get("/health")
     async def health():
         cols = manager.list()["collections"]
